@@ -1,0 +1,134 @@
+/* sdfnmpc.h -- C ABI of the MI355X-native neural-SDF NMPC evaluator (libsdfnmpc.so).
+ *
+ * Plain pointers and sizes only: no torch types, no C++ types.  Every entry point returns
+ * SDFNMPC_OK (0) or a negative error code and never throws; sdfnmpc_last_error() gives the message
+ * (thread-local).  Device pointers are HIP device pointers on the context's device; work is enqueued
+ * on the context's stream (asynchronous unless stated otherwise).
+ *
+ * Which reference interface each entry point replaces (paths relative to the reference checkout):
+ *
+ *   sdfnmpc_net_load / _load_file      torch.jit.load(sdf weights) + .to(device) + .eval()
+ *                                      (sdf_nmpc/gen_model.py:32-34); weights as a packed .sdfw blob
+ *   sdfnmpc_net_siren                  NeuralDF(...) + init_linear_layer_sine (df_train.py:109-110,
+ *                                      layer_init.py:15-25) with a counter-based PRNG
+ *   sdfnmpc_sdf_eval                   NeuralDF.forward (network/neural_df.py:91-103) + autograd
+ *                                      d df / d input, batched over rows -- what L4CasADi's
+ *                                      sdf_l4c / jac_sdf_l4c compute one row at a time
+ *                                      (gen_model.py:39,60)
+ *   sdfnmpc_linearize                  the per-node evaluations acados performs in the SQP-RTI
+ *                                      preparation phase of Ocp.solve (ocp.py:159-170, rti_phase 0):
+ *                                      ERK4 + forward sensitivities (ocp.py:106), NONLINEAR_LS residual
+ *                                      and Jacobian (model/quad_rollpitchyawrate.py:370-377), and the
+ *                                      constraint vector h = [hfov, vfov, sdf] with its Jacobian
+ *                                      (model/cost_const_helpers.py:48-75, gen_model.py:46-70)
+ *   sdfnmpc_shooting_grid              Ocp.__init__ shooting nodes / time steps (ocp.py:18-27)
+ *
+ * The CasADi external-function symbols that acados links (sdf_l4c, jac_sdf_l4c, ...) are in
+ * sdf_l4c.h / libsdf_l4c.so.
+ */
+#ifndef SDFNMPC_H
+#define SDFNMPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SDFNMPC_ABI_VERSION 1
+
+enum {
+    SDFNMPC_OK = 0,
+    SDFNMPC_E_ARG = -1,          /* invalid argument / shape */
+    SDFNMPC_E_HIP = -2,          /* HIP runtime error (message has the HIP error string) */
+    SDFNMPC_E_FORMAT = -3,       /* malformed weight blob */
+    SDFNMPC_E_UNSUPPORTED = -4,  /* network architecture / model option not built for */
+    SDFNMPC_E_NODEVICE = -5      /* no HIP device visible */
+};
+
+typedef struct sdfnmpc_ctx sdfnmpc_ctx;
+typedef struct sdfnmpc_net sdfnmpc_net;
+
+/* 'att' model constants (model/quad_rollpitchyawrate.py; config robot.limits / sensor / mpc) */
+typedef struct {
+    double gamma, roll, pitch, wz; /* robot.limits.{gamma, roll, pitch, wz}: u -> physical inputs */
+    double g;                      /* gravity, 9.81 (model/base_model.py:10) */
+    double B_p_C[3];               /* sensor.B_p_C (utils/config.py:43) */
+    double B_R_C[9];               /* sensor.B_R_C, row-major (utils/config.py:44) */
+    double fov_const_offset;       /* mpc.fov_const_offset (cost_const_helpers.py:452) */
+} sdfnmpc_quad_model;
+
+/* Batched preparation phase: B instances x (N+1) shooting nodes, fp64, row-major C arrays.
+ * Jacobian blocks are column-major (column j contiguous), j over (x[0..9], u[0..3]). */
+typedef struct {
+    int B, N;         /* instances, horizon */
+    int np;           /* parameters per node, >= 17 + 128 (p layout: default.yaml mpc.p_idx) */
+    int latent_mode;  /* 0: latent shared per instance (node 0's, as Nmpc.set_latent writes all
+                         rows, controller.py:50-54); 1: latent read per node */
+    const double* x;  /* [B][N+1][10] current iterate */
+    const double* u;  /* [B][N][4] */
+    const double* p;  /* [B][N+1][np] stage parameters (Ocp.solve p[k], ocp.py:165,168) */
+    const double* dt; /* [N] time steps (sdfnmpc_shooting_grid) */
+    double* xn;       /* [B][N][10]      x_{k+1} = RK4(x_k, u_k, dt_k) */
+    double* AB;       /* [B][N][14][10]  [A_k | B_k] column-major */
+    double* y;        /* [B][N][11]      NONLINEAR_LS residual */
+    double* Jy;       /* [B][N][14][11]  column-major */
+    double* yN;       /* [B][4]          terminal residual */
+    double* JyN;      /* [B][10][4]      column-major */
+    double* h;        /* [B][N+1][3]     [hfov, vfov, sdf] */
+    double* Jh;       /* [B][N+1][10][3] column-major, d h / d x (d h / d u == 0) */
+    float* sdf;       /* [B][N+1][4]     optional: (df, d df / d Co_p_B); NULL = internal buffer */
+} sdfnmpc_lin_args;
+
+int sdfnmpc_abi_version(void);
+const char* sdfnmpc_last_error(void);
+
+/* ---- context: one device + one stream (+ workspaces, kernel timing) ---- */
+int sdfnmpc_ctx_create(int device, void* hip_stream /* NULL: create a non-blocking stream */, sdfnmpc_ctx** out);
+void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx);
+int sdfnmpc_ctx_set_stream(sdfnmpc_ctx* ctx, void* hip_stream);
+void* sdfnmpc_ctx_stream(sdfnmpc_ctx* ctx);
+int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx);
+/* rows per SDF workgroup: 32 (2 workgroups / CU) or 64 (1 workgroup / CU); default 32 */
+int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows);
+/* per-kernel HIP-event timing on the context stream (off by default) */
+int sdfnmpc_ctx_enable_timing(sdfnmpc_ctx* ctx, int on);
+/* kernel: "sdf_mlp", "sdf_hoist", "prep_rows", "linearize"; synchronizes the stream */
+int sdfnmpc_ctx_kernel_stats(sdfnmpc_ctx* ctx, const char* kernel, double* total_ms, long long* launches);
+int sdfnmpc_ctx_reset_stats(sdfnmpc_ctx* ctx);
+
+/* ---- network ---- */
+int sdfnmpc_net_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes, sdfnmpc_net** out);
+int sdfnmpc_net_load_file(sdfnmpc_ctx* ctx, const char* path, sdfnmpc_net** out);
+int sdfnmpc_net_siren(sdfnmpc_ctx* ctx, uint64_t seed, float weight_gain, float bias_gain, sdfnmpc_net** out);
+void sdfnmpc_net_free(sdfnmpc_net* net);
+float sdfnmpc_net_max_df(const sdfnmpc_net* net);
+int sdfnmpc_net_size_latent(const sdfnmpc_net* net);
+/* FNV-1a of the fp32 parameters in torch order (identity check across ranks / files) */
+uint64_t sdfnmpc_net_fingerprint(const sdfnmpc_net* net);
+
+/* ---- SDF evaluation, device pointers ----
+ * pos4[rows][4] = (Co_p_B, unused); latent[n_inst][128] fp32 with row r -> instance r / rows_per_inst;
+ * out4[rows][4] = (df, d df / d pos); grad_latent[rows][128] optional (NULL to skip). */
+int sdfnmpc_sdf_eval(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, const float* pos4,
+                     const float* latent, int rows_per_inst, float* out4, float* grad_latent);
+
+/* ---- SDF evaluation, host pointers, synchronous (the CasADi external path) ----
+ * in[rows][3+128] doubles (the L4CasADi input vertcat(Co_p_B, latent), gen_model.py:60) ->
+ * df[rows], grad[rows][3+128] (optional). Computed in fp32 on the device, returned as fp64. */
+int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const double* in, double* df,
+                          double* grad);
+
+/* ---- batched preparation phase ---- */
+int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* model,
+                      const sdfnmpc_lin_args* args);
+
+/* ---- shooting grid (host, bit-exact numpy.linspace/diff semantics of ocp.py:21-27) ---- */
+int sdfnmpc_shooting_grid(int N, double T, int uniform, int nb_short_nodes, double dt_short, double* nodes,
+                          double* dt);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SDFNMPC_H */

@@ -1,0 +1,159 @@
+"""ctypes front-end of the C oracle (oracle.c).  TEST INFRASTRUCTURE ONLY.
+
+Importable by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg -- as the checker /
+the timed CPU baseline, never as a product path.  ``build()`` compiles ``_build/liboracle.so`` with
+the Makefile next to this file.
+"""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "_build", "liboracle.so")
+
+
+class Spec(C.Structure):
+    _fields_ = [("L", C.c_int), ("n1", C.c_int), ("n2", C.c_int), ("n3", C.c_int), ("n4", C.c_int),
+                ("nf", C.c_int), ("nd", C.c_int), ("w0", C.c_float), ("max_df", C.c_float)]
+
+
+class Quad(C.Structure):
+    _fields_ = [("gamma", C.c_double), ("roll", C.c_double), ("pitch", C.c_double), ("wz", C.c_double),
+                ("g", C.c_double), ("B_p_C", C.c_double * 3), ("B_R_C", C.c_double * 9),
+                ("fov_offset", C.c_double), ("max_df", C.c_double)]
+
+
+def build(force=False):
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
+            os.path.getmtime(os.path.join(HERE, f)) for f in ("oracle.c", "sdf_net.inc", "Makefile")):
+        subprocess.run(["make", "-s", "-C", HERE], check=True)
+    return LIB
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = C.CDLL(LIB)
+        P = C.POINTER
+        f, d, i64 = C.c_float, C.c_double, C.c_int64
+        _lib.orc_prng_uniform.argtypes = [C.c_uint64, C.c_uint64, i64, P(d)]
+        _lib.orc_sdf_f32.argtypes = [P(Spec), P(f), P(f), P(f), i64, P(f), P(f), P(f), P(f), C.c_int]
+        _lib.orc_sdf_f64.argtypes = [P(Spec), P(f), P(f), P(f), i64, P(d), P(d), P(d), P(d)]
+        _lib.orc_quad_rk4.argtypes = [P(Quad), P(d), P(d), d, P(d), P(d)]
+        _lib.orc_quad_cost.argtypes = [P(Quad), P(d), P(d), P(d), P(d), P(d), P(d), P(d)]
+        _lib.orc_quad_constr.argtypes = [P(Quad), P(d), P(d), d, P(d), P(d), P(d), P(d)]
+        _lib.orc_shooting_grid.argtypes = [C.c_int, d, C.c_int, C.c_int, d, P(d), P(d)]
+        _lib.orc_linearize_batch.argtypes = [P(Quad), P(Spec), P(f), P(f), P(f), C.c_int, C.c_int, C.c_int,
+                                             P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d),
+                                             P(d), P(d), P(f), C.c_int]
+        _lib.orc_max_threads.restype = C.c_int
+    return _lib
+
+
+def _p(a, t):
+    return None if a is None else a.ctypes.data_as(C.POINTER(t))
+
+
+class Net:
+    """A network held as flat fp32 params in torch order (weights.param_shapes)."""
+
+    def __init__(self, spec, params):
+        from sdf_nmpc_amd import weights as W
+        self.spec = spec
+        self.flat = np.ascontiguousarray(np.concatenate([params[k].ravel() for k, _ in spec.param_shapes()]),
+                                         dtype=np.float32)
+        self.dirs = np.ascontiguousarray(W.embedding_dirs(spec.embed), dtype=np.float32)
+        self.freqs = (2.0 ** np.arange(spec.nb_freqs)).astype(np.float32)
+        n1, n2, n3, n4 = spec.layer_sizes
+        self.cs = Spec(spec.size_latent, n1, n2, n3, n4, spec.nb_freqs, self.dirs.shape[1], spec.w0, spec.max_df)
+
+    def f32(self, inp, nthreads=1, full_grad=True):
+        inp = np.ascontiguousarray(inp, dtype=np.float32)
+        n = inp.shape[0]
+        df = np.empty(n, np.float32)
+        g = np.empty_like(inp) if full_grad else None
+        gp = np.empty((n, 3), np.float32)
+        lib().orc_sdf_f32(C.byref(self.cs), _p(self.dirs, C.c_float), _p(self.freqs, C.c_float),
+                          _p(self.flat, C.c_float), n, _p(inp, C.c_float), _p(df, C.c_float),
+                          _p(g, C.c_float), _p(gp, C.c_float), nthreads)
+        return df, gp, g
+
+    def f64(self, inp):
+        inp = np.ascontiguousarray(inp, dtype=np.float64)
+        n = inp.shape[0]
+        df = np.empty(n)
+        g = np.empty_like(inp)
+        gp = np.empty((n, 3))
+        lib().orc_sdf_f64(C.byref(self.cs), _p(self.dirs, C.c_float), _p(self.freqs, C.c_float),
+                          _p(self.flat, C.c_float), n, _p(inp, C.c_double), _p(df, C.c_double),
+                          _p(g, C.c_double), _p(gp, C.c_double))
+        return df, gp, g
+
+
+def quad_model(cfg, max_df=1.0):
+    L = cfg.robot.limits
+    R = np.asarray(cfg.sensor.B_R_C, dtype=np.float64).ravel()
+    return Quad(L.gamma, L.roll, L.pitch, L.wz, 9.81, (C.c_double * 3)(*cfg.sensor.B_p_C),
+                (C.c_double * 9)(*R), cfg.mpc.fov_const_offset, max_df)
+
+
+def rk4(m, x, u, dt):
+    x = np.ascontiguousarray(x, np.float64); u = np.ascontiguousarray(u, np.float64)
+    xn = np.empty(10); AB = np.empty((14, 10))
+    lib().orc_quad_rk4(C.byref(m), _p(x, C.c_double), _p(u, C.c_double), dt, _p(xn, C.c_double), _p(AB, C.c_double))
+    return xn, AB.T.copy()  # AB.T: [10][14]
+
+
+def cost(m, x, u, p):
+    x = np.ascontiguousarray(x, np.float64); u = np.ascontiguousarray(u, np.float64)
+    p = np.ascontiguousarray(p, np.float64)
+    y = np.empty(11); Jy = np.empty((14, 11)); yN = np.empty(4); JyN = np.empty((10, 4))
+    lib().orc_quad_cost(C.byref(m), _p(x, C.c_double), _p(u, C.c_double), _p(p, C.c_double), _p(y, C.c_double),
+                        _p(Jy, C.c_double), _p(yN, C.c_double), _p(JyN, C.c_double))
+    return y, Jy.T.copy(), yN, JyN.T.copy()
+
+
+def constr(m, x, p, df, gdf):
+    x = np.ascontiguousarray(x, np.float64); p = np.ascontiguousarray(p, np.float64)
+    g = np.ascontiguousarray(gdf, np.float64)
+    h = np.empty(3); Jh = np.empty((10, 3)); cpb = np.empty(3)
+    lib().orc_quad_constr(C.byref(m), _p(x, C.c_double), _p(p, C.c_double), float(df), _p(g, C.c_double),
+                          _p(h, C.c_double), _p(Jh, C.c_double), _p(cpb, C.c_double))
+    return h, Jh.T.copy(), cpb
+
+
+def shooting_grid(N, T, uniform=True, n_short=2, dt_short=0.01):
+    nodes = np.empty(N + 1); dt = np.empty(N)
+    rc = lib().orc_shooting_grid(N, T, int(uniform), n_short, dt_short, _p(nodes, C.c_double), _p(dt, C.c_double))
+    if rc != 0:
+        raise ValueError("bad grid arguments")
+    return nodes, dt
+
+
+def prng_uniform(seed, stream, n):
+    out = np.empty(n)
+    lib().orc_prng_uniform(seed, stream, n, _p(out, C.c_double))
+    return out
+
+
+def linearize_batch(m, net, x, u, p, dt, nthreads=1):
+    """Whole preparation phase on the CPU; layouts match include/sdfnmpc.h outputs."""
+    B, N1, _ = x.shape
+    N = N1 - 1
+    x = np.ascontiguousarray(x, np.float64); u = np.ascontiguousarray(u, np.float64)
+    p = np.ascontiguousarray(p, np.float64); dt = np.ascontiguousarray(dt, np.float64)
+    out = dict(xn=np.empty((B, N, 10)), AB=np.empty((B, N, 14, 10)), y=np.empty((B, N, 11)),
+               Jy=np.empty((B, N, 14, 11)), yN=np.empty((B, 4)), JyN=np.empty((B, 10, 4)),
+               h=np.empty((B, N1, 3)), Jh=np.empty((B, N1, 10, 3)), sdf=np.empty((B, N1, 4), np.float32))
+    lib().orc_linearize_batch(C.byref(m), C.byref(net.cs), _p(net.dirs, C.c_float), _p(net.freqs, C.c_float),
+                              _p(net.flat, C.c_float), B, N, p.shape[-1], _p(x, C.c_double), _p(u, C.c_double),
+                              _p(p, C.c_double), _p(dt, C.c_double), *(_p(out[k], C.c_double) for k in
+                              ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh")), _p(out["sdf"], C.c_float), nthreads)
+    return out

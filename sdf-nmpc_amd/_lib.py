@@ -1,0 +1,242 @@
+"""ctypes binding of libsdfnmpc.so (include/sdfnmpc.h).
+
+This is the only way Python reaches the hot path: every compute call goes through the C ABI into
+the HIP kernels.  There is deliberately no CPU fallback -- if the library is missing, or no gfx950
+device is visible, construction raises.
+
+Device buffers are plain device pointers (ints).  Callers normally pass torch CUDA(HIP) tensors,
+which are used for allocation and streams only (``tensor.data_ptr()``).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_DIR = os.path.join(PKG_DIR, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libsdfnmpc.so")
+L4C_PATH = os.path.join(LIB_DIR, "libsdf_l4c.so")
+
+# exported symbols declared in include/sdfnmpc.h (checked by tests/test_abi.py)
+SYMBOLS = [
+    "sdfnmpc_abi_version", "sdfnmpc_last_error", "sdfnmpc_ctx_create", "sdfnmpc_ctx_destroy",
+    "sdfnmpc_ctx_set_stream", "sdfnmpc_ctx_stream", "sdfnmpc_ctx_synchronize", "sdfnmpc_ctx_set_tile_rows",
+    "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
+    "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
+    "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
+    "sdfnmpc_linearize", "sdfnmpc_shooting_grid",
+]
+L4C_SYMBOLS = [
+    f"{p}sdf_l4c{s}" for p in ("", "jac_", "adj1_")
+    for s in ("", "_n_in", "_n_out", "_sparsity_in", "_sparsity_out", "_work")
+] + ["sdf_l4c_name_in", "sdf_l4c_name_out", "sdf_l4c_checkout", "sdf_l4c_release", "sdf_l4c_incref",
+     "sdf_l4c_decref", "sdf_l4c_configure", "sdf_l4c_last_error"]
+
+
+class SdfnmpcError(RuntimeError):
+    pass
+
+
+class QuadModelC(C.Structure):
+    _fields_ = [("gamma", C.c_double), ("roll", C.c_double), ("pitch", C.c_double), ("wz", C.c_double),
+                ("g", C.c_double), ("B_p_C", C.c_double * 3), ("B_R_C", C.c_double * 9),
+                ("fov_const_offset", C.c_double)]
+
+
+class LinArgsC(C.Structure):
+    _fields_ = [("B", C.c_int), ("N", C.c_int), ("np", C.c_int), ("latent_mode", C.c_int)] + [
+        (n, C.c_void_p) for n in ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "sdf")]
+
+
+_lib = None
+
+
+def load():
+    """Load libsdfnmpc.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SdfnmpcError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'` "
+                           "(the HIP extension is the only compute path)")
+    lib = C.CDLL(LIB_PATH)
+    vp, i, f, d, ll, sz = C.c_void_p, C.c_int, C.c_float, C.c_double, C.c_longlong, C.c_size_t
+    P = C.POINTER
+    sig = {
+        "sdfnmpc_abi_version": (i, []),
+        "sdfnmpc_last_error": (C.c_char_p, []),
+        "sdfnmpc_ctx_create": (i, [i, vp, P(vp)]),
+        "sdfnmpc_ctx_destroy": (None, [vp]),
+        "sdfnmpc_ctx_set_stream": (i, [vp, vp]),
+        "sdfnmpc_ctx_stream": (vp, [vp]),
+        "sdfnmpc_ctx_synchronize": (i, [vp]),
+        "sdfnmpc_ctx_set_tile_rows": (i, [vp, i]),
+        "sdfnmpc_ctx_enable_timing": (i, [vp, i]),
+        "sdfnmpc_ctx_kernel_stats": (i, [vp, C.c_char_p, P(d), P(ll)]),
+        "sdfnmpc_ctx_reset_stats": (i, [vp]),
+        "sdfnmpc_net_load": (i, [vp, vp, sz, P(vp)]),
+        "sdfnmpc_net_load_file": (i, [vp, C.c_char_p, P(vp)]),
+        "sdfnmpc_net_siren": (i, [vp, C.c_uint64, f, f, P(vp)]),
+        "sdfnmpc_net_free": (None, [vp]),
+        "sdfnmpc_net_max_df": (f, [vp]),
+        "sdfnmpc_net_size_latent": (i, [vp]),
+        "sdfnmpc_net_fingerprint": (C.c_uint64, [vp]),
+        "sdfnmpc_sdf_eval": (i, [vp, vp, ll, vp, vp, i, vp, vp]),
+        "sdfnmpc_sdf_eval_host": (i, [vp, vp, i, P(d), P(d), P(d)]),
+        "sdfnmpc_linearize": (i, [vp, vp, P(QuadModelC), P(LinArgsC)]),
+        "sdfnmpc_shooting_grid": (i, [i, d, i, i, d, P(d), P(d)]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype, fn.argtypes = res, args
+    if lib.sdfnmpc_abi_version() != 1:
+        raise SdfnmpcError("libsdfnmpc.so ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise SdfnmpcError(f"sdfnmpc error {rc}: {load().sdfnmpc_last_error().decode()}")
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if isinstance(t, int):
+        return t
+    return t.data_ptr()
+
+
+class Context:
+    """One HIP device + stream (sdfnmpc_ctx)."""
+
+    def __init__(self, device: int = 0, stream=None, tile_rows: int = 32):
+        lib = load()
+        h = C.c_void_p()
+        _check(lib.sdfnmpc_ctx_create(device, stream, C.byref(h)))
+        self.h = h
+        self.device = device
+        self.set_tile_rows(tile_rows)
+
+    def set_tile_rows(self, rows: int):
+        _check(load().sdfnmpc_ctx_set_tile_rows(self.h, rows))
+
+    def set_stream(self, stream):
+        _check(load().sdfnmpc_ctx_set_stream(self.h, stream))
+
+    def synchronize(self):
+        _check(load().sdfnmpc_ctx_synchronize(self.h))
+
+    @property
+    def stream(self) -> int:
+        return load().sdfnmpc_ctx_stream(self.h)
+
+    def enable_timing(self, on=True):
+        _check(load().sdfnmpc_ctx_enable_timing(self.h, int(on)))
+
+    def kernel_stats(self, name: str):
+        ms, n = C.c_double(), C.c_longlong()
+        _check(load().sdfnmpc_ctx_kernel_stats(self.h, name.encode(), C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def reset_stats(self):
+        _check(load().sdfnmpc_ctx_reset_stats(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().sdfnmpc_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class Net:
+    """Device-resident packed NeuralDF (sdfnmpc_net)."""
+
+    def __init__(self, ctx: Context, handle):
+        self.ctx, self.h = ctx, handle
+
+    @classmethod
+    def siren(cls, ctx: Context, seed: int = 0, weight_gain: float = 1.0, bias_gain: float = 0.0):
+        h = C.c_void_p()
+        _check(load().sdfnmpc_net_siren(ctx.h, seed, weight_gain, bias_gain, C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_blob(cls, ctx: Context, blob: bytes):
+        h = C.c_void_p()
+        buf = C.create_string_buffer(blob, len(blob))
+        _check(load().sdfnmpc_net_load(ctx.h, buf, len(blob), C.byref(h)))
+        return cls(ctx, h)
+
+    @classmethod
+    def from_file(cls, ctx: Context, path: str):
+        h = C.c_void_p()
+        _check(load().sdfnmpc_net_load_file(ctx.h, path.encode(), C.byref(h)))
+        return cls(ctx, h)
+
+    @property
+    def max_df(self) -> float:
+        return float(load().sdfnmpc_net_max_df(self.h))
+
+    @property
+    def fingerprint(self) -> int:
+        return int(load().sdfnmpc_net_fingerprint(self.h))
+
+    def eval(self, rows, pos4, latent, rows_per_inst, out4, grad_latent=None):
+        """Device-pointer SDF evaluation (asynchronous on the context stream)."""
+        _check(load().sdfnmpc_sdf_eval(self.ctx.h, self.h, rows, _ptr(pos4), _ptr(latent), rows_per_inst,
+                                       _ptr(out4), _ptr(grad_latent)))
+
+    def eval_host(self, inp: np.ndarray, want_grad=True):
+        """Host-pointer synchronous evaluation: inp [rows, 131] fp64 -> (df [rows], grad [rows,131])."""
+        inp = np.ascontiguousarray(inp, dtype=np.float64)
+        rows = inp.shape[0]
+        df = np.empty(rows)
+        g = np.empty_like(inp) if want_grad else None
+        P = C.POINTER(C.c_double)
+        _check(load().sdfnmpc_sdf_eval_host(self.ctx.h, self.h, rows, inp.ctypes.data_as(P), df.ctypes.data_as(P),
+                                            None if g is None else g.ctypes.data_as(P)))
+        return df, g
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().sdfnmpc_net_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def quad_model(cfg) -> QuadModelC:
+    lim = cfg.robot.limits
+    R = np.asarray(cfg.sensor.B_R_C, dtype=np.float64).ravel()
+    return QuadModelC(float(lim.gamma), float(lim.roll), float(lim.pitch), float(lim.wz), 9.81,
+                      (C.c_double * 3)(*[float(v) for v in cfg.sensor.B_p_C]), (C.c_double * 9)(*R),
+                      float(cfg.mpc.fov_const_offset))
+
+
+def linearize(ctx: Context, net: Net, model: QuadModelC, B: int, N: int, np_: int, bufs: dict, latent_mode=0):
+    """Enqueue the batched preparation phase.  bufs: device tensors named as sdfnmpc_lin_args."""
+    a = LinArgsC(B, N, np_, latent_mode, *[_ptr(bufs.get(k)) for k in
+                                           ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh",
+                                            "sdf")])
+    _check(load().sdfnmpc_linearize(ctx.h, net.h, C.byref(model), C.byref(a)))
+
+
+def shooting_grid(N: int, T: float, uniform=True, nb_short_nodes=2, dt_short=0.01):
+    nodes, dt = np.empty(N + 1), np.empty(N)
+    P = C.POINTER(C.c_double)
+    _check(load().sdfnmpc_shooting_grid(N, T, int(bool(uniform)), nb_short_nodes, dt_short, nodes.ctypes.data_as(P),
+                                        dt.ctypes.data_as(P)))
+    return nodes, dt

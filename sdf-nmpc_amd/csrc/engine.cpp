@@ -1,0 +1,654 @@
+// C ABI implementation (include/sdfnmpc.h): contexts, device-resident packed networks, launches.
+//
+// Host-side runtime only: all arithmetic of the hot path happens in sdf_mlp.hip / linearize.hip.
+// There is no CPU fallback: without a HIP device every compute entry point fails with
+// SDFNMPC_E_NODEVICE / SDFNMPC_E_HIP.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/sdfnmpc.h"
+#include "lin_kernels.h"
+#include "sdf_kernels.h"
+
+using namespace sdfn;
+
+// ------------------------------------------------------------------------------------------------
+// errors
+static thread_local std::string g_err;
+static int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+#define HIPCHK(expr)                                                                              \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess) return fail(SDFNMPC_E_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+extern "C" int sdfnmpc_abi_version(void) { return SDFNMPC_ABI_VERSION; }
+extern "C" const char* sdfnmpc_last_error(void) { return g_err.c_str(); }
+
+// ------------------------------------------------------------------------------------------------
+// context
+struct DevBuf {
+    void* p = nullptr;
+    size_t bytes = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= bytes) return hipSuccess;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        bytes = 0;
+        hipError_t e = hipMalloc(&p, n);
+        if (e == hipSuccess) bytes = n;
+        return e;
+    }
+    ~DevBuf() {
+        if (p) (void)hipFree(p);
+    }
+};
+
+struct KStat {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    double ms = 0.0;
+    long long n = 0;
+};
+
+struct sdfnmpc_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool own_stream = false;
+    int tile_rows = 32;
+    bool timing = false;
+    DevBuf pos4, c13, sdf4, lat, out4, glat;
+    std::vector<float> h_in;  // host staging for sdf_eval_host
+    std::map<std::string, KStat> stats;
+    std::mutex mu;  // serialises the host-pointer path (CasADi externals may be called concurrently)
+};
+
+struct ScopedDevice {
+    int prev = -1;
+    explicit ScopedDevice(int d) {
+        (void)hipGetDevice(&prev);
+        if (prev != d) (void)hipSetDevice(d);
+    }
+    ~ScopedDevice() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        if (prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+// launch helper with optional HIP-event timing on the context stream
+template <typename F>
+static hipError_t timed(sdfnmpc_ctx* ctx, const char* name, F&& launch) {
+    if (!ctx->timing) return launch();
+    hipEvent_t a, b;
+    hipError_t e = hipEventCreate(&a);
+    if (e != hipSuccess) return e;
+    e = hipEventCreate(&b);
+    if (e != hipSuccess) return e;
+    (void)hipEventRecord(a, ctx->stream);
+    e = launch();
+    (void)hipEventRecord(b, ctx->stream);
+    ctx->stats[name].pending.emplace_back(a, b);
+    return e;
+}
+
+extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
+    if (!out) return fail(SDFNMPC_E_ARG, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(SDFNMPC_E_NODEVICE, "no HIP device visible: the sdfnmpc compute path has no CPU fallback");
+    if (device < 0 || device >= n) return fail(SDFNMPC_E_ARG, "device index out of range");
+    ScopedDevice sd(device);
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::string(prop.gcnArchName).rfind("gfx950", 0) != 0)
+        return fail(SDFNMPC_E_UNSUPPORTED, std::string("built for gfx950 only, device is ") + prop.gcnArchName);
+    HIPCHK(sdf_set_lds_limits());
+    auto* c = new sdfnmpc_ctx();
+    c->device = device;
+    if (stream) {
+        c->stream = (hipStream_t)stream;
+    } else {
+        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete c;
+            return fail(SDFNMPC_E_HIP, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+        }
+        c->own_stream = true;
+    }
+    *out = c;
+    return SDFNMPC_OK;
+}
+
+extern "C" void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx) {
+    if (!ctx) return;
+    ScopedDevice sd(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& kv : ctx->stats)
+        for (auto& ev : kv.second.pending) {
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+    if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;  // device buffers are freed by their destructors, on ctx->device
+}
+
+extern "C" int sdfnmpc_ctx_set_stream(sdfnmpc_ctx* ctx, void* stream) {
+    if (!ctx) return fail(SDFNMPC_E_ARG, "ctx is NULL");
+    ScopedDevice sd(ctx->device);
+    if (ctx->own_stream) {
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        (void)hipStreamDestroy(ctx->stream);
+        ctx->own_stream = false;
+    }
+    if (stream) {
+        ctx->stream = (hipStream_t)stream;
+    } else {
+        HIPCHK(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+        ctx->own_stream = true;
+    }
+    return SDFNMPC_OK;
+}
+
+extern "C" void* sdfnmpc_ctx_stream(sdfnmpc_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+
+extern "C" int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx) {
+    if (!ctx) return fail(SDFNMPC_E_ARG, "ctx is NULL");
+    ScopedDevice sd(ctx->device);
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows) {
+    if (!ctx) return fail(SDFNMPC_E_ARG, "ctx is NULL");
+    if (rows != 32 && rows != 64) return fail(SDFNMPC_E_ARG, "tile rows must be 32 or 64");
+    ctx->tile_rows = rows;
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_ctx_enable_timing(sdfnmpc_ctx* ctx, int on) {
+    if (!ctx) return fail(SDFNMPC_E_ARG, "ctx is NULL");
+    ctx->timing = on != 0;
+    return SDFNMPC_OK;
+}
+
+static int resolve_stats(sdfnmpc_ctx* ctx) {
+    ScopedDevice sd(ctx->device);
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (auto& kv : ctx->stats) {
+        for (auto& ev : kv.second.pending) {
+            float ms = 0.0f;
+            HIPCHK(hipEventElapsedTime(&ms, ev.first, ev.second));
+            kv.second.ms += ms;
+            kv.second.n += 1;
+            (void)hipEventDestroy(ev.first);
+            (void)hipEventDestroy(ev.second);
+        }
+        kv.second.pending.clear();
+    }
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_ctx_kernel_stats(sdfnmpc_ctx* ctx, const char* kernel, double* total_ms, long long* launches) {
+    if (!ctx || !kernel) return fail(SDFNMPC_E_ARG, "ctx/kernel is NULL");
+    int rc = resolve_stats(ctx);
+    if (rc) return rc;
+    auto it = ctx->stats.find(kernel);
+    if (total_ms) *total_ms = it == ctx->stats.end() ? 0.0 : it->second.ms;
+    if (launches) *launches = it == ctx->stats.end() ? 0 : it->second.n;
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_ctx_reset_stats(sdfnmpc_ctx* ctx) {
+    if (!ctx) return fail(SDFNMPC_E_ARG, "ctx is NULL");
+    int rc = resolve_stats(ctx);
+    if (rc) return rc;
+    ctx->stats.clear();
+    return SDFNMPC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// network: .sdfw parsing (sdf-nmpc_amd/weights.py:pack) and packing into the kernels' layouts
+namespace {
+
+struct HostNet {
+    int nb_states = 3, L = 0, n1 = 0, n2 = 0, n3 = 0, n4 = 0, nf = 0, nd = 0;
+    float w0 = 0, max_df = 1;
+    std::vector<float> dirs, freqs;                           // [3][nd], [nf]
+    std::vector<float> W1, b1, W2, b2, W3, b3, W4, b4, W5, b5;  // torch order / shapes
+    int E() const { return 3 + 2 * nd * nf; }
+};
+
+uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+// identical to weights.prng_uniform / oracle orc_prng_uniform
+void prng_fill(uint64_t seed, uint64_t stream, std::vector<double>& out) {
+    const uint64_t key = mix64(seed * 0x9E3779B97F4A7C15ULL + stream * 0xD1B54A32D192ED03ULL + 1ULL);
+    for (size_t i = 0; i < out.size(); ++i)
+        out[i] = (double)(mix64(key + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ULL) >> 40) * (1.0 / 16777216.0);
+}
+
+std::vector<float*> param_list(HostNet& h) {
+    return {h.W1.data(), h.b1.data(), h.W2.data(), h.b2.data(), h.W3.data(),
+            h.b3.data(), h.W4.data(), h.b4.data(), h.W5.data(), h.b5.data()};
+}
+std::vector<std::pair<int, int>> param_shapes(const HostNet& h) {
+    const int E = h.E(), L = h.L;
+    return {{h.n1, E + L}, {h.n1, 1}, {h.n2, h.n1}, {h.n2, 1}, {h.n3, h.n2 + E + L},
+            {h.n3, 1},     {h.n4, h.n3}, {h.n4, 1}, {1, h.n4}, {1, 1}};
+}
+void alloc_params(HostNet& h) {
+    auto sh = param_shapes(h);
+    std::vector<std::vector<float>*> v = {&h.W1, &h.b1, &h.W2, &h.b2, &h.W3, &h.b3, &h.W4, &h.b4, &h.W5, &h.b5};
+    for (size_t i = 0; i < v.size(); ++i) v[i]->assign((size_t)sh[i].first * sh[i].second, 0.0f);
+}
+
+int check_supported(const HostNet& h) {
+    if (h.nb_states != 3 || h.L != L || h.n1 != N1 || h.n2 != N2 || h.n3 != N3 || h.n4 != N4 || h.nd != EMB_ND ||
+        h.nf != EMB_NF) {
+        char buf[256];
+        snprintf(buf, sizeof buf,
+                 "network architecture (states %d, latent %d, layers [%d,%d,%d,%d], dirs %d, freqs %d) is not "
+                 "built for; this build supports latent 128, [256,256,128,64], 'oct' embedding, 5 freqs",
+                 h.nb_states, h.L, h.n1, h.n2, h.n3, h.n4, h.nd, h.nf);
+        return fail(SDFNMPC_E_UNSUPPORTED, buf);
+    }
+    return SDFNMPC_OK;
+}
+
+int parse_sdfw(const void* blob, size_t bytes, HostNet& h) {
+    const unsigned char* p = (const unsigned char*)blob;
+    const size_t HDR = 8 + 10 * 4 + 2 * 4;
+    if (!blob || bytes < HDR || memcmp(p, "SDFNMPCW", 8) != 0) return fail(SDFNMPC_E_FORMAT, "not an .sdfw blob");
+    uint32_t u[10];
+    memcpy(u, p + 8, sizeof u);
+    float f[2];
+    memcpy(f, p + 48, sizeof f);
+    if (u[0] != 1) return fail(SDFNMPC_E_FORMAT, "unsupported .sdfw version");
+    if (u[9] != 0) return fail(SDFNMPC_E_UNSUPPORTED, "only res='full' networks are supported");
+    h.nb_states = (int)u[1];
+    h.L = (int)u[2];
+    h.n1 = (int)u[3]; h.n2 = (int)u[4]; h.n3 = (int)u[5]; h.n4 = (int)u[6];
+    h.nf = (int)u[7];
+    h.nd = (int)u[8];
+    h.w0 = f[0];
+    h.max_df = f[1];
+    if (h.nd <= 0 || h.nf <= 0 || h.nd > 64 || h.nf > 64 || h.L < 0 || h.n1 <= 0 || h.n2 <= 0 || h.n3 <= 0 || h.n4 <= 0)
+        return fail(SDFNMPC_E_FORMAT, "bad .sdfw header");
+    size_t off = HDR;
+    auto take = [&](std::vector<float>& v, size_t n) -> bool {
+        if (off + 4 * n > bytes) return false;
+        v.resize(n);
+        memcpy(v.data(), p + off, 4 * n);
+        off += 4 * n;
+        return true;
+    };
+    if (!take(h.dirs, (size_t)3 * h.nd) || !take(h.freqs, (size_t)h.nf)) return fail(SDFNMPC_E_FORMAT, "truncated");
+    auto sh = param_shapes(h);
+    std::vector<std::vector<float>*> v = {&h.W1, &h.b1, &h.W2, &h.b2, &h.W3, &h.b3, &h.W4, &h.b4, &h.W5, &h.b5};
+    for (size_t i = 0; i < v.size(); ++i)
+        if (!take(*v[i], (size_t)sh[i].first * sh[i].second)) return fail(SDFNMPC_E_FORMAT, "truncated .sdfw params");
+    if (off != bytes) return fail(SDFNMPC_E_FORMAT, "trailing bytes in .sdfw blob");
+    return check_supported(h);
+}
+
+void siren_host(HostNet& h, uint64_t seed, float wg, float bg) {
+    h.nb_states = 3; h.L = L; h.n1 = N1; h.n2 = N2; h.n3 = N3; h.n4 = N4; h.nf = EMB_NF; h.nd = EMB_ND;
+    h.w0 = 20.0f;
+    h.max_df = 1.0f;
+    // 'oct' dirs exactly as torch builds them (embeddings.py:140-154): +-1 / fp32 sqrt(3)
+    static const int sg[8][3] = {{-1, -1, -1}, {-1, -1, 1}, {-1, 1, -1}, {-1, 1, 1},
+                                 {1, -1, -1},  {1, -1, 1},  {1, 1, -1},  {1, 1, 1}};
+    const float nrm = sqrtf(3.0f);
+    h.dirs.assign(3 * 8, 0.0f);
+    for (int d = 0; d < 8; ++d)
+        for (int c = 0; c < 3; ++c) h.dirs[c * 8 + d] = (float)sg[d][c] / nrm;
+    h.freqs = {1.0f, 2.0f, 4.0f, 8.0f, 16.0f};
+    alloc_params(h);
+    auto ptr = param_list(h);
+    auto sh = param_shapes(h);
+    std::vector<double> u;
+    for (int t = 0; t < 10; t += 2) {
+        const double bound = std::sqrt(6.0 / sh[t].second) / (double)h.w0;
+        u.assign((size_t)sh[t].first * sh[t].second, 0.0);
+        prng_fill(seed, t, u);
+        for (size_t i = 0; i < u.size(); ++i) ptr[t][i] = (float)((2.0 * u[i] - 1.0) * (bound * (double)wg));
+        if (bg > 0.0f) {
+            u.assign((size_t)sh[t + 1].first * sh[t + 1].second, 0.0);
+            prng_fill(seed, t + 1, u);
+            for (size_t i = 0; i < u.size(); ++i) ptr[t + 1][i] = (float)((2.0 * u[i] - 1.0) * (bound * (double)bg));
+        }
+    }
+}
+
+template <typename F>
+void pack_operand(std::vector<float>& dst, int N, int K, F&& W) {
+    const int CB = (N + 31) / 32, G = K / 8;
+    const size_t base = dst.size();
+    dst.resize(base + packed_floats(N, K), 0.0f);
+    for (int cb = 0; cb < CB; ++cb)
+        for (int g = 0; g < G; ++g)
+            for (int ln = 0; ln < 64; ++ln)
+                for (int i = 0; i < 4; ++i) {
+                    const int j = cb * 32 + (ln & 31), k = (ln >> 5) * (K / 2) + 4 * g + i;
+                    dst[base + (((size_t)cb * G + g) * 64 + ln) * 4 + i] = (j < N) ? W(j, k) : 0.0f;
+                }
+}
+
+}  // namespace
+
+struct sdfnmpc_net {
+    int device = 0;
+    HostNet host;
+    void* dmem = nullptr;
+    SdfArgs args{};  // weight pointers filled; per-call fields left zero
+    const float* WzT = nullptr;
+    const float* bias13 = nullptr;
+    uint64_t fingerprint = 0;
+};
+
+static int upload_net(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
+    const int Ein = h.E(), Lh = h.L;
+    const float* W1 = h.W1.data();
+    const float* W2 = h.W2.data();
+    const float* W3 = h.W3.data();
+    const float* W4 = h.W4.data();
+    const int c1 = Ein + Lh, c3 = N2 + Ein + Lh;  // row lengths of W1, W3
+    std::vector<float> blob;
+    std::vector<size_t> off;
+    auto mark = [&]() { off.push_back(blob.size()); };
+    mark(); pack_operand(blob, N1, KE, [&](int j, int k) { return k < E ? W1[(size_t)j * c1 + k] : 0.0f; });
+    mark(); pack_operand(blob, N2, N1, [&](int j, int k) { return W2[(size_t)j * N1 + k]; });
+    mark(); pack_operand(blob, N3, N2, [&](int j, int k) { return W3[(size_t)j * c3 + k]; });
+    mark(); pack_operand(blob, N3, KE, [&](int j, int k) { return k < E ? W3[(size_t)j * c3 + N2 + k] : 0.0f; });
+    mark(); pack_operand(blob, N4, N3, [&](int j, int k) { return W4[(size_t)j * N3 + k]; });
+    mark(); pack_operand(blob, N3, N4, [&](int j, int k) { return W4[(size_t)k * N3 + j]; });
+    mark(); pack_operand(blob, N2, N3, [&](int j, int k) { return W3[(size_t)k * c3 + j]; });
+    mark(); pack_operand(blob, NE, N3, [&](int j, int k) { return j < E ? W3[(size_t)k * c3 + N2 + j] : 0.0f; });
+    mark(); pack_operand(blob, N1, N2, [&](int j, int k) { return W2[(size_t)k * N1 + j]; });
+    mark(); pack_operand(blob, NE, N1, [&](int j, int k) { return j < E ? W1[(size_t)k * c1 + j] : 0.0f; });
+    mark(); pack_operand(blob, L, N3, [&](int j, int k) { return W3[(size_t)k * c3 + N2 + E + j]; });
+    mark(); pack_operand(blob, L, N1, [&](int j, int k) { return W1[(size_t)k * c1 + E + j]; });
+    // WzT [L][C13_STRIDE], bias13, b2, b4, w5, emb_tab[NE] (float4)
+    mark();
+    blob.resize(blob.size() + (size_t)L * C13_STRIDE);
+    for (int k = 0; k < L; ++k)
+        for (int j = 0; j < C13_STRIDE; ++j)
+            blob[off.back() + (size_t)k * C13_STRIDE + j] =
+                j < N1 ? W1[(size_t)j * c1 + E + k] : W3[(size_t)(j - N1) * c3 + N2 + E + k];
+    mark(); for (int j = 0; j < N1; ++j) blob.push_back(h.b1[j]); for (int j = 0; j < N3; ++j) blob.push_back(h.b3[j]);
+    mark(); blob.insert(blob.end(), h.b2.begin(), h.b2.end());
+    mark(); blob.insert(blob.end(), h.b4.begin(), h.b4.end());
+    mark(); blob.insert(blob.end(), h.W5.begin(), h.W5.end());
+    while (blob.size() % 4) blob.push_back(0.0f);
+    mark();
+    for (int m = 0; m < NE; ++m) {
+        float v[4] = {0, 0, 0, 0};
+        int j = -1;
+        if (m >= 3 && m < 3 + EMB_NB) j = m - 3;
+        else if (m >= 3 + EMB_NB && m < E) j = m - 3 - EMB_NB;
+        if (j >= 0) {
+            const int d = j / EMB_NF, f = j % EMB_NF;
+            for (int c = 0; c < 3; ++c) v[c] = h.dirs[c * EMB_ND + d] * h.freqs[f];  // freq = 2^f: exact
+        }
+        blob.insert(blob.end(), v, v + 4);
+    }
+    for (size_t o : off)
+        if (o % 4) return fail(SDFNMPC_E_FORMAT, "internal: misaligned packed operand");
+
+    auto* net = new sdfnmpc_net();
+    net->device = ctx->device;
+    ScopedDevice sd(ctx->device);
+    hipError_t e = hipMalloc(&net->dmem, blob.size() * sizeof(float));
+    if (e != hipSuccess) {
+        delete net;
+        return fail(SDFNMPC_E_HIP, std::string("hipMalloc(net): ") + hipGetErrorString(e));
+    }
+    e = hipMemcpy(net->dmem, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        (void)hipFree(net->dmem);
+        delete net;
+        return fail(SDFNMPC_E_HIP, std::string("hipMemcpy(net): ") + hipGetErrorString(e));
+    }
+    const float* d = (const float*)net->dmem;
+    SdfArgs& a = net->args;
+    int i = 0;
+    a.wF1 = (const float4*)(d + off[i++]);
+    a.wF2 = (const float4*)(d + off[i++]);
+    a.wF3h = (const float4*)(d + off[i++]);
+    a.wF3e = (const float4*)(d + off[i++]);
+    a.wF4 = (const float4*)(d + off[i++]);
+    a.wB4 = (const float4*)(d + off[i++]);
+    a.wB3 = (const float4*)(d + off[i++]);
+    a.wB3e = (const float4*)(d + off[i++]);
+    a.wB2 = (const float4*)(d + off[i++]);
+    a.wB1e = (const float4*)(d + off[i++]);
+    a.wB3z = (const float4*)(d + off[i++]);
+    a.wB1z = (const float4*)(d + off[i++]);
+    net->WzT = d + off[i++];
+    net->bias13 = d + off[i++];
+    a.b2 = d + off[i++];
+    a.b4 = d + off[i++];
+    a.w5 = d + off[i++];
+    a.emb_tab = (const float4*)(d + off[i++]);
+    a.b5 = h.b5[0];
+    a.w0 = h.w0;
+    // fingerprint: FNV-1a over the parameters in torch order
+    uint64_t fp = 1469598103934665603ULL;
+    auto sh = param_shapes(h);
+    auto pl = param_list(h);
+    for (size_t t = 0; t < pl.size(); ++t) {
+        const unsigned char* b = (const unsigned char*)pl[t];
+        const size_t nb = (size_t)sh[t].first * sh[t].second * 4;
+        for (size_t q = 0; q < nb; ++q) fp = (fp ^ b[q]) * 1099511628211ULL;
+    }
+    net->fingerprint = fp;
+    net->host = std::move(h);
+    *out = net;
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_net_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes, sdfnmpc_net** out) {
+    if (!ctx || !out) return fail(SDFNMPC_E_ARG, "ctx/out is NULL");
+    HostNet h;
+    int rc = parse_sdfw(blob, bytes, h);
+    if (rc) return rc;
+    return upload_net(ctx, std::move(h), out);
+}
+
+extern "C" int sdfnmpc_net_load_file(sdfnmpc_ctx* ctx, const char* path, sdfnmpc_net** out) {
+    if (!ctx || !path || !out) return fail(SDFNMPC_E_ARG, "NULL argument");
+    FILE* f = fopen(path, "rb");
+    if (!f) return fail(SDFNMPC_E_ARG, std::string("cannot open ") + path);
+    std::vector<unsigned char> buf;
+    unsigned char tmp[1 << 16];
+    size_t n;
+    while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) buf.insert(buf.end(), tmp, tmp + n);
+    fclose(f);
+    return sdfnmpc_net_load(ctx, buf.data(), buf.size(), out);
+}
+
+extern "C" int sdfnmpc_net_siren(sdfnmpc_ctx* ctx, uint64_t seed, float wg, float bg, sdfnmpc_net** out) {
+    if (!ctx || !out) return fail(SDFNMPC_E_ARG, "ctx/out is NULL");
+    HostNet h;
+    siren_host(h, seed, wg, bg);
+    return upload_net(ctx, std::move(h), out);
+}
+
+extern "C" void sdfnmpc_net_free(sdfnmpc_net* net) {
+    if (!net) return;
+    ScopedDevice sd(net->device);
+    if (net->dmem) (void)hipFree(net->dmem);
+    delete net;
+}
+
+extern "C" float sdfnmpc_net_max_df(const sdfnmpc_net* net) { return net ? net->host.max_df : NAN; }
+extern "C" int sdfnmpc_net_size_latent(const sdfnmpc_net* net) { return net ? net->host.L : -1; }
+extern "C" uint64_t sdfnmpc_net_fingerprint(const sdfnmpc_net* net) { return net ? net->fingerprint : 0; }
+
+// ------------------------------------------------------------------------------------------------
+// SDF evaluation
+static int run_sdf(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, const float4* pos4, const float* c13,
+                   int rows_per_inst, float4* out4, float* glat, int M) {
+    if (rows > 0x7fffffffLL / 2) return fail(SDFNMPC_E_ARG, "too many rows");
+    SdfArgs a = net->args;
+    a.c13 = c13;
+    a.pos = pos4;
+    a.out = out4;
+    a.grad_latent = glat;
+    a.rows = (int)rows;
+    a.rows_per_inst = rows_per_inst;
+    HIPCHK(timed(ctx, "sdf_mlp", [&] { return launch_sdf_mlp(a, M, glat != nullptr, ctx->stream); }));
+    return SDFNMPC_OK;
+}
+
+template <typename T>
+static int run_hoist(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const T* latent, long long stride, int n_inst,
+                     float* c13) {
+    HoistArgs<T> h{latent, stride, net->WzT, net->bias13, c13, n_inst};
+    HIPCHK(timed(ctx, "sdf_hoist", [&] { return launch_hoist<T>(h, ctx->stream); }));
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_sdf_eval(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, const float* pos4,
+                                const float* latent, int rows_per_inst, float* out4, float* grad_latent) {
+    if (!ctx || !net || (!pos4 && rows > 0) || (!latent && rows > 0) || (!out4 && rows > 0) || rows < 0 ||
+        rows_per_inst < 1)
+        return fail(SDFNMPC_E_ARG, "bad sdfnmpc_sdf_eval arguments");
+    if (net->device != ctx->device) return fail(SDFNMPC_E_ARG, "net and ctx are on different devices");
+    if (rows == 0) return SDFNMPC_OK;
+    ScopedDevice sd(ctx->device);
+    const int n_inst = (int)((rows + rows_per_inst - 1) / rows_per_inst);
+    HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
+    int rc = run_hoist<float>(ctx, net, latent, L, n_inst, (float*)ctx->c13.p);
+    if (rc) return rc;
+    return run_sdf(ctx, net, rows, (const float4*)pos4, (const float*)ctx->c13.p, rows_per_inst, (float4*)out4,
+                   grad_latent, grad_latent ? 32 : ctx->tile_rows);
+}
+
+extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const double* in,
+                                     double* df, double* grad) {
+    if (!ctx || !net || rows < 0 || (rows > 0 && (!in || !df))) return fail(SDFNMPC_E_ARG, "bad sdf_eval_host arguments");
+    if (rows == 0) return SDFNMPC_OK;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ScopedDevice sd(ctx->device);
+    const int D = 3 + L;
+    // host staging: [rows][4] pos | [rows][L] latent   (double -> float as L4CasADi does)
+    ctx->h_in.assign((size_t)rows * (4 + L), 0.0f);
+    float* hp = ctx->h_in.data();
+    float* hl = hp + (size_t)rows * 4;
+    for (int r = 0; r < rows; ++r) {
+        for (int c = 0; c < 3; ++c) hp[r * 4 + c] = (float)in[(size_t)r * D + c];
+        for (int k = 0; k < L; ++k) hl[(size_t)r * L + k] = (float)in[(size_t)r * D + 3 + k];
+    }
+    HIPCHK(ctx->lat.ensure(ctx->h_in.size() * sizeof(float)));
+    HIPCHK(ctx->out4.ensure((size_t)rows * 4 * sizeof(float)));
+    if (grad) HIPCHK(ctx->glat.ensure((size_t)rows * L * sizeof(float)));
+    HIPCHK(hipMemcpyAsync(ctx->lat.p, hp, ctx->h_in.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+    float* dpos = (float*)ctx->lat.p;
+    float* dlat = dpos + (size_t)rows * 4;
+    int rc = sdfnmpc_sdf_eval(ctx, net, rows, dpos, dlat, 1, (float*)ctx->out4.p, grad ? (float*)ctx->glat.p : nullptr);
+    if (rc) return rc;
+    std::vector<float> o((size_t)rows * 4), gl(grad ? (size_t)rows * L : 0);
+    HIPCHK(hipMemcpyAsync(o.data(), ctx->out4.p, o.size() * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    if (grad) HIPCHK(hipMemcpyAsync(gl.data(), ctx->glat.p, gl.size() * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    for (int r = 0; r < rows; ++r) {
+        df[r] = o[(size_t)r * 4];
+        if (grad) {
+            for (int c = 0; c < 3; ++c) grad[(size_t)r * D + c] = o[(size_t)r * 4 + 1 + c];
+            for (int k = 0; k < L; ++k) grad[(size_t)r * D + 3 + k] = gl[(size_t)r * L + k];
+        }
+    }
+    return SDFNMPC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// batched preparation phase
+extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
+                                 const sdfnmpc_lin_args* a) {
+    if (!ctx || !net || !mdl || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
+    if (a->B < 0 || a->N < 1 || a->np < 17 + net->host.L || (a->latent_mode != 0 && a->latent_mode != 1))
+        return fail(SDFNMPC_E_ARG, "bad B/N/np/latent_mode");
+    if (a->B == 0) return SDFNMPC_OK;
+    if (!a->x || !a->u || !a->p || !a->dt || !a->xn || !a->AB || !a->y || !a->Jy || !a->yN || !a->JyN || !a->h ||
+        !a->Jh)
+        return fail(SDFNMPC_E_ARG, "NULL array in sdfnmpc_lin_args");
+    if (net->device != ctx->device) return fail(SDFNMPC_E_ARG, "net and ctx are on different devices");
+    ScopedDevice sd(ctx->device);
+    const long long rows = (long long)a->B * (a->N + 1);
+    HIPCHK(ctx->pos4.ensure((size_t)rows * 16));
+    float4* sdf4 = (float4*)a->sdf;
+    if (!sdf4) {
+        HIPCHK(ctx->sdf4.ensure((size_t)rows * 16));
+        sdf4 = (float4*)ctx->sdf4.p;
+    }
+    const int n_inst = a->latent_mode == 0 ? a->B : (int)rows;
+    HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
+    // 1. Co_p_B per row
+    PrepArgs pa{a->x, a->p, (float4*)ctx->pos4.p, rows, a->np};
+    HIPCHK(timed(ctx, "prep_rows", [&] { return launch_prep_rows(pa, ctx->stream); }));
+    // 2. latent hoisting (latent = p[.][17:] as fp32)
+    const long long stride = a->latent_mode == 0 ? (long long)(a->N + 1) * a->np : (long long)a->np;
+    int rc = run_hoist<double>(ctx, net, a->p + 17, stride, n_inst, (float*)ctx->c13.p);
+    if (rc) return rc;
+    // 3. network forward + position gradient
+    rc = run_sdf(ctx, net, rows, (const float4*)ctx->pos4.p, (const float*)ctx->c13.p,
+                 a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows);
+    if (rc) return rc;
+    // 4. dynamics / cost / constraints
+    LinArgs la{};
+    la.x = a->x; la.u = a->u; la.p = a->p; la.dt = a->dt; la.sdf = sdf4;
+    la.xn = a->xn; la.AB = a->AB; la.y = a->y; la.Jy = a->Jy; la.yN = a->yN; la.JyN = a->JyN; la.h = a->h; la.Jh = a->Jh;
+    la.B = a->B; la.N = a->N; la.np = a->np;
+    la.m.gamma = mdl->gamma; la.m.roll = mdl->roll; la.m.pitch = mdl->pitch; la.m.wz = mdl->wz; la.m.g = mdl->g;
+    for (int i = 0; i < 3; ++i)  // B_R_C^T B_p_C + [fov_const_offset, 0, 0]
+        la.m.fov_off[i] = mdl->B_R_C[0 * 3 + i] * mdl->B_p_C[0] + mdl->B_R_C[1 * 3 + i] * mdl->B_p_C[1] +
+                          mdl->B_R_C[2 * 3 + i] * mdl->B_p_C[2] + (i == 0 ? mdl->fov_const_offset : 0.0);
+    la.m.max_df = net->host.max_df;
+    HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }));
+    return SDFNMPC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// shooting grid: numpy.linspace(start, stop, num) = i * ((stop - start) / (num - 1)) + start, last = stop
+static void np_linspace(double start, double stop, int num, double* y) {
+    if (num == 1) {  // numpy: div = 0 -> y = [start]
+        y[0] = start;
+        return;
+    }
+    const double step = (stop - start) / (num - 1);
+    for (int i = 0; i < num; ++i) {
+        volatile double t = (double)i * step;  // two roundings as numpy, no FMA contraction
+        y[i] = t + start;
+    }
+    if (num > 1) y[num - 1] = stop;
+}
+
+extern "C" int sdfnmpc_shooting_grid(int N, double T, int uniform, int n_short, double dt_short, double* nodes,
+                                     double* dt) {
+    if (N < 1 || !nodes || !dt) return fail(SDFNMPC_E_ARG, "bad grid arguments");
+    if (uniform) {
+        np_linspace(0.0, T, N + 1, nodes);
+    } else {
+        if (n_short < 1 || n_short > N) return fail(SDFNMPC_E_ARG, "nb_short_nodes out of range");
+        np_linspace(0.0, dt_short * (n_short - 1), n_short, nodes);
+        np_linspace(dt_short * n_short, T, N - n_short + 1, nodes + n_short);
+    }
+    for (int k = 0; k < N; ++k) dt[k] = nodes[k + 1] - nodes[k];
+    return SDFNMPC_OK;
+}

@@ -1,0 +1,44 @@
+// Shared definitions of the fp64 linearisation kernels (linearize.hip) and the engine.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace sdfn {
+
+// 'att' quadrotor model constants (quad_rollpitchyawrate.py, default.yaml robot.limits / sensor)
+struct QuadModel {
+    double gamma, roll, pitch, wz;  // input scalings u -> (thrust/m, roll, pitch, yaw rate)
+    double g;                       // 9.81 (base_model.py:10)
+    double fov_off[3];              // B_R_C^T B_p_C + [fov_const_offset, 0, 0] (cost_const_helpers.py:451-452)
+    double max_df;                  // NeuralDF.max_df: h_sdf when flag = 0 (gen_model.py:61)
+};
+
+struct LinArgs {
+    const double* x;   // [B][N+1][10]
+    const double* u;   // [B][N][4]
+    const double* p;   // [B][N+1][np]
+    const double* dt;  // [N]
+    const float4* sdf; // [B][N+1] (df, d df / d Co_p_B)
+    double* xn;        // [B][N][10]
+    double* AB;        // [B][N][14][10]   column j = d x_{k+1} / d (x,u)_j
+    double* y;         // [B][N][11]
+    double* Jy;        // [B][N][14][11]
+    double* yN;        // [B][4]
+    double* JyN;       // [B][10][4]
+    double* h;         // [B][N+1][3]
+    double* Jh;        // [B][N+1][10][3]
+    QuadModel m;
+    int B, N, np;
+};
+
+struct PrepArgs {
+    const double* x;  // [rows][10]
+    const double* p;  // [rows][np]
+    float4* pos;      // [rows]
+    long long rows;
+    int np;
+};
+
+hipError_t launch_linearize(const LinArgs& a, hipStream_t s);
+hipError_t launch_prep_rows(const PrepArgs& a, hipStream_t s);
+
+}  // namespace sdfn

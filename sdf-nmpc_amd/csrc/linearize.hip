@@ -1,0 +1,209 @@
+// Per-node linearisation of the SQP-RTI preparation phase (fp64) -- the HBM-bound half of the path.
+//
+// For every (instance b, shooting node k) this computes what acados evaluates per node
+// (SURVEY.md §3.2 step 4):
+//   k < N : x_{k+1} = RK4(x_k, u_k, dt_k) and [A_k | B_k] = d x_{k+1} / d (x_k, u_k)
+//           (acados ERK, ocp.py:106: RK4, 1 step, forward sensitivities == exact derivative of the
+//           RK4 map); NONLINEAR_LS residual y_k (11) and J_y (11 x 14)
+//   k = N : terminal residual y_N (4) and J_yN (4 x 10)
+//   all k : h_k = [hfov, vfov, sdf] and J_h = d h / d x (3 x 10; d h / d u == 0)
+// Model: quad_rollpitchyawrate.py:19-55 ('att'), utils/math.py:7-54,169-192; constraints
+// cost_const_helpers.py:48-75 (add_fov_const_trigo) and gen_model.py:46-70 (sdf with flag).
+//
+// Derivatives are forward-mode dual numbers with ONE tangent per lane: a node is served by 16
+// lanes, lane t < 14 carrying d/d(x,u)_t, so every lane writes one Jacobian column (column-major
+// blocks, 80-112 contiguous bytes per lane).  The SDF entries use the network output of
+// sdf_mlp_kernel: d s / d W_p_B = flag * (d df / d Co_p_B) W_R_Co^T.
+#include <hip/hip_runtime.h>
+
+#include "lin_kernels.h"
+
+namespace sdfn {
+
+struct dd {
+    double v, t;
+};
+__device__ __forceinline__ dd C(double c) { return {c, 0.0}; }
+__device__ __forceinline__ dd operator+(dd a, dd b) { return {a.v + b.v, a.t + b.t}; }
+__device__ __forceinline__ dd operator-(dd a, dd b) { return {a.v - b.v, a.t - b.t}; }
+__device__ __forceinline__ dd operator-(dd a) { return {-a.v, -a.t}; }
+__device__ __forceinline__ dd operator*(dd a, dd b) { return {a.v * b.v, a.t * b.v + a.v * b.t}; }
+__device__ __forceinline__ dd operator*(dd a, double c) { return {a.v * c, a.t * c}; }
+__device__ __forceinline__ dd operator/(dd a, dd b) {
+    const double q = a.v / b.v;
+    return {q, (a.t - q * b.t) / b.v};
+}
+__device__ __forceinline__ dd dsqrt(dd a) {
+    const double s = sqrt(a.v);
+    return {s, a.t / (2.0 * s)};
+}
+__device__ __forceinline__ dd datan2(dd y, dd x) {
+    const double den = x.v * x.v + y.v * y.v;
+    return {atan2(y.v, x.v), (x.v * y.t - y.v * x.t) / den};
+}
+
+// f_expl of the 'att' model; sr/cr/sp/cp = sin/cos of roll, pitch (constant over RK4 stages)
+__device__ __forceinline__ void quad_f(const QuadModel& m, const dd* x, dd gamma, dd sr, dd cr, dd sp, dd cp, dd wz,
+                                       dd* f, dd* W_a2) {
+    const dd nq = dsqrt(x[3] * x[3] + x[4] * x[4] + (x[5] * x[5] + x[6] * x[6]));
+    const dd q0 = x[3] / nq, q1 = x[4] / nq, q2 = x[5] / nq, q3 = x[6] / nq;
+    // theta_z = atan2(q3, q0); (cos, sin)(theta_z) = (q0, q3) / |(q0, q3)|
+    dd c, s;
+    const dd n03 = dsqrt(q0 * q0 + q3 * q3);
+    if (n03.v > 0.0) {
+        c = q0 / n03;
+        s = q3 / n03;
+    } else {
+        c = C(1.0);
+        s = C(0.0);
+    }
+    // V_R_B e_z gamma = [cr sp, -sr, cr cp] gamma (euler2rot with yaw = 0, math.py:34-42)
+    const dd b0 = cr * sp * gamma, b1 = -sr * gamma, b2 = cr * cp * gamma;
+    // W_R_V = quat2rot([c,0,0,s]) (math.py:11-19)
+    const dd r11 = c * c - s * s, r21 = (c * s) * 2.0, r33 = c * c + s * s;
+    f[0] = x[7];
+    f[1] = x[8];
+    f[2] = x[9];
+    f[3] = (-q3 * wz) * 0.5;  // hamilton_prod(q, [0,0,0,wz]) / 2
+    f[4] = (q2 * wz) * 0.5;
+    f[5] = (-q1 * wz) * 0.5;
+    f[6] = (q0 * wz) * 0.5;
+    f[7] = r11 * b0 - r21 * b1;
+    f[8] = r21 * b0 + r11 * b1;
+    f[9] = r33 * b2 - C(m.g);
+    if (W_a2) *W_a2 = f[9];
+}
+
+__global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
+    const int tid = threadIdx.x;
+    const int t = tid & 15;                           // tangent direction of this lane
+    const long long r = (long long)blockIdx.x * 16 + (tid >> 4);  // node row = b * (N+1) + k
+    const int N = A.N, N1 = A.N + 1;
+    if (r >= (long long)A.B * N1) return;
+    const long long b = r / N1;
+    const int k = (int)(r - b * N1);
+    const QuadModel& m = A.m;
+
+    const double* xr = A.x + r * 10;
+    dd X[10];
+#pragma unroll
+    for (int i = 0; i < 10; ++i) X[i] = {xr[i], (i == t) ? 1.0 : 0.0};
+
+    if (k < N) {
+        const long long s = b * N + k;
+        const double* ur = A.u + s * 4;
+        dd U[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) U[i] = {ur[i], (10 + i == t) ? 1.0 : 0.0};
+        const dd gamma = U[0] * m.gamma, roll = U[1] * m.roll, pitch = U[2] * m.pitch, wz = U[3] * m.wz;
+        double s_r, c_r, s_p, c_p;
+        sincos(roll.v, &s_r, &c_r);
+        sincos(pitch.v, &s_p, &c_p);
+        const dd sr = {s_r, c_r * roll.t}, cr = {c_r, -s_r * roll.t};
+        const dd sp = {s_p, c_p * pitch.t}, cp = {c_p, -s_p * pitch.t};
+        // ---- ERK4 (Butcher c = [0, 1/2, 1/2, 1], b = [1/6, 1/3, 1/3, 1/6]); acados-style
+        //      accumulation x_out = x + (h b_1) k_1 + ... + (h b_4) k_4, stage input x + (h a_s) k_{s-1}
+        const double dt = A.dt[k];
+        const double hb[4] = {dt / 6, dt / 3, dt / 3, dt / 6}, ha[4] = {0.0, dt / 2, dt / 2, dt};
+        dd xo[10], kk[10], tmp[10], W_a2;
+        quad_f(m, X, gamma, sr, cr, sp, cp, wz, kk, &W_a2);
+#pragma unroll
+        for (int i = 0; i < 10; ++i) xo[i] = X[i] + kk[i] * hb[0];
+#pragma unroll
+        for (int st = 1; st < 4; ++st) {
+#pragma unroll
+            for (int i = 0; i < 10; ++i) tmp[i] = X[i] + kk[i] * ha[st];
+            quad_f(m, tmp, gamma, sr, cr, sp, cp, wz, kk, nullptr);
+#pragma unroll
+            for (int i = 0; i < 10; ++i) xo[i] = xo[i] + kk[i] * hb[st];
+        }
+        double* ABc = A.AB + (s * 14 + t) * 10;
+#pragma unroll
+        for (int i = 0; i < 10; ++i) {
+            if (t < 14) ABc[i] = xo[i].t;
+            if (t == i) A.xn[s * 10 + i] = xo[i].v;
+        }
+        // ---- NONLINEAR_LS residual (quad_rollpitchyawrate.py:370-377)
+        const double* pr = A.p + r * A.np;
+        const dd nq = dsqrt(X[3] * X[3] + X[4] * X[4] + (X[5] * X[5] + X[6] * X[6]));
+        const dd q0 = X[3] / nq, q1 = X[4] / nq, q2 = X[5] / nq, q3 = X[6] / nq;
+        const dd nq2 = dsqrt(q0 * q0 + q1 * q1 + (q2 * q2 + q3 * q3));  // invert(q) = conj(q) / |q|
+        const dd i0 = q0 / nq2, i1 = -q1 / nq2, i2 = -q2 / nq2, i3 = -q3 / nq2;
+        const double d0 = pr[13], d1 = pr[14], d2 = pr[15], d3 = pr[16];  // p_idx.q_d
+        const dd qe3 = ((i3 * d0 + i2 * d1) - i1 * d2) + i0 * d3;         // (q_d (x) q^-1)[3]
+        dd Y[11] = {X[0], X[1], X[2], qe3, X[7], X[8], X[9], roll, pitch, wz, W_a2};
+        double* Jyc = A.Jy + (s * 14 + t) * 11;
+#pragma unroll
+        for (int i = 0; i < 11; ++i) {
+            if (t < 14) Jyc[i] = Y[i].t;
+            if (t == i) A.y[s * 11 + i] = Y[i].v;
+        }
+    } else {
+        // ---- terminal residual y_N = [p, q_e[3]]
+        const double* pr = A.p + r * A.np;
+        const dd nq = dsqrt(X[3] * X[3] + X[4] * X[4] + (X[5] * X[5] + X[6] * X[6]));
+        const dd q0 = X[3] / nq, q1 = X[4] / nq, q2 = X[5] / nq, q3 = X[6] / nq;
+        const dd nq2 = dsqrt(q0 * q0 + q1 * q1 + (q2 * q2 + q3 * q3));
+        const dd i0 = q0 / nq2, i1 = -q1 / nq2, i2 = -q2 / nq2, i3 = -q3 / nq2;
+        const double d0 = pr[13], d1 = pr[14], d2 = pr[15], d3 = pr[16];
+        const dd qe3 = ((i3 * d0 + i2 * d1) - i1 * d2) + i0 * d3;
+        const dd Y[4] = {X[0], X[1], X[2], qe3};
+        if (t < 10) {
+            double* J = A.JyN + (b * 10 + t) * 4;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) J[i] = Y[i].t;
+        }
+        if (t < 4) A.yN[b * 4 + t] = Y[t].v;
+    }
+
+    // ---- constraints h = [hfov, vfov, sdf] (cost_const_helpers.py:443-452, gen_model.py:46-61)
+    const double* pr = A.p + r * A.np;
+    const double flag = pr[0];
+    const double Wp0 = pr[1], Wp1 = pr[2], Wp2 = pr[3];
+    const double* R = pr + 4;  // W_R_Co row-major (== casadi reshape((3,3)).T)
+    const dd e0 = X[0] - C(Wp0), e1 = X[1] - C(Wp1), e2 = X[2] - C(Wp2);
+    const dd cx = (e0 * R[0] + e1 * R[3]) + e2 * R[6] + C(m.fov_off[0]);
+    const dd cy = (e0 * R[1] + e1 * R[4]) + e2 * R[7] + C(m.fov_off[1]);
+    const dd cz = (e0 * R[2] + e1 * R[5]) + e2 * R[8] + C(m.fov_off[2]);
+    const dd hf = datan2(cy, cx) * flag;
+    const dd vf = datan2(cz, dsqrt(cx * cx + cy * cy)) * flag;
+    const float4 sd = A.sdf[r];
+    if (t < 10) {
+        double* J = A.Jh + (r * 10 + t) * 3;
+        J[0] = hf.t;
+        J[1] = vf.t;
+        J[2] = (t < 3) ? flag * (((double)sd.y * R[t * 3 + 0] + (double)sd.z * R[t * 3 + 1]) + (double)sd.w * R[t * 3 + 2])
+                       : 0.0;
+    }
+    if (t == 0) A.h[r * 3 + 0] = hf.v;
+    if (t == 1) A.h[r * 3 + 1] = vf.v;
+    if (t == 2) A.h[r * 3 + 2] = flag * (double)sd.x + (1.0 - flag) * m.max_df;
+}
+
+// Co_p_B = W_R_Co^T (W_p_B - W_p_Co) in fp64, handed to the network as fp32 (L4CasADi converts the
+// CasADi double arguments to a float tensor) -- gen_model.py:46-51.
+__global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs A) {
+    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.rows) return;
+    const double* x = A.x + r * 10;
+    const double* p = A.p + r * A.np;
+    const double e0 = x[0] - p[1], e1 = x[1] - p[2], e2 = x[2] - p[3];
+    const double* R = p + 4;
+    A.pos[r] = make_float4((float)((e0 * R[0] + e1 * R[3]) + e2 * R[6]), (float)((e0 * R[1] + e1 * R[4]) + e2 * R[7]),
+                           (float)((e0 * R[2] + e1 * R[5]) + e2 * R[8]), 0.0f);
+}
+
+hipError_t launch_linearize(const LinArgs& a, hipStream_t s) {
+    const long long rows = (long long)a.B * (a.N + 1);
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(linearize_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_prep_rows(const PrepArgs& a, hipStream_t s) {
+    if (a.rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((a.rows + 255) / 256)), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace sdfn

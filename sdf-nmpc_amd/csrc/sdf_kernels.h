@@ -1,0 +1,71 @@
+// Shared definitions of the SDF kernels (sdf_mlp.hip) and their host launchers (engine.cpp).
+// Architecture: the deployed NeuralDF (scripts/neural_nets/df_train.py:98-102):
+// embed 'oct', nb_freqs 5, latent 128, layer_sizes [256, 256, 128, 64], res 'full'.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+
+namespace sdfn {
+
+constexpr int EMB_ND = 8, EMB_NF = 5;
+constexpr int EMB_NB = EMB_ND * EMB_NF;  // 40 projected frequencies
+constexpr int E = 3 + 2 * EMB_NB;        // 83 embedding features (embeddings.py:207)
+constexpr int KE = 88;                   // E padded to a multiple of 8 (MFMA k-grouping)
+constexpr int NE = 96;                   // E padded to 3 column blocks of 32 (d e GEMM)
+constexpr int L = 128;                   // latent size (default.yaml nn.size_latent)
+constexpr int N1 = 256, N2 = 256, N3 = 128, N4 = 64;
+constexpr int C13_STRIDE = N1 + N3;      // hoisted [c1 | c3] per instance
+constexpr int SE = 92;                   // LDS row strides (floats): stride/4 odd -> conflict-free b128
+constexpr int SA = 260;
+constexpr int HOIST_INST = 8;
+
+// Packed operand: OUT[M x N] = IN[M x K] . Wsrc^T, Wsrc(j, k) = weight of output j, input k.
+// Layout [cb][g][lane][4] with value Wsrc(cb*32 + (lane&31), (lane>>5)*K/2 + 4g + i), zero-padded.
+inline size_t packed_floats(int N, int K) { return (size_t)((N + 31) / 32) * (K / 8) * 64 * 4; }
+
+struct SdfArgs {
+    // forward operands
+    const float4* wF1;   // W1[:, :E]            N1 x KE
+    const float4* wF2;   // W2                   N2 x N1
+    const float4* wF3h;  // W3[:, :N2]           N3 x N2
+    const float4* wF3e;  // W3[:, N2:N2+E]       N3 x KE
+    const float4* wF4;   // W4                   N4 x N3
+    // backward operands (transposed)
+    const float4* wB4;   // W4^T                 N3 x N4
+    const float4* wB3;   // W3[:, :N2]^T         N2 x N3
+    const float4* wB3e;  // W3[:, N2:N2+E]^T     NE x N3
+    const float4* wB2;   // W2^T                 N1 x N2
+    const float4* wB1e;  // W1[:, :E]^T          NE x N1
+    const float4* wB3z;  // W3[:, N2+E:]^T       L x N3   (latent gradient only)
+    const float4* wB1z;  // W1[:, E:]^T          L x N1   (latent gradient only)
+    const float* b2;
+    const float* b4;
+    const float* w5;
+    const float4* emb_tab;  // [NE] (dirs[:, d] * 2^f) for m in the sin/cos ranges, else 0
+    const float* c13;       // [n_inst][C13_STRIDE]
+    const float4* pos;      // [rows] (Co_p_B as fp32, pad)
+    float4* out;            // [rows] (df, d df/d pos)
+    float* grad_latent;     // [rows][L] (latent-gradient variant only)
+    float b5;
+    float w0;
+    int rows;
+    int rows_per_inst;      // row r uses c13[r / rows_per_inst]
+};
+
+template <typename T>
+struct HoistArgs {
+    const T* latent;   // latent of instance i at latent[i * stride + k]
+    long long stride;
+    const float* WzT;  // [L][C13_STRIDE] = [W1[:, E:]^T | W3[:, N2+E:]^T]
+    const float* bias; // [C13_STRIDE] = [b1 | b3]
+    float* c13;        // [n_inst][C13_STRIDE]
+    int n_inst;
+};
+
+size_t sdf_lds_bytes(int M);
+hipError_t sdf_set_lds_limits();
+hipError_t launch_sdf_mlp(const SdfArgs& a, int M, bool latent_grad, hipStream_t s);
+template <typename T>
+hipError_t launch_hoist(const HoistArgs<T>& a, hipStream_t s);
+
+}  // namespace sdfn

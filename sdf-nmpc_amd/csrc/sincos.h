@@ -1,0 +1,48 @@
+// Range-reduced fp32 sine/cosine for the SIREN activations (sin(w0 * a), w0 = 20) and the positional
+// embedding (sin(2^f * proj), |arg| up to tens of radians), reference activation.py:12-13 and
+// embeddings.py:106-111.
+//
+// CDNA's v_sin_f32 / v_cos_f32 (and __sinf) take a revolution argument and are inaccurate beyond a
+// few periods, so they cannot meet the 1e-5 parity bar.  This is a 3-constant Cody-Waite reduction
+// by pi/2 with fused multiply-adds, then minimax polynomials on [-pi/4, pi/4]: ~1 ulp for
+// |x| < 2^17, one shared reduction for sin and cos.  Larger |x| (never reached by a sane network)
+// take the libm/ocml path, so the function is correct everywhere.
+#pragma once
+
+#if defined(__HIPCC__)
+#define SDFN_HD __host__ __device__ __forceinline__
+#else
+#define SDFN_HD static inline
+#include <math.h>
+#endif
+
+SDFN_HD void sdfn_sincosf(float x, float* s_out, float* c_out) {
+    if (!(fabsf(x) < 131072.0f)) {  // also NaN / inf
+#if defined(__HIP_DEVICE_COMPILE__)
+        sincosf(x, s_out, c_out);
+#else
+        *s_out = sinf(x);
+        *c_out = cosf(x);
+#endif
+        return;
+    }
+    const float q = rintf(x * 0.636619772367581343f);  // x * 2/pi
+    // pi/2 = C1 + C2 + C3, C1/C2 exact fp32
+    float r = fmaf(q, -1.57079637050628662109375f, x);
+    r = fmaf(q, 4.37113882867379289e-8f, r);
+    r = fmaf(q, 1.71512451e-15f, r);  // C2 = -4.3711388e-8, C3 = -1.7151245e-15
+    const float r2 = r * r;
+    // sin on [-pi/4, pi/4]
+    float ps = fmaf(r2, -1.9515295891e-4f, 8.3321608736e-3f);
+    ps = fmaf(r2, ps, -1.6666654611e-1f);
+    const float sr = fmaf(r * r2, ps, r);
+    // cos on [-pi/4, pi/4]
+    float pc = fmaf(r2, 2.443315711809948e-5f, -1.388731625493765e-3f);
+    pc = fmaf(r2, pc, 4.166664568298827e-2f);
+    const float cr = fmaf(r2 * r2, pc, fmaf(r2, -0.5f, 1.0f));
+    const int qi = (int)q;
+    const float s1 = (qi & 1) ? cr : sr;
+    const float c1 = (qi & 1) ? sr : cr;
+    *s_out = (qi & 2) ? -s1 : s1;
+    *c_out = ((qi + 1) & 2) ? -c1 : c1;
+}

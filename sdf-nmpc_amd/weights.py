@@ -1,0 +1,215 @@
+"""NeuralDF weights: architecture spec, deterministic SIREN-init generator, packed `.sdfw` format.
+
+This module is host-side plumbing for the hot path: it produces the fp32 parameter set that the
+HIP kernels (``csrc/sdf_mlp.hip``) consume through the C ABI (``include/sdfnmpc.h``).
+
+Reference anchors (``/root/reference``):
+  * architecture / parameter order ... ``sdf_nmpc/network/neural_df.py:61-89`` (``layers`` ModuleDict)
+  * forward semantics ................ ``sdf_nmpc/network/neural_df.py:91-103``
+  * positional embedding ............. ``sdf_nmpc/utils/embeddings.py:115-214`` ('oct' dirs :140-154)
+  * SIREN init ....................... ``sdf_nmpc/utils/layer_init.py:15-25``
+  * deployed hyper-parameters ........ ``scripts/neural_nets/df_train.py:98-102``
+    (``layer_sizes=[256,256,128,64]``, ``embed='oct'``, ``nb_freqs=5``, ``w0=20``, ``res='full'``)
+
+The real trained weights (``sdf_nmpc/data/sdf_90_25664.pt``) are git-LFS pointers that are absent
+from the reference checkout, so every test and benchmark uses weights regenerated from a seed by
+the counter-based PRNG below. The same PRNG is implemented in C (``csrc/sdfnmpc_prng.h``) and in the
+oracle, so weights never need to be committed.
+"""
+from __future__ import annotations
+
+import dataclasses
+import struct
+from typing import Dict, List, Tuple
+
+import numpy as np
+
+MAGIC = b"SDFNMPCW"
+VERSION = 1
+_HDR = struct.Struct("<8s10I2f")  # magic, version, nb_states, L, n1..n4, nb_freqs, n_dirs, res, w0, max_df
+
+# embedding projection directions, one row per direction (embeddings.py:127-201)
+_OCT = [(-1, -1, -1), (-1, -1, +1), (-1, +1, -1), (-1, +1, +1),
+        (+1, -1, -1), (+1, -1, +1), (+1, +1, -1), (+1, +1, +1)]
+_CUBE = [(-1, 0, 0), (+1, 0, 0), (0, -1, 0), (0, +1, 0), (0, 0, -1), (0, 0, +1)]
+
+
+def embedding_dirs(embed: str) -> np.ndarray:
+    """fp32 [3, n_dirs] projection matrix exactly as torch builds it (embeddings.py:127-154).
+
+    torch normalises each column with ``vector_norm`` in fp32: sqrt of a fp32 sum, then a
+    correctly-rounded fp32 division, which numpy reproduces bit for bit.
+    """
+    if embed == "pos":
+        return np.eye(3, dtype=np.float32)
+    if embed == "cube":  # not normalised in the reference (embeddings.py:129-139)
+        return np.array(_CUBE, dtype=np.float32).T.copy()
+    if embed == "oct":
+        d = np.array(_OCT, dtype=np.float32).T.copy()
+        n = np.sqrt((d * d).sum(axis=0, dtype=np.float32)).astype(np.float32)
+        return (d / n[None, :]).astype(np.float32)
+    raise ValueError(f"embedding '{embed}' is not supported by this build (supported: oct, pos, cube)")
+
+
+@dataclasses.dataclass(frozen=True)
+class NetSpec:
+    """Architecture of one NeuralDF (neural_df.py:13-26 constructor arguments)."""
+    size_latent: int = 128
+    layer_sizes: Tuple[int, int, int, int] = (256, 256, 128, 64)
+    nb_freqs: int = 5
+    embed: str = "oct"
+    w0: float = 20.0
+    max_df: float = 1.0
+    nb_states: int = 3
+
+    @property
+    def n_dirs(self) -> int:
+        return embedding_dirs(self.embed).shape[1]
+
+    @property
+    def n_embed(self) -> int:  # embeddings.py:207
+        return self.nb_freqs * self.n_dirs * 2 + 3
+
+    def param_shapes(self) -> List[Tuple[str, Tuple[int, ...]]]:
+        """Parameter names/shapes in torch ``state_dict`` order (neural_df.py:61-89, res='full')."""
+        E, L = self.n_embed, self.size_latent
+        n1, n2, n3, n4 = self.layer_sizes
+        return [
+            ("layers.main1.0.weight", (n1, E + L)), ("layers.main1.0.bias", (n1,)),
+            ("layers.main1.3.weight", (n2, n1)), ("layers.main1.3.bias", (n2,)),
+            ("layers.main2.0.weight", (n3, n2 + E + L)), ("layers.main2.0.bias", (n3,)),
+            ("layers.main2.3.weight", (n4, n3)), ("layers.main2.3.bias", (n4,)),
+            ("layers.df.0.weight", (1, n4)), ("layers.df.0.bias", (1,)),
+        ]
+
+    def n_params(self) -> int:
+        return int(sum(np.prod(s) for _, s in self.param_shapes()))
+
+
+DEFAULT_SPEC = NetSpec()
+WIDE_SPEC = NetSpec(layer_sizes=(1024, 1024, 512, 256))  # BASELINE config 5
+
+
+# ---------------------------------------------------------------------------------------------
+# counter-based PRNG (splitmix64 finaliser); mirrored in csrc/sdfnmpc_prng.h and oracle/oracle.c
+# ---------------------------------------------------------------------------------------------
+_M64 = (1 << 64) - 1
+_GOLD = 0x9E3779B97F4A7C15
+_TSTEP = 0xD1B54A32D192ED03
+
+
+def _mix64_int(z: int) -> int:
+    z &= _M64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & _M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & _M64
+    return z ^ (z >> 31)
+
+
+def _mix64_np(z: np.ndarray) -> np.ndarray:
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    return z ^ (z >> np.uint64(31))
+
+
+def prng_uniform(seed: int, stream: int, n: int) -> np.ndarray:
+    """n doubles in [0,1) with 24 random bits each; element i depends only on (seed, stream, i)."""
+    key = _mix64_int(seed * _GOLD + stream * _TSTEP + 1)
+    i = np.arange(1, n + 1, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        x = _mix64_np(np.uint64(key) + i * np.uint64(_GOLD))
+    return (x >> np.uint64(40)).astype(np.float64) * (2.0 ** -24)
+
+
+def siren_weights(spec: NetSpec = DEFAULT_SPEC, seed: int = 0, weight_gain: float = 1.0,
+                  bias_gain: float = 0.0) -> Dict[str, np.ndarray]:
+    """SIREN-initialised parameters (layer_init.py:15-25): W ~ U(+-sqrt(6/n_in)/w0), b = 0.
+
+    ``weight_gain`` scales the weight range (x2..x4 stresses the sin range reduction: trained nets
+    need not stay inside the init range); ``bias_gain`` > 0 draws biases from
+    U(+-bias_gain*sqrt(6/n_in)/w0) so the bias path is exercised (the reference init zeroes them).
+    Values are rounded once from double to fp32, identically in the C generator.
+    """
+    out = {}
+    shapes = spec.param_shapes()
+    for t in range(0, len(shapes), 2):
+        (wn, ws), (bn, bs) = shapes[t], shapes[t + 1]
+        bound = np.sqrt(6.0 / ws[-1]) / spec.w0
+        u = prng_uniform(seed, t, int(np.prod(ws)))
+        out[wn] = ((2.0 * u - 1.0) * (bound * weight_gain)).astype(np.float32).reshape(ws)
+        if bias_gain > 0.0:
+            ub = prng_uniform(seed, t + 1, int(np.prod(bs)))
+            out[bn] = ((2.0 * ub - 1.0) * (bound * bias_gain)).astype(np.float32).reshape(bs)
+        else:
+            out[bn] = np.zeros(bs, dtype=np.float32)
+    return out
+
+
+# ---------------------------------------------------------------------------------------------
+# packed binary format
+# ---------------------------------------------------------------------------------------------
+def pack(spec: NetSpec, params: Dict[str, np.ndarray]) -> bytes:
+    """Serialise to the `.sdfw` layout read by ``sdfnmpc_net_load_file`` (include/sdfnmpc.h)."""
+    dirs = embedding_dirs(spec.embed)
+    freqs = (2.0 ** np.linspace(0, spec.nb_freqs - 1, spec.nb_freqs)).astype(np.float32)
+    hdr = _HDR.pack(MAGIC, VERSION, spec.nb_states, spec.size_latent, *spec.layer_sizes,
+                    spec.nb_freqs, dirs.shape[1], 0, spec.w0, spec.max_df)
+    body = [dirs.astype("<f4").tobytes(), freqs.astype("<f4").tobytes()]
+    for name, shape in spec.param_shapes():
+        a = np.asarray(params[name], dtype=np.float32)
+        if a.shape != shape:
+            raise ValueError(f"{name}: shape {a.shape} != {shape}")
+        body.append(a.astype("<f4").tobytes())
+    return hdr + b"".join(body)
+
+
+def unpack(blob: bytes) -> Tuple[NetSpec, Dict[str, np.ndarray]]:
+    magic, ver, ns, L, n1, n2, n3, n4, nf, nd, res, w0, max_df = _HDR.unpack_from(blob, 0)
+    if magic != MAGIC or ver != VERSION or res != 0:
+        raise ValueError("not a version-1 res='full' .sdfw blob")
+    embed = {8: "oct", 3: "pos", 6: "cube"}[nd]
+    spec = NetSpec(size_latent=L, layer_sizes=(n1, n2, n3, n4), nb_freqs=nf, embed=embed,
+                   w0=float(w0), max_df=float(max_df), nb_states=ns)
+    off = _HDR.size + 4 * (3 * nd + nf)
+    params = {}
+    for name, shape in spec.param_shapes():
+        n = int(np.prod(shape))
+        params[name] = np.frombuffer(blob, dtype="<f4", count=n, offset=off).reshape(shape).copy()
+        off += 4 * n
+    if off != len(blob):
+        raise ValueError("trailing bytes in .sdfw blob")
+    return spec, params
+
+
+def save(path: str, spec: NetSpec, params: Dict[str, np.ndarray]) -> None:
+    with open(path, "wb") as f:
+        f.write(pack(spec, params))
+
+
+def load(path: str) -> Tuple[NetSpec, Dict[str, np.ndarray]]:
+    with open(path, "rb") as f:
+        return unpack(f.read())
+
+
+def from_torchscript(path: str) -> Tuple[NetSpec, Dict[str, np.ndarray]]:
+    """Convert a NeuralDF TorchScript archive of YOUR OWN (e.g. a df_train.py output,
+    ``df_train.py:250-253``) to (spec, params). Offline tool; the product never calls it.
+    The reference's ``sdf_nmpc/data/*.pt`` are LFS pointers in this checkout and are not read.
+    """
+    import torch  # offline only
+
+    m = torch.jit.load(path, map_location="cpu")
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    n1 = sd["layers.main1.0.weight"].shape[0]
+    n2 = sd["layers.main1.3.weight"].shape[0]
+    n3 = sd["layers.main2.0.weight"].shape[0]
+    n4 = sd["layers.main2.3.weight"].shape[0]
+    nd = sd["embed.dirs"].shape[1]
+    nf = sd["embed.freq_bands"].shape[0]
+    E = 3 + 2 * nf * nd
+    L = sd["layers.main1.0.weight"].shape[1] - E
+    embed = {8: "oct", 3: "pos", 6: "cube"}[nd]
+    spec = NetSpec(size_latent=L, layer_sizes=(n1, n2, n3, n4), nb_freqs=nf, embed=embed,
+                   w0=float(m.w0), max_df=float(m.max_df))
+    if not np.array_equal(sd["embed.dirs"], embedding_dirs(embed)):
+        raise ValueError("unexpected embedding directions")
+    return spec, {k: sd[k] for k, _ in spec.param_shapes()}
