@@ -1,0 +1,139 @@
+"""HIP SDF path (sdf_mlp.hip through libsdfnmpc.so / libsdf_l4c.so) vs the reference fixtures and oracle."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+from sdf_nmpc_amd import _lib, weights as W
+from tolerances import STRESS_FACTOR, sdf_df_err, sdf_df_ok, sdf_grad_err, sdf_grad_ok
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def eval_device(ctx, net, inp, rows_per_inst=1, latent=None):
+    torch = _torch()
+    dev = torch.device("cuda", ctx.device)
+    n = inp.shape[0]
+    pos4 = torch.zeros(n, 4, device=dev)
+    pos4[:, :3] = torch.from_numpy(np.ascontiguousarray(inp[:, :3], dtype=np.float32)).to(dev)
+    lat = torch.from_numpy(np.ascontiguousarray(inp[:, 3:] if latent is None else latent, dtype=np.float32)).to(dev)
+    out = torch.full((n, 4), float("nan"), device=dev)
+    torch.cuda.synchronize()
+    net.eval(n, pos4, lat, rows_per_inst, out)
+    ctx.synchronize()
+    return out.cpu().numpy()
+
+
+@pytest.mark.parametrize("tile_rows", [32, 64])
+def test_sdf_golden_siren(golden, gpu_ctx, tile_rows):
+    g = golden["sdf"]
+    gpu_ctx.set_tile_rows(tile_rows)
+    net = _lib.Net.siren(gpu_ctx, 0)
+    o = eval_device(gpu_ctx, net, g["input"])
+    for tag in ("f32", "f64"):
+        assert sdf_df_ok(o[:, 0], g[f"siren/df_{tag}"]), sdf_df_err(o[:, 0], g[f"siren/df_{tag}"])
+        assert sdf_grad_ok(o[:, 1:], g[f"siren/grad_{tag}"][:, :3]), sdf_grad_err(o[:, 1:], g[f"siren/grad_{tag}"][:, :3])
+    gpu_ctx.set_tile_rows(32)
+
+
+def test_sdf_golden_stress_no_worse_than_reference_fp32(golden, gpu_ctx):
+    """x3 weights + biases: sin arguments reach hundreds of radians (range-reduction stress)."""
+    g = golden["sdf"]
+    seed, wg, bg = g["stress/spec"]
+    net = _lib.Net.siren(gpu_ctx, int(seed), float(wg), float(bg))
+    o = eval_device(gpu_ctx, net, g["input"])
+    d64, G64 = g["stress/df_f64"], g["stress/grad_f64"][:, :3]
+    ref_df_err = np.abs(g["stress/df_f32"] - d64).max()
+    ref_g_err = np.linalg.norm(g["stress/grad_f32"][:, :3] - G64, axis=1).max()
+    assert np.abs(o[:, 0] - d64).max() <= STRESS_FACTOR * ref_df_err
+    assert np.linalg.norm(o[:, 1:] - G64, axis=1).max() <= STRESS_FACTOR * ref_g_err
+
+
+@pytest.mark.parametrize("rows,rpi", [(1, 1), (31, 1), (33, 33), (95, 5), (1000, 41)])
+def test_sdf_ragged_rows_vs_oracle(gpu_ctx, oracle_lib, rows, rpi):
+    """Row counts that are not tile multiples, shared latents (rows_per_inst > 1)."""
+    rng = np.random.default_rng(rows)
+    n_inst = (rows + rpi - 1) // rpi
+    lat = rng.normal(size=(n_inst, 128)).astype(np.float32)
+    pos = rng.uniform(-4, 4, (rows, 3)).astype(np.float32)
+    inp = np.concatenate([pos, lat[np.arange(rows) // rpi]], 1)
+    net = _lib.Net.siren(gpu_ctx, 0)
+    o = eval_device(gpu_ctx, net, inp, rpi, latent=lat)
+    onet = oracle_lib.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
+    df64, gp64, _ = onet.f64(inp.astype(np.float64))
+    assert np.isfinite(o).all()
+    assert sdf_df_ok(o[:, 0], df64) and sdf_grad_ok(o[:, 1:], gp64)
+
+
+def test_sdf_rows_independent_bitwise(gpu_ctx):
+    """A row's result does not depend on the other rows of its tile or on its position (bitwise)."""
+    rng = np.random.default_rng(3)
+    inp = np.concatenate([rng.uniform(-3, 3, (200, 3)), rng.normal(size=(200, 128))], 1).astype(np.float32)
+    net = _lib.Net.siren(gpu_ctx, 0)
+    a = eval_device(gpu_ctx, net, inp)
+    perm = rng.permutation(200)
+    b = eval_device(gpu_ctx, net, inp[perm])
+    assert np.array_equal(a[perm], b)
+    c = eval_device(gpu_ctx, net, inp[:7])
+    assert np.array_equal(a[:7], c)
+    gpu_ctx.set_tile_rows(64)
+    d = eval_device(gpu_ctx, net, inp)
+    gpu_ctx.set_tile_rows(32)
+    assert np.array_equal(a, d)
+
+
+def test_sdf_host_path_full_jacobian(golden, gpu_ctx):
+    """sdfnmpc_sdf_eval_host: the 1x131 Jacobian L4CasADi's jac_sdf_l4c returns (latent part included)."""
+    g = golden["sdf"]
+    net = _lib.Net.siren(gpu_ctx, 0)
+    df, gr = net.eval_host(g["input"][:96].astype(np.float64))
+    assert sdf_df_ok(df, g["siren/df_f32"][:96]) and sdf_df_ok(df, g["siren/df_f64"][:96])
+    for tag in ("f32", "f64"):
+        ref = g[f"siren/grad_{tag}"][:96]
+        assert sdf_grad_ok(gr[:, :3], ref[:, :3])
+        assert np.abs(gr[:, 3:] - ref[:, 3:]).max() <= 1e-5 * max(1.0, np.abs(ref[:, 3:]).max())
+
+
+def test_weight_blob_roundtrip_and_fingerprint(gpu_ctx):
+    params = W.siren_weights(W.DEFAULT_SPEC, 0)
+    a = _lib.Net.siren(gpu_ctx, 0)
+    b = _lib.Net.from_blob(gpu_ctx, W.pack(W.DEFAULT_SPEC, params))
+    assert a.fingerprint == b.fingerprint
+    assert _lib.Net.siren(gpu_ctx, 1).fingerprint != a.fingerprint
+    with pytest.raises(_lib.SdfnmpcError):
+        _lib.Net.from_blob(gpu_ctx, b"SDFNMPCW" + b"\0" * 40)
+    wide = W.pack(W.WIDE_SPEC, W.siren_weights(W.WIDE_SPEC, 0))
+    with pytest.raises(_lib.SdfnmpcError, match="not built for"):
+        _lib.Net.from_blob(gpu_ctx, wide)
+
+
+def test_l4c_shim_casadi_calls(golden, tmp_path):
+    """libsdf_l4c.so as acados/CasADi would call it: sdf_l4c then jac_sdf_l4c on the same input."""
+    g = golden["sdf"]
+    wpath = tmp_path / "sdf_l4c.sdfw"
+    W.save(str(wpath), W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
+    lib = ctypes.CDLL(_lib.L4C_PATH)
+    lib.sdf_l4c_configure.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    assert lib.sdf_l4c_configure(str(wpath).encode(), 0) == 0
+    D = ctypes.POINTER(ctypes.c_double)
+    for fn in (lib.sdf_l4c, lib.jac_sdf_l4c, lib.adj1_sdf_l4c):
+        fn.argtypes = [ctypes.POINTER(D), ctypes.POINTER(D), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    for i in range(0, 256, 17):
+        x = np.ascontiguousarray(g["input"][i].astype(np.float64))
+        out, jac, adj, seed = np.zeros(1), np.zeros(131), np.zeros(131), np.array([0.5])
+        args = (D * 3)(x.ctypes.data_as(D), out.ctypes.data_as(D), seed.ctypes.data_as(D))
+        assert lib.sdf_l4c(args, (D * 1)(out.ctypes.data_as(D)), None, None, 0) == 0
+        assert lib.jac_sdf_l4c(args, (D * 1)(jac.ctypes.data_as(D)), None, None, 0) == 0
+        assert lib.adj1_sdf_l4c(args, (D * 1)(adj.ctypes.data_as(D)), None, None, 0) == 0
+        assert sdf_df_ok(out, g["siren/df_f32"][i:i + 1])
+        assert sdf_grad_ok(jac[None, :3], g["siren/grad_f32"][i:i + 1, :3])
+        assert np.abs(jac[3:] - g["siren/grad_f32"][i, 3:]).max() <= 1e-5
+        np.testing.assert_array_equal(adj, 0.5 * jac)
+    # bad weights path -> non-zero status, never an exception across the ABI
+    assert lib.sdf_l4c_configure(str(tmp_path / "missing.sdfw").encode(), 0) != 0
