@@ -137,7 +137,7 @@ def main():
     reps = max(10, min(args.steps, 50))
     for _ in range(reps):
         step()
-    kst = {k: ctx.kernel_stats(k) for k in ("prep_rows", "sdf_hoist", "sdf_mlp", "linearize")}
+    kst = {k: ctx.kernel_stats(k) for k in ("sdf_hoist", "sdf_mlp", "linearize")}
     ctx.enable_timing(False)
     kms = {k: (v[0] / v[1] if v[1] else None) for k, v in kst.items()}
     rows = B * (N + 1)

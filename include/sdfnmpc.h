@@ -94,7 +94,7 @@ int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx);
 int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows);
 /* per-kernel HIP-event timing on the context stream (off by default) */
 int sdfnmpc_ctx_enable_timing(sdfnmpc_ctx* ctx, int on);
-/* kernel: "sdf_mlp", "sdf_hoist", "prep_rows", "linearize"; synchronizes the stream */
+/* kernel: "sdf_mlp", "sdf_hoist", "linearize"; synchronizes the stream(s) */
 int sdfnmpc_ctx_kernel_stats(sdfnmpc_ctx* ctx, const char* kernel, double* total_ms, long long* launches);
 int sdfnmpc_ctx_reset_stats(sdfnmpc_ctx* ctx);
 

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -65,9 +66,12 @@ struct sdfnmpc_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     bool own_stream = false;
+    hipStream_t aux = nullptr;                       // low-priority side stream (fork/join per call)
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    bool lin_first = false;
     int tile_rows = 32;
     bool timing = false;
-    DevBuf pos4, c13, sdf4, lat, out4, glat;
+    DevBuf c13, sdf4, lat, out4, glat;
     std::vector<float> h_in;  // host staging for sdf_eval_host
     std::map<std::string, KStat> stats;
     std::mutex mu;  // serialises the host-pointer path (CasADi externals may be called concurrently)
@@ -88,16 +92,17 @@ struct ScopedDevice {
 
 // launch helper with optional HIP-event timing on the context stream
 template <typename F>
-static hipError_t timed(sdfnmpc_ctx* ctx, const char* name, F&& launch) {
+static hipError_t timed(sdfnmpc_ctx* ctx, const char* name, F&& launch, hipStream_t st = nullptr) {
     if (!ctx->timing) return launch();
+    if (!st) st = ctx->stream;
     hipEvent_t a, b;
     hipError_t e = hipEventCreate(&a);
     if (e != hipSuccess) return e;
     e = hipEventCreate(&b);
     if (e != hipSuccess) return e;
-    (void)hipEventRecord(a, ctx->stream);
+    (void)hipEventRecord(a, st);
     e = launch();
-    (void)hipEventRecord(b, ctx->stream);
+    (void)hipEventRecord(b, st);
     ctx->stats[name].pending.emplace_back(a, b);
     return e;
 }
@@ -127,6 +132,17 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
         }
         c->own_stream = true;
     }
+    int lo = 0, hi = 0;
+    hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);  // lo = least urgent
+    if (e == hipSuccess) e = hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, lo);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming);
+    if (e != hipSuccess) {
+        sdfnmpc_ctx_destroy(c);
+        return fail(SDFNMPC_E_HIP, std::string("aux stream/events: ") + hipGetErrorString(e));
+    }
+    const char* lf = getenv("SDFNMPC_LIN_FIRST");
+    c->lin_first = lf && *lf == '1';
     *out = c;
     return SDFNMPC_OK;
 }
@@ -140,6 +156,12 @@ extern "C" void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx) {
             (void)hipEventDestroy(ev.first);
             (void)hipEventDestroy(ev.second);
         }
+    if (ctx->aux) {
+        (void)hipStreamSynchronize(ctx->aux);
+        (void)hipStreamDestroy(ctx->aux);
+    }
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;  // device buffers are freed by their destructors, on ctx->device
 }
@@ -186,6 +208,7 @@ extern "C" int sdfnmpc_ctx_enable_timing(sdfnmpc_ctx* ctx, int on) {
 static int resolve_stats(sdfnmpc_ctx* ctx) {
     ScopedDevice sd(ctx->device);
     HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->aux));
     for (auto& kv : ctx->stats) {
         for (auto& ev : kv.second.pending) {
             float ms = 0.0f;
@@ -356,7 +379,7 @@ struct sdfnmpc_net {
     HostNet host;
     void* dmem = nullptr;
     SdfArgs args{};  // weight pointers filled; per-call fields left zero
-    const float* WzT = nullptr;
+    const float4* WzT = nullptr;
     const float* bias13 = nullptr;
     uint64_t fingerprint = 0;
 };
@@ -383,13 +406,11 @@ static int upload_net(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     mark(); pack_operand(blob, NE, N1, [&](int j, int k) { return j < E ? W1[(size_t)k * c1 + j] : 0.0f; });
     mark(); pack_operand(blob, L, N3, [&](int j, int k) { return W3[(size_t)k * c3 + N2 + E + j]; });
     mark(); pack_operand(blob, L, N1, [&](int j, int k) { return W1[(size_t)k * c1 + E + j]; });
-    // WzT [L][C13_STRIDE], bias13, b2, b4, w5, emb_tab[NE] (float4)
+    // hoist operand Wsrc(j, k) = [W1[:, E:] ; W3[:, N2+E:]](j, k): N = C13_STRIDE, K = L
     mark();
-    blob.resize(blob.size() + (size_t)L * C13_STRIDE);
-    for (int k = 0; k < L; ++k)
-        for (int j = 0; j < C13_STRIDE; ++j)
-            blob[off.back() + (size_t)k * C13_STRIDE + j] =
-                j < N1 ? W1[(size_t)j * c1 + E + k] : W3[(size_t)(j - N1) * c3 + N2 + E + k];
+    pack_operand(blob, C13_STRIDE, L, [&](int j, int k) {
+        return j < N1 ? W1[(size_t)j * c1 + E + k] : W3[(size_t)(j - N1) * c3 + N2 + E + k];
+    });
     mark(); for (int j = 0; j < N1; ++j) blob.push_back(h.b1[j]); for (int j = 0; j < N3; ++j) blob.push_back(h.b3[j]);
     mark(); blob.insert(blob.end(), h.b2.begin(), h.b2.end());
     mark(); blob.insert(blob.end(), h.b4.begin(), h.b4.end());
@@ -439,7 +460,7 @@ static int upload_net(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     a.wB1e = (const float4*)(d + off[i++]);
     a.wB3z = (const float4*)(d + off[i++]);
     a.wB1z = (const float4*)(d + off[i++]);
-    net->WzT = d + off[i++];
+    net->WzT = (const float4*)(d + off[i++]);
     net->bias13 = d + off[i++];
     a.b2 = d + off[i++];
     a.b4 = d + off[i++];
@@ -503,9 +524,17 @@ extern "C" uint64_t sdfnmpc_net_fingerprint(const sdfnmpc_net* net) { return net
 // ------------------------------------------------------------------------------------------------
 // SDF evaluation
 static int run_sdf(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, const float4* pos4, const float* c13,
-                   int rows_per_inst, float4* out4, float* glat, int M) {
+                   int rows_per_inst, float4* out4, float* glat, int M, const SdfArgs* cons = nullptr) {
     if (rows > 0x7fffffffLL / 2) return fail(SDFNMPC_E_ARG, "too many rows");
     SdfArgs a = net->args;
+    if (cons) {
+        a.x = cons->x;
+        a.p = cons->p;
+        a.np = cons->np;
+        a.h = cons->h;
+        a.Jh = cons->Jh;
+        a.max_df = cons->max_df;
+    }
     a.c13 = c13;
     a.pos = pos4;
     a.out = out4;
@@ -591,7 +620,6 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
     if (net->device != ctx->device) return fail(SDFNMPC_E_ARG, "net and ctx are on different devices");
     ScopedDevice sd(ctx->device);
     const long long rows = (long long)a->B * (a->N + 1);
-    HIPCHK(ctx->pos4.ensure((size_t)rows * 16));
     float4* sdf4 = (float4*)a->sdf;
     if (!sdf4) {
         HIPCHK(ctx->sdf4.ensure((size_t)rows * 16));
@@ -599,20 +627,10 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
     }
     const int n_inst = a->latent_mode == 0 ? a->B : (int)rows;
     HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
-    // 1. Co_p_B per row
-    PrepArgs pa{a->x, a->p, (float4*)ctx->pos4.p, rows, a->np};
-    HIPCHK(timed(ctx, "prep_rows", [&] { return launch_prep_rows(pa, ctx->stream); }));
-    // 2. latent hoisting (latent = p[.][17:] as fp32)
-    const long long stride = a->latent_mode == 0 ? (long long)(a->N + 1) * a->np : (long long)a->np;
-    int rc = run_hoist<double>(ctx, net, a->p + 17, stride, n_inst, (float*)ctx->c13.p);
-    if (rc) return rc;
-    // 3. network forward + position gradient
-    rc = run_sdf(ctx, net, rows, (const float4*)ctx->pos4.p, (const float*)ctx->c13.p,
-                 a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows);
-    if (rc) return rc;
-    // 4. dynamics / cost / constraints
+    // dynamics / cost / FOV constraints (independent of the network): forked onto the low-priority
+    // aux stream so they fill the CUs the SDF kernel leaves idle (its tail), joined at the end
     LinArgs la{};
-    la.x = a->x; la.u = a->u; la.p = a->p; la.dt = a->dt; la.sdf = sdf4;
+    la.x = a->x; la.u = a->u; la.p = a->p; la.dt = a->dt;
     la.xn = a->xn; la.AB = a->AB; la.y = a->y; la.Jy = a->Jy; la.yN = a->yN; la.JyN = a->JyN; la.h = a->h; la.Jh = a->Jh;
     la.B = a->B; la.N = a->N; la.np = a->np;
     la.m.gamma = mdl->gamma; la.m.roll = mdl->roll; la.m.pitch = mdl->pitch; la.m.wz = mdl->wz; la.m.g = mdl->g;
@@ -620,7 +638,32 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
         la.m.fov_off[i] = mdl->B_R_C[0 * 3 + i] * mdl->B_p_C[0] + mdl->B_R_C[1 * 3 + i] * mdl->B_p_C[1] +
                           mdl->B_R_C[2 * 3 + i] * mdl->B_p_C[2] + (i == 0 ? mdl->fov_const_offset : 0.0);
     la.m.max_df = net->host.max_df;
-    HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }));
+    auto fork_lin = [&]() -> int {
+        HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
+        HIPCHK(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
+        HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->aux); }, ctx->aux));
+        HIPCHK(hipEventRecord(ctx->ev_join, ctx->aux));
+        return SDFNMPC_OK;
+    };
+    int rc;
+    if (ctx->lin_first && (rc = fork_lin())) return rc;
+    // 2. latent hoisting (latent = p[.][17:] as fp32)
+    const long long stride = a->latent_mode == 0 ? (long long)(a->N + 1) * a->np : (long long)a->np;
+    rc = run_hoist<double>(ctx, net, a->p + 17, stride, n_inst, (float*)ctx->c13.p);
+    if (rc) return rc;
+    if (!ctx->lin_first && (rc = fork_lin())) return rc;
+    // 3. network forward + position gradient, with the sdf row of h / J_h in its epilogue
+    SdfArgs cons{};
+    cons.x = a->x;
+    cons.p = a->p;
+    cons.np = a->np;
+    cons.h = a->h;
+    cons.Jh = a->Jh;
+    cons.max_df = net->host.max_df;
+    rc = run_sdf(ctx, net, rows, nullptr, (const float*)ctx->c13.p,
+                 a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows, &cons);
+    if (rc) return rc;
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
     return SDFNMPC_OK;
 }
 

@@ -17,28 +17,18 @@ struct LinArgs {
     const double* u;   // [B][N][4]
     const double* p;   // [B][N+1][np]
     const double* dt;  // [N]
-    const float4* sdf; // [B][N+1] (df, d df / d Co_p_B)
     double* xn;        // [B][N][10]
     double* AB;        // [B][N][14][10]   column j = d x_{k+1} / d (x,u)_j
     double* y;         // [B][N][11]
     double* Jy;        // [B][N][14][11]
     double* yN;        // [B][4]
     double* JyN;       // [B][10][4]
-    double* h;         // [B][N+1][3]
-    double* Jh;        // [B][N+1][10][3]
+    double* h;         // [B][N+1][3]      rows 0,1 (row 2: sdf_mlp_kernel)
+    double* Jh;        // [B][N+1][10][3]  rows 0,1
     QuadModel m;
     int B, N, np;
 };
 
-struct PrepArgs {
-    const double* x;  // [rows][10]
-    const double* p;  // [rows][np]
-    float4* pos;      // [rows]
-    long long rows;
-    int np;
-};
-
 hipError_t launch_linearize(const LinArgs& a, hipStream_t s);
-hipError_t launch_prep_rows(const PrepArgs& a, hipStream_t s);
 
 }  // namespace sdfn

@@ -12,8 +12,8 @@
 //
 // Derivatives are forward-mode dual numbers with ONE tangent per lane: a node is served by 16
 // lanes, lane t < 14 carrying d/d(x,u)_t, so every lane writes one Jacobian column (column-major
-// blocks, 80-112 contiguous bytes per lane).  The SDF entries use the network output of
-// sdf_mlp_kernel: d s / d W_p_B = flag * (d df / d Co_p_B) W_R_Co^T.
+// blocks, 80-112 contiguous bytes per lane).  The sdf row of h / J_h is written by sdf_mlp_kernel's
+// epilogue, so this kernel is independent of the network and runs concurrently with it.
 #include <hip/hip_runtime.h>
 
 #include "lin_kernels.h"
@@ -42,18 +42,25 @@ __device__ __forceinline__ dd datan2(dd y, dd x) {
     return {atan2(y.v, x.v), (x.v * y.t - y.v * x.t) / den};
 }
 
-// f_expl of the 'att' model; sr/cr/sp/cp = sin/cos of roll, pitch (constant over RK4 stages)
+// 1 / sqrt(a) as a dual number: one fp64 sqrt + one division
+__device__ __forceinline__ dd drsqrt(dd a) {
+    const double r = 1.0 / sqrt(a.v);
+    return {r, -0.5 * a.t * r * r * r};
+}
+
+// f_expl of the 'att' model; sr/cr/sp/cp = sin/cos of roll, pitch (constant over RK4 stages).
+// q = x[3:7] / |x[3:7]|; theta_z = atan2(q3, q0) is scale-invariant, so
+// (cos, sin)(theta_z) = (x3, x6) / |(x3, x6)| without forming q first.
 __device__ __forceinline__ void quad_f(const QuadModel& m, const dd* x, dd gamma, dd sr, dd cr, dd sp, dd cp, dd wz,
-                                       dd* f, dd* W_a2) {
-    const dd nq = dsqrt(x[3] * x[3] + x[4] * x[4] + (x[5] * x[5] + x[6] * x[6]));
-    const dd q0 = x[3] / nq, q1 = x[4] / nq, q2 = x[5] / nq, q3 = x[6] / nq;
-    // theta_z = atan2(q3, q0); (cos, sin)(theta_z) = (q0, q3) / |(q0, q3)|
+                                       dd* f) {
+    const dd inv = drsqrt(x[3] * x[3] + x[4] * x[4] + (x[5] * x[5] + x[6] * x[6]));
+    const dd s03 = x[3] * x[3] + x[6] * x[6];
     dd c, s;
-    const dd n03 = dsqrt(q0 * q0 + q3 * q3);
-    if (n03.v > 0.0) {
-        c = q0 / n03;
-        s = q3 / n03;
-    } else {
+    if (s03.v > 0.0) {
+        const dd r = drsqrt(s03);
+        c = x[3] * r;
+        s = x[6] * r;
+    } else {  // atan2(0, 0) = 0
         c = C(1.0);
         s = C(0.0);
     }
@@ -61,17 +68,23 @@ __device__ __forceinline__ void quad_f(const QuadModel& m, const dd* x, dd gamma
     const dd b0 = cr * sp * gamma, b1 = -sr * gamma, b2 = cr * cp * gamma;
     // W_R_V = quat2rot([c,0,0,s]) (math.py:11-19)
     const dd r11 = c * c - s * s, r21 = (c * s) * 2.0, r33 = c * c + s * s;
+    const dd hw = (wz * inv) * 0.5;  // hamilton_prod(q, [0,0,0,wz]) / 2 with q = x * inv
     f[0] = x[7];
     f[1] = x[8];
     f[2] = x[9];
-    f[3] = (-q3 * wz) * 0.5;  // hamilton_prod(q, [0,0,0,wz]) / 2
-    f[4] = (q2 * wz) * 0.5;
-    f[5] = (-q1 * wz) * 0.5;
-    f[6] = (q0 * wz) * 0.5;
+    f[3] = -(x[6] * hw);
+    f[4] = x[5] * hw;
+    f[5] = -(x[4] * hw);
+    f[6] = x[3] * hw;
     f[7] = r11 * b0 - r21 * b1;
     f[8] = r21 * b0 + r11 * b1;
     f[9] = r33 * b2 - C(m.g);
-    if (W_a2) *W_a2 = f[9];
+}
+
+// (q_d (x) invert(q))[3] with q = x[3:7]/|x[3:7]| (|q| = 1 up to rounding): quad_rollpitchyawrate.py:372
+__device__ __forceinline__ dd qerr3(const dd* x, const double* qd) {
+    const dd inv = drsqrt(x[3] * x[3] + x[4] * x[4] + (x[5] * x[5] + x[6] * x[6]));
+    return (((x[3] * qd[3] + x[4] * qd[2]) - x[5] * qd[1]) - x[6] * qd[0]) * inv;
 }
 
 __global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
@@ -105,15 +118,16 @@ __global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
         //      accumulation x_out = x + (h b_1) k_1 + ... + (h b_4) k_4, stage input x + (h a_s) k_{s-1}
         const double dt = A.dt[k];
         const double hb[4] = {dt / 6, dt / 3, dt / 3, dt / 6}, ha[4] = {0.0, dt / 2, dt / 2, dt};
-        dd xo[10], kk[10], tmp[10], W_a2;
-        quad_f(m, X, gamma, sr, cr, sp, cp, wz, kk, &W_a2);
+        dd xo[10], kk[10], tmp[10];
+        quad_f(m, X, gamma, sr, cr, sp, cp, wz, kk);
+        const dd W_a2 = kk[9];
 #pragma unroll
         for (int i = 0; i < 10; ++i) xo[i] = X[i] + kk[i] * hb[0];
 #pragma unroll
         for (int st = 1; st < 4; ++st) {
 #pragma unroll
             for (int i = 0; i < 10; ++i) tmp[i] = X[i] + kk[i] * ha[st];
-            quad_f(m, tmp, gamma, sr, cr, sp, cp, wz, kk, nullptr);
+            quad_f(m, tmp, gamma, sr, cr, sp, cp, wz, kk);
 #pragma unroll
             for (int i = 0; i < 10; ++i) xo[i] = xo[i] + kk[i] * hb[st];
         }
@@ -125,12 +139,7 @@ __global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
         }
         // ---- NONLINEAR_LS residual (quad_rollpitchyawrate.py:370-377)
         const double* pr = A.p + r * A.np;
-        const dd nq = dsqrt(X[3] * X[3] + X[4] * X[4] + (X[5] * X[5] + X[6] * X[6]));
-        const dd q0 = X[3] / nq, q1 = X[4] / nq, q2 = X[5] / nq, q3 = X[6] / nq;
-        const dd nq2 = dsqrt(q0 * q0 + q1 * q1 + (q2 * q2 + q3 * q3));  // invert(q) = conj(q) / |q|
-        const dd i0 = q0 / nq2, i1 = -q1 / nq2, i2 = -q2 / nq2, i3 = -q3 / nq2;
-        const double d0 = pr[13], d1 = pr[14], d2 = pr[15], d3 = pr[16];  // p_idx.q_d
-        const dd qe3 = ((i3 * d0 + i2 * d1) - i1 * d2) + i0 * d3;         // (q_d (x) q^-1)[3]
+        const dd qe3 = qerr3(X, pr + 13);  // p_idx.q_d
         dd Y[11] = {X[0], X[1], X[2], qe3, X[7], X[8], X[9], roll, pitch, wz, W_a2};
         double* Jyc = A.Jy + (s * 14 + t) * 11;
 #pragma unroll
@@ -141,12 +150,7 @@ __global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
     } else {
         // ---- terminal residual y_N = [p, q_e[3]]
         const double* pr = A.p + r * A.np;
-        const dd nq = dsqrt(X[3] * X[3] + X[4] * X[4] + (X[5] * X[5] + X[6] * X[6]));
-        const dd q0 = X[3] / nq, q1 = X[4] / nq, q2 = X[5] / nq, q3 = X[6] / nq;
-        const dd nq2 = dsqrt(q0 * q0 + q1 * q1 + (q2 * q2 + q3 * q3));
-        const dd i0 = q0 / nq2, i1 = -q1 / nq2, i2 = -q2 / nq2, i3 = -q3 / nq2;
-        const double d0 = pr[13], d1 = pr[14], d2 = pr[15], d3 = pr[16];
-        const dd qe3 = ((i3 * d0 + i2 * d1) - i1 * d2) + i0 * d3;
+        const dd qe3 = qerr3(X, pr + 13);
         const dd Y[4] = {X[0], X[1], X[2], qe3};
         if (t < 10) {
             double* J = A.JyN + (b * 10 + t) * 4;
@@ -167,42 +171,19 @@ __global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
     const dd cz = (e0 * R[2] + e1 * R[5]) + e2 * R[8] + C(m.fov_off[2]);
     const dd hf = datan2(cy, cx) * flag;
     const dd vf = datan2(cz, dsqrt(cx * cx + cy * cy)) * flag;
-    const float4 sd = A.sdf[r];
-    if (t < 10) {
+    if (t < 10) {  // rows 0, 1; row 2 (sdf) is written by the SDF kernel's epilogue
         double* J = A.Jh + (r * 10 + t) * 3;
         J[0] = hf.t;
         J[1] = vf.t;
-        J[2] = (t < 3) ? flag * (((double)sd.y * R[t * 3 + 0] + (double)sd.z * R[t * 3 + 1]) + (double)sd.w * R[t * 3 + 2])
-                       : 0.0;
     }
     if (t == 0) A.h[r * 3 + 0] = hf.v;
     if (t == 1) A.h[r * 3 + 1] = vf.v;
-    if (t == 2) A.h[r * 3 + 2] = flag * (double)sd.x + (1.0 - flag) * m.max_df;
-}
-
-// Co_p_B = W_R_Co^T (W_p_B - W_p_Co) in fp64, handed to the network as fp32 (L4CasADi converts the
-// CasADi double arguments to a float tensor) -- gen_model.py:46-51.
-__global__ __launch_bounds__(256) void prep_rows_kernel(PrepArgs A) {
-    const long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= A.rows) return;
-    const double* x = A.x + r * 10;
-    const double* p = A.p + r * A.np;
-    const double e0 = x[0] - p[1], e1 = x[1] - p[2], e2 = x[2] - p[3];
-    const double* R = p + 4;
-    A.pos[r] = make_float4((float)((e0 * R[0] + e1 * R[3]) + e2 * R[6]), (float)((e0 * R[1] + e1 * R[4]) + e2 * R[7]),
-                           (float)((e0 * R[2] + e1 * R[5]) + e2 * R[8]), 0.0f);
 }
 
 hipError_t launch_linearize(const LinArgs& a, hipStream_t s) {
     const long long rows = (long long)a.B * (a.N + 1);
     if (rows <= 0) return hipSuccess;
     hipLaunchKernelGGL(linearize_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_prep_rows(const PrepArgs& a, hipStream_t s) {
-    if (a.rows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(prep_rows_kernel, dim3((unsigned)((a.rows + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

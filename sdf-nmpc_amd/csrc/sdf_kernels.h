@@ -17,7 +17,6 @@ constexpr int N1 = 256, N2 = 256, N3 = 128, N4 = 64;
 constexpr int C13_STRIDE = N1 + N3;      // hoisted [c1 | c3] per instance
 constexpr int SE = 92;                   // LDS row strides (floats): stride/4 odd -> conflict-free b128
 constexpr int SA = 260;
-constexpr int HOIST_INST = 8;
 
 // Packed operand: OUT[M x N] = IN[M x K] . Wsrc^T, Wsrc(j, k) = weight of output j, input k.
 // Layout [cb][g][lane][4] with value Wsrc(cb*32 + (lane&31), (lane>>5)*K/2 + 4g + i), zero-padded.
@@ -43,9 +42,17 @@ struct SdfArgs {
     const float* w5;
     const float4* emb_tab;  // [NE] (dirs[:, d] * 2^f) for m in the sin/cos ranges, else 0
     const float* c13;       // [n_inst][C13_STRIDE]
-    const float4* pos;      // [rows] (Co_p_B as fp32, pad)
+    const float4* pos;      // [rows] (Co_p_B as fp32, pad)           -- or, when x != NULL:
+    const double* x;        // [rows][10] iterate; Co_p_B = W_R_Co^T (x[0:3] - W_p_Co) from p (fp64 -> fp32)
     float4* out;            // [rows] (df, d df/d pos)
     float* grad_latent;     // [rows][L] (latent-gradient variant only)
+    // optional fused constraint epilogue (sdfnmpc_linearize): h[r][2] = flag df + (1 - flag) max_df,
+    // Jh[r][j][2] = flag (d df / d Co_p_B) W_R_Co^T (j < 3), 0 (j >= 3)   -- gen_model.py:46-61
+    const double* p;        // [rows][np] stage parameters (flag at 0, W_R_Co row-major at 4..12)
+    double* h;              // [rows][3]      (NULL: no constraint epilogue)
+    double* Jh;             // [rows][10][3]
+    double max_df;
+    int np;
     float b5;
     float w0;
     int rows;
@@ -54,13 +61,16 @@ struct SdfArgs {
 
 template <typename T>
 struct HoistArgs {
-    const T* latent;   // latent of instance i at latent[i * stride + k]
+    const T* latent;     // latent of instance i at latent[i * stride + k]
     long long stride;
-    const float* WzT;  // [L][C13_STRIDE] = [W1[:, E:]^T | W3[:, N2+E:]^T]
-    const float* bias; // [C13_STRIDE] = [b1 | b3]
-    float* c13;        // [n_inst][C13_STRIDE]
+    const float4* wpk;   // packed operand Wsrc(j, k) = [W1[:, E:] ; W3[:, N2+E:]](j, k), N = C13_STRIDE, K = L
+    const float* bias;   // [C13_STRIDE] = [b1 | b3]
+    float* c13;          // [n_inst][C13_STRIDE]
     int n_inst;
 };
+constexpr int HOIST_ROWS = 32;                    // instances per hoist workgroup (one MFMA row block)
+constexpr int HOIST_COLS = 128;                   // output columns per hoist workgroup (4 waves x 32)
+constexpr int SZ = L + 4;                         // LDS row stride of the latent tile
 
 size_t sdf_lds_bytes(int M);
 hipError_t sdf_set_lds_limits();

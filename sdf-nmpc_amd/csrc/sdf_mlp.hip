@@ -37,28 +37,44 @@ __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * 
 // acc[rb][c] += IN[rb*32 .. +32][0..K) . Wpk(cb = cb0 + 4c)  for every row block rb and the wave's
 // column blocks.  Feature k of k-step s, lane half h is k = h*K/2 + s (any bijection works as long as
 // A and B agree; this one makes both operands 16-B contiguous per lane over 4 k-steps).
-template <int RB, int NCB, int K>
+// Weights (L2-resident) are prefetched PF groups ahead in a register ring, activations (LDS) one ahead.
+// Only groups [G0, G1) of the K/8 groups of 4 k-steps are accumulated (K-split between waves).
+template <int RB, int NCB, int K, int CBS = 4, int G0 = 0, int G1 = K / 8>
 __device__ __forceinline__ void gemm(f32x16 (&acc)[RB][NCB], const float* lds, int stride,
                                      const float4* __restrict__ wpk, int cb0, int lane) {
     constexpr int G = K / 8;
+    constexpr int NG = G1 - G0;
+    constexpr int PF = (NG < 3) ? NG : 3;
+    static_assert(0 <= G0 && G0 < G1 && G1 <= G, "group range");
     static_assert(K % 8 == 0, "K must be a multiple of 8");
     const int r = lane & 31, h = lane >> 5;
     const float* abase = lds + r * stride + h * (K / 2);
     const float4* bbase = wpk + (size_t)cb0 * G * 64 + lane;
-    float4 a[RB], b[NCB];
+    float4 bring[PF][NCB];
+    float4 a[RB];
 #pragma unroll
-    for (int rb = 0; rb < RB; ++rb) a[rb] = *(const float4*)(abase + rb * 32 * stride);
+    for (int q = 0; q < PF; ++q)
 #pragma unroll
-    for (int c = 0; c < NCB; ++c) b[c] = bbase[(size_t)c * 4 * G * 64];
+        for (int c = 0; c < NCB; ++c) bring[q][c] = bbase[(size_t)c * CBS * G * 64 + (G0 + q) * 64];
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-        float4 an[RB], bn[NCB];
-        if (g + 1 < G) {
+    for (int rb = 0; rb < RB; ++rb) a[rb] = *(const float4*)(abase + rb * 32 * stride + 4 * G0);
+#pragma unroll
+    for (int q = 0; q < NG; ++q) {
+        const int g = G0 + q;
+        float4 b[NCB], an[RB];
+#pragma unroll
+        for (int c = 0; c < NCB; ++c) b[c] = bring[q % PF][c];
+        if (q + PF < NG) {
+#pragma unroll
+            for (int c = 0; c < NCB; ++c) bring[q % PF][c] = bbase[(size_t)c * CBS * G * 64 + (g + PF) * 64];
+        }
+        if (q + 1 < NG) {
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) an[rb] = *(const float4*)(abase + rb * 32 * stride + 4 * (g + 1));
-#pragma unroll
-            for (int c = 0; c < NCB; ++c) bn[c] = bbase[(size_t)c * 4 * G * 64 + (g + 1) * 64];
         }
+        // keep the prefetches issued here: the scheduler would otherwise sink every load to just
+        // before its first use (one MFMA group ahead), exposing the L2 latency
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -68,11 +84,10 @@ __device__ __forceinline__ void gemm(f32x16 (&acc)[RB][NCB], const float* lds, i
                 acc[rb][c] = mfma(a[rb].z, b[c].z, acc[rb][c]);
                 acc[rb][c] = mfma(a[rb].w, b[c].w, acc[rb][c]);
             }
-        if (g + 1 < G) {
+        __builtin_amdgcn_sched_barrier(0);
+        if (q + 1 < NG) {
 #pragma unroll
             for (int rb = 0; rb < RB; ++rb) a[rb] = an[rb];
-#pragma unroll
-            for (int c = 0; c < NCB; ++c) b[c] = bn[c];
         }
     }
 }
@@ -88,11 +103,11 @@ __device__ __forceinline__ void zero(f32x16 (&acc)[RB][NCB]) {
 }
 
 // accumulator init from a per-column vector (bias)
-template <int RB, int NCB>
+template <int RB, int NCB, int CBS = 4>
 __device__ __forceinline__ void init_bias(f32x16 (&acc)[RB][NCB], const float* __restrict__ v, int cb0, int lane) {
 #pragma unroll
     for (int c = 0; c < NCB; ++c) {
-        const float bv = v[(cb0 + 4 * c) * 32 + (lane & 31)];
+        const float bv = v[(cb0 + CBS * c) * 32 + (lane & 31)];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -167,7 +182,17 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
     if (tid < M) {
         const int r = row0 + tid;
         const int rr = r < A.rows ? r : A.rows - 1;
-        const float4 p = A.pos[rr];
+        float4 p;
+        if (A.x) {  // Co_p_B = W_R_Co^T (W_p_B - W_p_Co) in fp64, handed over as fp32 (gen_model.py:46-51)
+            const double* xr = A.x + (size_t)rr * 10;
+            const double* pr = A.p + (size_t)rr * A.np;
+            const double* R = pr + 4;
+            const double e0 = xr[0] - pr[1], e1 = xr[1] - pr[2], e2 = xr[2] - pr[3];
+            p = make_float4((float)((e0 * R[0] + e1 * R[3]) + e2 * R[6]), (float)((e0 * R[1] + e1 * R[4]) + e2 * R[7]),
+                            (float)((e0 * R[2] + e1 * R[5]) + e2 * R[8]), 0.0f);
+        } else {
+            p = A.pos[rr];
+        }
         posb[tid * 4 + 0] = r < A.rows ? p.x : 0.0f;
         posb[tid * 4 + 1] = r < A.rows ? p.y : 0.0f;
         posb[tid * 4 + 2] = r < A.rows ? p.z : 0.0f;
@@ -227,12 +252,13 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
     gemm<RB, 1, KE>(acc1, Ebuf, SE, A.wF3e, w, lane);
     act_fwd(acc1, d3, Abuf, SA, w0, w, lane);
     __syncthreads();
-    // ---- L4: h4 = sin(w0 (W4 h3 + b4))                  [M x 64], waves 0,1 (col block w)
+    // ---- L4: h4 = sin(w0 (W4 h3 + b4))                  [M x 64], waves 2,3 (col block w-2)
     //      delta4 = (W5 * cos(t4)) * w0 -> Bbuf, h4 -> Ebuf
-    if (w < 2) {
-        init_bias(acc1, A.b4, w, lane);
-        gemm<RB, 1, N3>(acc1, Abuf, SA, A.wF4, w, lane);
-        const float w5 = A.w5[w * 32 + col];
+    if (w >= 2) {
+        const int cb4 = w - 2;
+        init_bias(acc1, A.b4, cb4, lane);
+        gemm<RB, 1, N3>(acc1, Abuf, SA, A.wF4, cb4, lane);
+        const float w5 = A.w5[cb4 * 32 + col];
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
 #pragma unroll
@@ -240,8 +266,8 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
                 float s, co;
                 sdfn_sincosf(w0 * acc1[rb][0][i], &s, &co);
                 const int row = rb * 32 + acc_row(i, hh);
-                Ebuf[row * SE + w * 32 + col] = s;
-                Bbuf[row * SA + w * 32 + col] = (w5 * co) * w0;
+                Ebuf[row * SE + cb4 * 32 + col] = s;
+                Bbuf[row * SA + cb4 * 32 + col] = (w5 * co) * w0;
             }
     }
     __syncthreads();
@@ -263,9 +289,16 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
     zero(acc2);
     gemm<RB, 2, N3>(acc2, Abuf, SA, A.wB3, w, lane);
     act_bwd(acc2, d2, Bbuf, SA, w0, w, lane);
-    f32x16 de[RB][1];
+    // d e = delta3 W3e (+ delta1 W1e below), [M x 96]: K-split so every wave does the same MFMA count:
+    // waves 0..2 own column block w over groups [0, 3G/4), wave 3 all three blocks over [3G/4, G)
+    f32x16 de[RB][1], de3[RB][3];
     zero(de);
-    if (w < 3) gemm<RB, 1, N3>(de, Abuf, SA, A.wB3e, w, lane);
+    if (w < 3) {
+        gemm<RB, 1, N3, 4, 0, 3 * N3 / 32>(de, Abuf, SA, A.wB3e, w, lane);
+    } else {
+        zero(de3);
+        gemm<RB, 3, N3, 1, 3 * N3 / 32, N3 / 8>(de3, Abuf, SA, A.wB3e, 0, lane);
+    }
     f32x16 dz[RB][1];
     if constexpr (LATENT_GRAD) {
         zero(dz);
@@ -277,8 +310,9 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
     gemm<RB, 2, N2>(acc2, Bbuf, SA, A.wB2, w, lane);
     act_bwd(acc2, d1, Abuf, SA, w0, w, lane);
     __syncthreads();
-    // ---- b1: d e += delta1 W1e ; d z += delta1 W1z
-    if (w < 3) gemm<RB, 1, N1>(de, Abuf, SA, A.wB1e, w, lane);
+    // ---- b1: d e += delta1 W1e (same K-split) ; d z += delta1 W1z
+    if (w < 3) gemm<RB, 1, N1, 4, 0, 3 * N1 / 32>(de, Abuf, SA, A.wB1e, w, lane);
+    else gemm<RB, 3, N1, 1, 3 * N1 / 32, N1 / 8>(de3, Abuf, SA, A.wB1e, 0, lane);
     if constexpr (LATENT_GRAD) {
         gemm<RB, 1, N1>(dz, Abuf, SA, A.wB1z, w, lane);
 #pragma unroll
@@ -288,6 +322,23 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
                 const int r = row0 + rb * 32 + acc_row(i, hh);
                 if (r < A.rows) A.grad_latent[(size_t)r * L + w * 32 + col] = dz[rb][0][i];
             }
+    }
+    // ---- wave 3 hands its K-slice of d e to the owners of the column blocks (through Abuf)
+    __syncthreads();  // everyone is done reading delta1 in Abuf
+    if (w == 3) {
+#pragma unroll
+        for (int c = 0; c < 3; ++c)
+#pragma unroll
+            for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) Abuf[(rb * 32 + acc_row(i, hh)) * SA + c * 32 + col] = de3[rb][c][i];
+    }
+    __syncthreads();
+    if (w < 3) {
+#pragma unroll
+        for (int rb = 0; rb < RB; ++rb)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) de[rb][0][i] += Abuf[(rb * 32 + acc_row(i, hh)) * SA + w * 32 + col];
     }
     // ---- embedding backward: grad_c = sum_m (d e_m * g_m) * P[m][c]  (+ d e_c for m < 3)
     //      partials per (row, c, m) -> Ebuf..Bbuf (contiguous, both free), then one thread per
@@ -325,36 +376,49 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
         posb[(tid / 3) * 4 + 1 + tid % 3] = s;
     }
     __syncthreads();
-    if (tid < M && row0 + tid < A.rows)
-        A.out[row0 + tid] = make_float4(df, posb[tid * 4 + 1], posb[tid * 4 + 2], posb[tid * 4 + 3]);
+    if (tid < M && row0 + tid < A.rows) {
+        const int r = row0 + tid;
+        const float g0 = posb[tid * 4 + 1], g1 = posb[tid * 4 + 2], g2 = posb[tid * 4 + 3];
+        A.out[r] = make_float4(df, g0, g1, g2);
+        if (A.h) {  // sdf row of the constraint vector and its Jacobian (gen_model.py:46-61)
+            const double* pr = A.p + (size_t)r * A.np;
+            const double flag = pr[0];
+            const double* R = pr + 4;  // W_R_Co row-major (== casadi reshape((3,3)).T)
+            A.h[(size_t)r * 3 + 2] = flag * (double)df + (1.0 - flag) * A.max_df;
+            double* J = A.Jh + (size_t)r * 30 + 2;
+#pragma unroll
+            for (int j = 0; j < 10; ++j)
+                J[j * 3] = (j < 3) ? flag * (((double)g0 * R[j * 3 + 0] + (double)g1 * R[j * 3 + 1]) + (double)g2 * R[j * 3 + 2])
+                                   : 0.0;
+        }
+    }
 }
 
-// c13[i] = [W1[:, E:] z_i + b1 | W3[:, n2+E:] z_i + b3]   (latent hoisting, per instance)
-// z_i = (float) latent source (fp64 p vector at stride, or fp32 array)
+// c13[i] = [W1[:, E:] z_i + b1 | W3[:, N2+E:] z_i + b3]   (latent hoisting, per instance)
+// A [n_inst x L] . [L x C13_STRIDE] GEMM on the same fp32 MFMA: workgroup (ib, jb) = 32 instances x
+// 128 output columns, one 32-column block per wave; bias as the initial accumulator.
+// z_i = (float) latent source (fp64 stage parameters at a stride, or an fp32 array).
 template <typename T>
-__global__ __launch_bounds__(C13_STRIDE) void sdf_hoist_kernel(HoistArgs<T> A) {
-    __shared__ float z[HOIST_INST][L];
-    const int i0 = blockIdx.x * HOIST_INST;
-    for (int t = threadIdx.x; t < HOIST_INST * L; t += blockDim.x) {
+__global__ __launch_bounds__(256) void sdf_hoist_kernel(HoistArgs<T> A) {
+    __shared__ __align__(16) float z[HOIST_ROWS * SZ];
+    const int i0 = blockIdx.x * HOIST_ROWS;
+    for (int t = threadIdx.x; t < HOIST_ROWS * L; t += blockDim.x) {
         const int ii = t / L, k = t % L;
         const int inst = i0 + ii < A.n_inst ? i0 + ii : A.n_inst - 1;
-        z[ii][k] = (float)A.latent[(size_t)inst * A.stride + k];
+        z[ii * SZ + k] = (float)A.latent[(size_t)inst * A.stride + k];
     }
     __syncthreads();
-    const int j = threadIdx.x;  // 0 .. n1+n3-1
-    const float* wt = A.WzT + j;  // [L][C13_STRIDE]
-    float acc[HOIST_INST];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int cb = blockIdx.y * (HOIST_COLS / 32) + w;  // global 32-column block
+    f32x16 acc[1][1];
+    init_bias<1, 1>(acc, A.bias, cb, lane);
+    gemm<1, 1, L>(acc, z, SZ, A.wpk, cb, lane);
+    const int col = cb * 32 + (lane & 31), hh = lane >> 5;
 #pragma unroll
-    for (int ii = 0; ii < HOIST_INST; ++ii) acc[ii] = 0.0f;
-    for (int k = 0; k < L; ++k) {
-        const float wv = wt[(size_t)k * C13_STRIDE];
-#pragma unroll
-        for (int ii = 0; ii < HOIST_INST; ++ii) acc[ii] = fmaf(wv, z[ii][k], acc[ii]);
+    for (int i = 0; i < 16; ++i) {
+        const int inst = i0 + acc_row(i, hh);
+        if (inst < A.n_inst) A.c13[(size_t)inst * C13_STRIDE + col] = acc[0][0][i];
     }
-    const float b = A.bias[j];
-#pragma unroll
-    for (int ii = 0; ii < HOIST_INST; ++ii)
-        if (i0 + ii < A.n_inst) A.c13[(size_t)(i0 + ii) * C13_STRIDE + j] = acc[ii] + b;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -387,7 +451,9 @@ hipError_t sdf_set_lds_limits() {
 template <typename T>
 hipError_t launch_hoist(const HoistArgs<T>& a, hipStream_t s) {
     if (a.n_inst <= 0) return hipSuccess;
-    hipLaunchKernelGGL((sdf_hoist_kernel<T>), dim3((a.n_inst + HOIST_INST - 1) / HOIST_INST), dim3(C13_STRIDE), 0, s, a);
+    static_assert(C13_STRIDE % HOIST_COLS == 0, "hoist column split");
+    hipLaunchKernelGGL((sdf_hoist_kernel<T>), dim3((a.n_inst + HOIST_ROWS - 1) / HOIST_ROWS, C13_STRIDE / HOIST_COLS),
+                       dim3(256), 0, s, a);
     return hipGetLastError();
 }
 template hipError_t launch_hoist<float>(const HoistArgs<float>&, hipStream_t);

@@ -90,7 +90,7 @@ for M in (32, 64):
         _lib.linearize(ctx, net, model, B, N, 145, bufs)
     ctx.synchronize()
     wall = (time.perf_counter() - t0) / K
-    st = {k: ctx.kernel_stats(k) for k in ("prep_rows", "sdf_hoist", "sdf_mlp", "linearize")}
+    st = {k: ctx.kernel_stats(k) for k in ("sdf_hoist", "sdf_mlp", "linearize")}
     ctx.enable_timing(False)
     sdf_ms = st["sdf_mlp"][0] / st["sdf_mlp"][1]
     flops = (B * (N + 1) * 553984) / (sdf_ms * 1e-3)
