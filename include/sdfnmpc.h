@@ -21,6 +21,12 @@
  *                                      and Jacobian (model/quad_rollpitchyawrate.py:370-377), and the
  *                                      constraint vector h = [hfov, vfov, sdf] with its Jacobian
  *                                      (model/cost_const_helpers.py:48-75, gen_model.py:46-70)
+ *   sdfnmpc_qp_solve                   the feedback phase of the same SQP-RTI step: the QP acados
+ *                                      builds (NONLINEAR_LS Gauss-Newton + levenberg_marquardt, soft
+ *                                      h rows, input boxes, ocp.py:54-120) and hands to HPIPM
+ *                                      (FULL_CONDENSING_HPIPM, ocp.py:113-116), batched over instances
+ *   sdfnmpc_rti_apply                  the SQP-RTI full step x <- x + dx, u <- u + du and u_0
+ *                                      (solve_for_x0's return value, ocp.py:169)
  *   sdfnmpc_shooting_grid              Ocp.__init__ shooting nodes / time steps (ocp.py:18-27)
  *
  * The CasADi external-function symbols that acados links (sdf_l4c, jac_sdf_l4c, ...) are in
@@ -81,6 +87,37 @@ typedef struct {
     float* sdf;       /* [B][N+1][4]     optional: (df, d df / d Co_p_B); NULL = internal buffer */
 } sdfnmpc_lin_args;
 
+/* QP model data and solver options (defaults in sdf-nmpc_amd/model.py / ocp.py) */
+typedef struct {
+    double lbu[4], ubu[4]; /* input box (model/quad_rollpitchyawrate.py:380-381) */
+    double lh[3], uh[3];   /* h bounds: +-fov_ratio*fov, [size.xy+bound_margin, max_df+0.2] */
+    double zl[3], Zl[3];   /* L1 / L2 slack penalties of the soft h rows, lower == upper (ocp.py:85-92) */
+    double lm;             /* levenberg_marquardt (ocp.py:120, mpc.lm_reg) */
+    int cost_scaling;      /* 1: stage cost and slack penalties x dt_k, terminal x 1 (acados default) */
+    int max_iter;          /* qp_solver_iter_max (ocp.py:115) */
+    double tol;            /* IPM stop: mean complementarity and max primal residual below tol */
+} sdfnmpc_qp_opts;
+
+/* Batched QP of the RTI feedback phase, built from sdfnmpc_linearize outputs. */
+typedef struct {
+    int B, N;
+    const double *xn, *AB, *y, *Jy, *yN, *JyN, *h, *Jh; /* sdfnmpc_lin_args outputs */
+    const double* x;     /* [B][N+1][10] iterate the QP was built at */
+    const double* u;     /* [B][N][4] */
+    const double* x0;    /* [B][10] measured state (Ocp.solve x0) */
+    const double* yref;  /* [B][N][11] stage references (Ocp.solve y[k]) */
+    const double* W;     /* [B][N][11] diagonal weights (Ocp.solve W[k], set as np.diag) */
+    const double* yNref; /* [B][4] */
+    const double* WN;    /* [B][4] */
+    const double* dt;    /* [N] */
+    double* dx;          /* [B][N+1][10] solution: the RTI step */
+    double* du;          /* [B][N][4] */
+    double* slack;       /* [B][N+1][3][2] optional: (sl, su) of the soft rows */
+    int* status;         /* [B] optional: 0 converged, 1 max_iter reached */
+    int* iters;          /* [B] optional */
+    double* res;         /* [B][2] optional: (mean complementarity, max primal residual) */
+} sdfnmpc_qp_args;
+
 int sdfnmpc_abi_version(void);
 const char* sdfnmpc_last_error(void);
 
@@ -123,6 +160,12 @@ int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, co
 /* ---- batched preparation phase ---- */
 int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* model,
                       const sdfnmpc_lin_args* args);
+
+/* ---- batched QP (feedback phase) and the RTI step ---- */
+int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* opts, const sdfnmpc_qp_args* args);
+/* x[B][N+1][10] += dx, u[B][N][4] += du, u0[B][4] = u[:, 0] (u0 may be NULL) */
+int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, const double* dx, const double* du,
+                      double* u0);
 
 /* ---- shooting grid (host, bit-exact numpy.linspace/diff semantics of ocp.py:21-27) ---- */
 int sdfnmpc_shooting_grid(int N, double T, int uniform, int nb_short_nodes, double dt_short, double* nodes,

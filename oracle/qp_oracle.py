@@ -1,0 +1,141 @@
+"""Dense reference solver for the SQP-RTI QP -- TEST INFRASTRUCTURE ONLY (the checker of csrc/rti_qp.hip).
+
+The QP is the one acados builds in the RTI preparation phase and HPIPM solves in the feedback phase
+(sdf_nmpc/ocp.py:54-120: NONLINEAR_LS + GAUSS_NEWTON, levenberg_marquardt = mpc.lm_reg, ERK, soft
+nonlinear constraints idxsh with L1/L2 slack penalties, input box constraints, x_0 fixed):
+
+  min  sum_{k<N} s_k [ 1/2 |J_y,k w_k + r_k|^2_{W_k} ] + 1/2 lm |w_k|^2
+     + s_N 1/2 |J_yN dx_N + r_N|^2_{W_N} + 1/2 lm |dx_N|^2
+     + sum_{k<=N} s_k (zl.sl_k + 1/2 Zl.sl_k^2 + zu.su_k + 1/2 Zu.su_k^2)
+  s.t. dx_0 = x0 - xbar_0,  dx_{k+1} = A_k dx_k + B_k du_k + (xn_k - xbar_{k+1})
+       lbu - ubar_k <= du_k <= ubu - ubar_k
+       lh - h_k - sl_k <= J_h,k dx_k <= uh - h_k + su_k,  sl_k, su_k >= 0
+  w_k = [dx_k; du_k], r_k = y_k - yref_k, s_k = cost scaling (acados default: dt_k for k < N, 1 at N)
+
+HPIPM's algorithm (Riccati-based IPM) is not reproducible here (acados is absent; parity at the
+acados boundary is unpinned); the QP is strictly convex (lm > 0) so its solution is
+unique, and this solver -- a textbook Mehrotra predictor-corrector on the full dense KKT system --
+pins it independently of the GPU solver's structure.
+"""
+import numpy as np
+
+
+def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=None):
+    """Assemble the per-stage QP data of ONE instance from the linearisation outputs.
+
+    lin: dict with xn [N,10], AB [N,14,10], y [N,11], Jy [N,14,11], yN [4], JyN [10,4], h [N+1,3],
+    Jh [N+1,10,3] (the sdfnmpc_linearize layouts, column-major blocks).
+    """
+    N = xbar.shape[0] - 1
+    s = np.concatenate([dt, [1.0]]) if scaling is None else np.asarray(scaling, float)
+    q = {"N": N, "s": s}
+    q["A"] = np.transpose(lin["AB"][:, :10, :], (0, 2, 1))    # [N,10,10] A[i][j]
+    q["B"] = np.transpose(lin["AB"][:, 10:, :], (0, 2, 1))    # [N,10,4]
+    q["c"] = lin["xn"] - xbar[1:]
+    Jy = np.transpose(lin["Jy"], (0, 2, 1))                   # [N,11,14]
+    r = lin["y"] - yref
+    q["H"] = np.einsum("kai,ka,kaj->kij", Jy, W, Jy) * s[:N, None, None] + lm * np.eye(14)
+    q["g"] = np.einsum("kai,ka,ka->ki", Jy, W, r) * s[:N, None]
+    JyN = lin["JyN"].T                                         # [4,10]
+    rN = lin["yN"] - yNref
+    q["HN"] = JyN.T @ np.diag(WN) @ JyN * s[N] + lm * np.eye(10)
+    q["gN"] = JyN.T @ (WN * rN) * s[N]
+    q["C"] = np.transpose(lin["Jh"], (0, 2, 1))               # [N+1,3,10]
+    q["hl"] = lin["h"] - model.lh                              # constant of the lower soft row
+    q["hu"] = model.uh - lin["h"]
+    q["ulo"] = model.lbu - ubar                                # du >= ulo
+    q["uhi"] = model.ubu - ubar
+    q["x0"] = x0 - xbar[0]
+    q["zl"], q["Zl"] = model.zl, model.Zl
+    return q
+
+
+def solve_dense(q, tol=1e-11, max_iter=100):
+    """Mehrotra IPM on the full KKT system.  Returns dict(dx [N+1,10], du [N,4], sl, su [N+1,3], iters)."""
+    N = q["N"]
+    nx, nu, ns = 10, 4, 3
+    ix = lambda k: k * nx
+    iu = lambda k: (N + 1) * nx + k * nu
+    isl = lambda k: (N + 1) * nx + N * nu + k * ns
+    isu = lambda k: (N + 1) * nx + N * nu + (N + 1) * ns + k * ns
+    nz = (N + 1) * nx + N * nu + 2 * (N + 1) * ns
+    H = np.zeros((nz, nz)); g = np.zeros(nz)
+    s = q["s"]
+    for k in range(N):
+        idx = np.r_[ix(k):ix(k) + nx, iu(k):iu(k) + nu]
+        H[np.ix_(idx, idx)] += q["H"][k]
+        g[idx] += q["g"][k]
+    H[ix(N):ix(N) + nx, ix(N):ix(N) + nx] += q["HN"]
+    g[ix(N):ix(N) + nx] += q["gN"]
+    for k in range(N + 1):
+        for j in range(ns):
+            H[isl(k) + j, isl(k) + j] += s[k] * q["Zl"][j]
+            H[isu(k) + j, isu(k) + j] += s[k] * q["Zl"][j]
+            g[isl(k) + j] += s[k] * q["zl"][j]
+            g[isu(k) + j] += s[k] * q["zl"][j]
+    # equalities E z = e
+    ne = (N + 1) * nx
+    E = np.zeros((ne, nz)); e = np.zeros(ne)
+    E[0:nx, ix(0):ix(0) + nx] = np.eye(nx); e[0:nx] = q["x0"]
+    for k in range(N):
+        r0 = (k + 1) * nx
+        E[r0:r0 + nx, ix(k + 1):ix(k + 1) + nx] = np.eye(nx)
+        E[r0:r0 + nx, ix(k):ix(k) + nx] = -q["A"][k]
+        E[r0:r0 + nx, iu(k):iu(k) + nu] = -q["B"][k]
+        e[r0:r0 + nx] = q["c"][k]
+    # inequalities G z + d >= 0
+    rows, d = [], []
+    for k in range(N):
+        for i in range(nu):
+            a = np.zeros(nz); a[iu(k) + i] = 1.0; rows.append(a); d.append(-q["ulo"][k, i])
+            a = np.zeros(nz); a[iu(k) + i] = -1.0; rows.append(a); d.append(q["uhi"][k, i])
+    for k in range(N + 1):
+        for j in range(ns):
+            C = q["C"][k, j]
+            a = np.zeros(nz); a[ix(k):ix(k) + nx] = C; a[isl(k) + j] = 1.0; rows.append(a); d.append(q["hl"][k, j])
+            a = np.zeros(nz); a[ix(k):ix(k) + nx] = -C; a[isu(k) + j] = 1.0; rows.append(a); d.append(q["hu"][k, j])
+            a = np.zeros(nz); a[isl(k) + j] = 1.0; rows.append(a); d.append(0.0)
+            a = np.zeros(nz); a[isu(k) + j] = 1.0; rows.append(a); d.append(0.0)
+    G = np.array(rows); d = np.array(d)
+    m = G.shape[0]
+    z = np.zeros(nz)
+    z = np.linalg.lstsq(E, e, rcond=None)[0]
+    t = np.maximum(G @ z + d, 1.0)
+    lam = np.ones(m)
+    y = np.zeros(ne)
+    it = 0
+    for it in range(1, max_iter + 1):
+        rd = H @ z + g - G.T @ lam + E.T @ y
+        rp = G @ z + d - t
+        re = E @ z - e
+        mu = t @ lam / m
+        if max(np.abs(rd).max(), np.abs(rp).max(), np.abs(re).max()) < tol and mu < tol:
+            break
+        Sig = lam / t
+        K = np.block([[H + G.T @ (Sig[:, None] * G), E.T], [E, np.zeros((ne, ne))]])
+
+        def solve(rc):
+            rhs1 = -rd - G.T @ (Sig * rp + rc / t)
+            sol = np.linalg.solve(K, np.concatenate([rhs1, -re]))
+            dz, dy = sol[:nz], sol[nz:]
+            dt_ = G @ dz + rp
+            dl = -(rc + lam * dt_) / t
+            return dz, dy, dt_, dl
+
+        def step(x, dx):
+            neg = dx < 0
+            return min(1.0, np.min(-x[neg] / dx[neg])) if neg.any() else 1.0
+
+        dz, dy, dt_, dl = solve(t * lam)
+        a = min(step(t, dt_), step(lam, dl))
+        mu_aff = (t + a * dt_) @ (lam + a * dl) / m
+        sig = (mu_aff / mu) ** 3
+        dz, dy, dt_, dl = solve(t * lam + dt_ * dl - sig * mu)
+        a = min(1.0, 0.995 * min(step(t, dt_), step(lam, dl)))
+        z += a * dz; y += a * dy; t += a * dt_; lam += a * dl
+    dx = np.array([z[ix(k):ix(k) + nx] for k in range(N + 1)])
+    du = np.array([z[iu(k):iu(k) + nu] for k in range(N)])
+    sl = np.array([z[isl(k):isl(k) + ns] for k in range(N + 1)])
+    su = np.array([z[isu(k):isu(k) + ns] for k in range(N + 1)])
+    return {"dx": dx, "du": du, "sl": sl, "su": su, "iters": it, "mu": t @ lam / m,
+            "obj": 0.5 * z @ H @ z + g @ z}

@@ -26,7 +26,7 @@ SYMBOLS = [
     "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
-    "sdfnmpc_linearize", "sdfnmpc_shooting_grid",
+    "sdfnmpc_linearize", "sdfnmpc_shooting_grid", "sdfnmpc_qp_solve", "sdfnmpc_rti_apply",
 ]
 L4C_SYMBOLS = [
     f"{p}sdf_l4c{s}" for p in ("", "jac_", "adj1_")
@@ -48,6 +48,20 @@ class QuadModelC(C.Structure):
 class LinArgsC(C.Structure):
     _fields_ = [("B", C.c_int), ("N", C.c_int), ("np", C.c_int), ("latent_mode", C.c_int)] + [
         (n, C.c_void_p) for n in ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "sdf")]
+
+
+class QpOptsC(C.Structure):
+    _fields_ = [("lbu", C.c_double * 4), ("ubu", C.c_double * 4), ("lh", C.c_double * 3), ("uh", C.c_double * 3),
+                ("zl", C.c_double * 3), ("Zl", C.c_double * 3), ("lm", C.c_double), ("cost_scaling", C.c_int),
+                ("max_iter", C.c_int), ("tol", C.c_double)]
+
+
+QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", "W", "yNref", "WN", "dt")
+QP_OUT = ("dx", "du", "slack", "status", "iters", "res")
+
+
+class QpArgsC(C.Structure):
+    _fields_ = [("B", C.c_int), ("N", C.c_int)] + [(n, C.c_void_p) for n in QP_IN + QP_OUT]
 
 
 _lib = None
@@ -87,6 +101,8 @@ def load():
         "sdfnmpc_sdf_eval_host": (i, [vp, vp, i, P(d), P(d), P(d)]),
         "sdfnmpc_linearize": (i, [vp, vp, P(QuadModelC), P(LinArgsC)]),
         "sdfnmpc_shooting_grid": (i, [i, d, i, i, d, P(d), P(d)]),
+        "sdfnmpc_qp_solve": (i, [vp, P(QpOptsC), P(QpArgsC)]),
+        "sdfnmpc_rti_apply": (i, [vp, i, i, vp, vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -232,6 +248,23 @@ def linearize(ctx: Context, net: Net, model: QuadModelC, B: int, N: int, np_: in
                                            ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh",
                                             "sdf")])
     _check(load().sdfnmpc_linearize(ctx.h, net.h, C.byref(model), C.byref(a)))
+
+
+def qp_opts(model, lm=10.0, cost_scaling=True, max_iter=100, tol=1e-8) -> QpOptsC:
+    """QP data of the 'att' model (model.Quad) + solver options (ocp.py:113-120 defaults)."""
+    v = lambda a, n: (C.c_double * n)(*[float(x) for x in a])
+    return QpOptsC(v(model.lbu, 4), v(model.ubu, 4), v(model.lh, 3), v(model.uh, 3), v(model.zl, 3),
+                   v(model.Zl, 3), float(lm), int(bool(cost_scaling)), int(max_iter), float(tol))
+
+
+def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
+    """Enqueue the batched feedback-phase QP.  bufs: device tensors named as sdfnmpc_qp_args."""
+    a = QpArgsC(B, N, *[_ptr(bufs.get(k)) for k in QP_IN + QP_OUT])
+    _check(load().sdfnmpc_qp_solve(ctx.h, C.byref(opts), C.byref(a)))
+
+
+def rti_apply(ctx: Context, B: int, N: int, x, u, dx, du, u0=None):
+    _check(load().sdfnmpc_rti_apply(ctx.h, B, N, _ptr(x), _ptr(u), _ptr(dx), _ptr(du), _ptr(u0)))
 
 
 def shooting_grid(N: int, T: float, uniform=True, nb_short_nodes=2, dt_short=0.01):

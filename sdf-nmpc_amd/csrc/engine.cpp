@@ -17,6 +17,7 @@
 
 #include "../../include/sdfnmpc.h"
 #include "lin_kernels.h"
+#include "qp_kernels.h"
 #include "sdf_kernels.h"
 
 using namespace sdfn;
@@ -71,7 +72,7 @@ struct sdfnmpc_ctx {
     bool lin_first = false;
     int tile_rows = 32;
     bool timing = false;
-    DevBuf c13, sdf4, lat, out4, glat;
+    DevBuf c13, sdf4, lat, out4, glat, qpw, qpst;
     std::vector<float> h_in;  // host staging for sdf_eval_host
     std::map<std::string, KStat> stats;
     std::mutex mu;  // serialises the host-pointer path (CasADi externals may be called concurrently)
@@ -664,6 +665,47 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
                  a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows, &cons);
     if (rc) return rc;
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+    return SDFNMPC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// batched QP (feedback phase) and RTI step
+extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* a) {
+    if (!ctx || !o || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
+    if (a->B < 0 || a->N < 1 || a->N > 200) return fail(SDFNMPC_E_ARG, "bad B/N for sdfnmpc_qp_solve");
+    if (a->B == 0) return SDFNMPC_OK;
+    if (!a->xn || !a->AB || !a->y || !a->Jy || !a->yN || !a->JyN || !a->h || !a->Jh || !a->x || !a->u || !a->x0 ||
+        !a->yref || !a->W || !a->yNref || !a->WN || !a->dt || !a->dx || !a->du)
+        return fail(SDFNMPC_E_ARG, "NULL array in sdfnmpc_qp_args");
+    if (o->lm <= 0.0 || o->max_iter < 1 || !(o->tol > 0.0))
+        return fail(SDFNMPC_E_ARG, "qp opts: lm > 0 (strict convexity), max_iter >= 1, tol > 0 required");
+    if (qp_lds_bytes(a->N) > 160 * 1024) return fail(SDFNMPC_E_UNSUPPORTED, "horizon too long for the LDS-resident QP");
+    ScopedDevice sd(ctx->device);
+    HIPCHK(ctx->qpw.ensure((size_t)a->B * qp_work_doubles(a->N) * sizeof(double)));
+    const bool own_st = !a->status || !a->iters || !a->res;
+    if (own_st) HIPCHK(ctx->qpst.ensure((size_t)a->B * (2 * sizeof(int) + 2 * sizeof(double))));
+    QpArgs q{};
+    q.B = a->B; q.N = a->N;
+    q.xn = a->xn; q.AB = a->AB; q.y = a->y; q.Jy = a->Jy; q.yN = a->yN; q.JyN = a->JyN; q.h = a->h; q.Jh = a->Jh;
+    q.x = a->x; q.u = a->u; q.x0 = a->x0; q.yref = a->yref; q.W = a->W; q.yNref = a->yNref; q.WN = a->WN; q.dt = a->dt;
+    q.dx = a->dx; q.du = a->du; q.slack = a->slack;
+    double* stbuf = (double*)ctx->qpst.p;
+    q.res = a->res ? a->res : stbuf;
+    q.status = a->status ? a->status : (int*)(stbuf + 2 * a->B);
+    q.iters = a->iters ? a->iters : (int*)(stbuf + 2 * a->B) + a->B;
+    q.work = (double*)ctx->qpw.p;
+    for (int i = 0; i < 4; ++i) { q.lbu[i] = o->lbu[i]; q.ubu[i] = o->ubu[i]; }
+    for (int i = 0; i < 3; ++i) { q.lh[i] = o->lh[i]; q.uh[i] = o->uh[i]; q.zl[i] = o->zl[i]; q.Zl[i] = o->Zl[i]; }
+    q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling;
+    HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, const double* dx,
+                                 const double* du, double* u0) {
+    if (!ctx || B < 0 || N < 1 || (B > 0 && (!x || !u || !dx || !du))) return fail(SDFNMPC_E_ARG, "bad rti_apply arguments");
+    ScopedDevice sd(ctx->device);
+    HIPCHK(timed(ctx, "rti_apply", [&] { return launch_rti_apply(B, N, x, u, dx, du, u0, ctx->stream); }));
     return SDFNMPC_OK;
 }
 
