@@ -17,24 +17,26 @@ struct QpArgs {
     int *status, *iters;
     double* res;      // [B][2] (mu, max primal residual)
     double* work;     // [B][qp_work_doubles(N)]
+    double* stamps;   // [B][8] cycle counters of the QP_STAMPS diagnostic build (NULL otherwise)
     // model / options
     double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3];
     double lm, tol;
     int max_iter, cost_scaling;
 };
 
-constexpr int QP_FSTRIDE = 100 + 40 + 40 + 16 + 4;  // per-stage factors: P, K, S, chol(R), k_ff
+constexpr int QP_REC = 300;   // stage record: [A B | c | g | C | H upper]   (rti_qp.hip)
+constexpr int QP_FREC = 110;  // factor record: [Y | chol(R) | k_ff | P_{k+1} upper]
 
-// global workspace per instance: GN Hessians / gradients per stage, then the Riccati factors
-__host__ __device__ inline size_t qp_work_doubles(int N) {
-    return (size_t)N * 196 + 100 + (size_t)N * 14 + 10 + (size_t)(N + 1) * QP_FSTRIDE;
-}
+// global workspace per instance: stage records and factor records for nodes 0..N
+__host__ __device__ inline size_t qp_work_doubles(int N) { return (size_t)(N + 1) * (QP_REC + QP_FREC); }
+// LDS per instance (one wavefront): duals/slacks, iterates, record buffers, stage scratch
 __host__ __device__ inline size_t qp_lds_bytes(int N) {
-    const size_t m = 8 * (size_t)N + 12 * (size_t)(N + 1);
-    const size_t n = 2 * ((size_t)(N + 1) * 10 + (size_t)N * 4 + 2 * (size_t)(N + 1) * 3) + 4 * m +
-                     100 + 10 + 140 + 196 + 14 + 10 + 140 + 40 + 40 + 16 + 4 + 10 + 64;
+    const size_t m = 8 * (size_t)N + 12 * (size_t)(N + 1), N1 = N + 1;
+    const size_t n = 2 * m + N1 * 10 + N * 4 + 3 * N1 * 3 + N * 4 + N1 * 3 + N1 * 10 + N * 4 + N1 * 3 +
+                     2 * QP_REC + 2 * QP_FREC + 220 + 140 + 196 + 14 + 10 + 6;
     return n * sizeof(double);
 }
+
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);
 hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx, const double* du, double* u0,
                             hipStream_t s);
