@@ -24,18 +24,28 @@ struct QpArgs {
     int max_iter, cost_scaling;
 };
 
-constexpr int QP_REC = 300;   // stage record: [A B | c | g | C | H upper]   (rti_qp.hip)
-constexpr int QP_FREC = 110;  // factor record: [Y | chol(R) | k_ff | P_{k+1} upper]
+constexpr int QP_REC = 300;   // stage record: [A B | c | g | C | H upper]          (rti_qp.hip)
+constexpr int QP_FREC = 64;   // factor record: [Y | chol(R^) (1/diag) | k_ff | P_{k+1} c_k]
+constexpr int QP_RING = 3;    // records in flight per wavefront
 
 // global workspace per instance: stage records and factor records for nodes 0..N
 __host__ __device__ inline size_t qp_work_doubles(int N) { return (size_t)(N + 1) * (QP_REC + QP_FREC); }
-// LDS per instance (one wavefront): duals/slacks, iterates, record buffers, stage scratch
-__host__ __device__ inline size_t qp_lds_bytes(int N) {
-    const size_t m = 8 * (size_t)N + 12 * (size_t)(N + 1), N1 = N + 1;
-    const size_t n = 2 * m + N1 * 10 + N * 4 + 3 * N1 * 3 + N * 4 + N1 * 3 + N1 * 10 + N * 4 + N1 * 3 +
-                     2 * QP_REC + 2 * QP_FREC + 220 + 140 + 196 + 14 + 10 + 6;
-    return n * sizeof(double);
+// LDS per instance (one wavefront); the order and sizes mirror carve() in rti_qp.hip
+__host__ __device__ inline size_t qp_lds_doubles(int N) {
+    const size_t N1 = N + 1, m = 8 * (size_t)N + 12 * N1;
+    return 2 * m                    // t, lambda
+           + 2 * N1 * 10            // dx, dxc
+           + 3 * (size_t)N * 4      // du, dua, duc
+           + 2 * N1 * 3             // cxa, cxc
+           + QP_REC + QP_FREC       // committed stage / factor record
+           + QP_RING * QP_FREC      // factor records of nodes 0..RING-1 (written late in a backward sweep)
+           + 100 + 10               // P, p
+           + 150 + 196 + 14         // W = P [A B c], M, m
+           + 4 * (size_t)N + 4 * N1 // u, (h, s_k)
+           + 6 * N1 + 8 * (size_t)N   // soft-row folds (w, gamma), box terms (diag, v)
+           + 20;                      // box / soft-row constants
 }
+__host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N) * sizeof(double); }
 
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);
 hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx, const double* du, double* u0,

@@ -11,15 +11,16 @@
 //   * each Newton system is an LQR in the new iterate z+ with Hessian H + D^T Sigma D and gradient
 //     g - D^T v (v folds the residuals), so dynamics hold exactly and no costate is carried
 //   * soft-constraint slacks (diagonal Hessian) are eliminated per row: a rank-3 update of the
-//     node's state block; recovered in closed form after each sweep
+//     node's state block; these folds and the box terms are formed for all nodes in one parallel
+//     pass before each sweep, so the serial sweeps hold no division
 //   * one factorisation per iteration serves predictor and corrector:
 //       Y = L^-1 S, P <- Q^ - Y^T Y, p <- m_x - Y^T (L^-1 m_u), K = -L^-T Y, k = -L^-T L^-1 m_u
-//     with L = chol(R^); the corrector and forward sweeps reuse (Y, L) and P_{k+1}
-// Memory: per-stage records [A B | c | g | C | H] are packed once per solve into a global workspace
-// and streamed through registers one stage ahead of the sweep (statically indexed: a runtime-indexed
-// ring would live in scratch); iterate, slacks and
-// duals live in LDS (< 40 KB: 4 instances per CU, one round for B = 1024).  Residuals are tracked
-// incrementally (r_p <- (1 - alpha) r_p) and the affine deltas are recomputed, not stored.
+//     with L = chol(R^) (rsq + Newton; the reciprocal diagonal is what is stored)
+// Memory: rti_qp_pack_kernel packs per-stage records [A B | c | g | C | H] into a global workspace
+// (a wide launch, one block per stage).  Each IPM iteration then walks the records in a fixed order
+// -- backward (factor), forward, backward (corrector), forward -- so they form one stream that is
+// prefetched QP_RING records ahead through registers, across sweep boundaries.  Iterate, duals and
+// stage scratch live in LDS (< 40 KB at N = 40: 4 instances per CU, one round for B = 1024).
 #include <hip/hip_runtime.h>
 
 #include "qp_kernels.h"
@@ -33,12 +34,13 @@ namespace {
 typedef __attribute__((address_space(3))) double ldsd;
 
 constexpr int NX = 10, NU = 4, NS = 3;
-// stage record (doubles): [AB 140 | c 10 | g 14 | C 30 | H 105 (upper triangle, row-major)] -> 300
+// stage record (doubles): [AB 140 (column j = d xn / d (x,u)_j) | c 10 | g 14 | C 30 | H 105 upper]
 constexpr int R_AB = 0, R_C = 140, R_G = 150, R_CH = 164, R_H = 194, REC = QP_REC;
-constexpr int PF_REC = (REC + 63) / 64;  // prefetch registers per lane per record
-// factor record: [Y 40 (4x10 row-major) | L 10 (lower packed) | kff 4 | P_{k+1} 55 (upper)] -> 110
-constexpr int F_Y = 0, F_L = 40, F_K = 50, F_P = 54, FREC = QP_FREC;
-constexpr int PF_F = (FREC + 63) / 64;
+constexpr int RR = (REC + 63) / 64;  // prefetch registers per lane per record
+// factor record: [Y 40 (4x10 row-major) | L 10 (lower packed, diagonal holds 1/L_ii) | kff 4 | P c 10]
+constexpr int F_Y = 0, F_L = 40, F_K = 50, F_PC = 54, FREC = QP_FREC;
+constexpr int PD = QP_RING;
+static_assert(FREC <= 64 && PD == 3, "ring layout");
 
 __device__ __forceinline__ int tri10(int a, int c) { return a * 10 - a * (a - 1) / 2 + (c - a); }  // a <= c
 __device__ __forceinline__ int ltri4(int i, int j) { return i * (i + 1) / 2 + j; }                  // j <= i
@@ -55,34 +57,113 @@ __device__ __forceinline__ double wmin(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
     return v;
 }
+// 1/sqrt(v), v > 0: hardware estimate + two Newton steps (full double precision)
+__device__ __forceinline__ double rsqrt_nr(double v) {
+    double y = __builtin_amdgcn_rsq(v);
+    const double h = 0.5 * v;
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    return y;
+}
 
 struct Smem {
-    ldsd *t, *lam;                  // [m] inequality slacks / duals
-    ldsd *dx, *du, *sl, *su, *cx;   // iterate z and cx[k][j] = C_j dx_k
-    ldsd *dua, *cxa;                // affine (predictor) solution: du, C dx
-    ldsd *dxc, *duc, *cxc;          // corrector solution (dxc is also the predictor sweep buffer)
-    ldsd *rec0, *rec1;              // stage record double buffer
-    ldsd *frc0, *frc1;              // factor record double buffer (corrector / forward sweeps)
-    ldsd *P0, *P1, *p0, *p1;        // Riccati P (full 10x10) / p ping-pong
-    ldsd *W, *M, *m, *Pb, *fold;    // stage scratch; fold: node's soft rows [w_j, gamma_j]
+    ldsd *t, *lam;                 // [m] inequality slacks / duals
+    ldsd *dx, *dxc;                // iterate dx; sweep solution (x of predictor, then corrector)
+    ldsd *du, *dua, *duc;          // iterate du; affine / corrector du
+    ldsd *cxa, *cxc;               // C dx of the affine / corrector solution
+    ldsd *rec, *frc, *fsave;       // committed stage record, factor record; F records of nodes < PD
+    ldsd *P, *p;                   // Riccati P (full 10x10), p (updated in place, one wavefront)
+    ldsd *W, *M, *m;               // W = P [A B c] (10 x 15), M (14 x 14), m (14)
+    ldsd *uu, *hv, *skv;           // u (box constants), h, cost scaling per node
+    ldsd *fw, *fg, *bd, *bv;       // soft folds [N+1][3] (w, gamma), box terms [N][4] (diag, v)
+    ldsd* cst;                     // lbu 4 | ubu 4 | lh 3 | uh 3 | zl 3 | Zl 3 (lane-indexed kernel arguments
+                                   // would be vector loads that wait behind the record stream)
 };
 
-__device__ __forceinline__ Smem carve(ldsd* q, int N) {
+__device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubles()
     Smem s;
     auto take = [&](int n) { ldsd* r = q; q += n; return r; };
     const int m = 8 * N + 12 * (N + 1), N1 = N + 1;
     s.t = take(m); s.lam = take(m);
-    s.dx = take(N1 * NX); s.du = take(N * NU); s.sl = take(N1 * NS); s.su = take(N1 * NS); s.cx = take(N1 * NS);
-    s.dua = take(N * NU); s.cxa = take(N1 * NS);
-    s.dxc = take(N1 * NX); s.duc = take(N * NU); s.cxc = take(N1 * NS);
-    s.rec0 = take(REC); s.rec1 = take(REC);
-    s.frc0 = take(FREC); s.frc1 = take(FREC);
-    s.P0 = take(100); s.P1 = take(100); s.p0 = take(10); s.p1 = take(10);
-    s.W = take(140); s.M = take(196); s.m = take(14); s.Pb = take(10); s.fold = take(6);
+    s.dx = take(N1 * NX); s.dxc = take(N1 * NX);
+    s.du = take(N * NU); s.dua = take(N * NU); s.duc = take(N * NU);
+    s.cxa = take(N1 * NS); s.cxc = take(N1 * NS);
+    s.rec = take(REC); s.frc = take(FREC); s.fsave = take(PD * FREC);
+    s.P = take(100); s.p = take(10);
+    s.W = take(150); s.M = take(196); s.m = take(14);
+    s.uu = take(N * NU); s.hv = take(N1 * NS); s.skv = take(N1);
+    s.fw = take(N1 * NS); s.fg = take(N1 * NS); s.bd = take(N * NU); s.bv = take(N * NU);
+    s.cst = take(20);
     return s;
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------------------------------------------
+// Stage records, one block per (instance, node): AB, c = xn_k - xbar_{k+1}, g = s_k J^T W r,
+// C = J_h, H = s_k J^T W J + lm I (upper); terminal: H_N = J_N^T W_N J_N + lm I (10x10 upper in the
+// H field), g_N (first 10 of g), C_N.
+__global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
+    const int N = A.N, N1 = N + 1;
+    const int b = blockIdx.x / N1, k = blockIdx.x - b * N1;
+    double* Rk = A.work + (size_t)b * qp_work_doubles(N) + (size_t)k * REC;
+    const double* Jh = A.Jh + ((size_t)b * N1 + k) * 30;
+    __shared__ double Js[154], Ws[11], rs[11];
+    if (k < N) {
+        const size_t bk = (size_t)b * N + k;
+        const double sk = A.cost_scaling ? A.dt[k] : 1.0;
+        for (int e = threadIdx.x; e < 154; e += 256) Js[e] = A.Jy[bk * 154 + e];
+        if (threadIdx.x < 11) {
+            Ws[threadIdx.x] = sk * A.W[bk * 11 + threadIdx.x];
+            rs[threadIdx.x] = A.y[bk * 11 + threadIdx.x] - A.yref[bk * 11 + threadIdx.x];
+        }
+        __syncthreads();
+        const double* AB = A.AB + bk * 140;
+        const double* xn = A.xn + bk * 10;
+        const double* xb1 = A.x + ((size_t)b * N1 + k + 1) * 10;
+        for (int e = threadIdx.x; e < REC; e += 256) {
+            double v = 0.0;
+            if (e < R_C) {
+                v = AB[e];
+            } else if (e < R_G) {
+                v = xn[e - R_C] - xb1[e - R_C];
+            } else if (e < R_CH) {
+                const int a = e - R_G;
+                for (int i = 0; i < 11; ++i) v += Js[a * 11 + i] * Ws[i] * rs[i];
+            } else if (e < R_H) {
+                v = Jh[e - R_CH];
+            } else if (e < R_H + 105) {
+                int q = e - R_H, a = 0;
+                while (q >= 14 - a) { q -= 14 - a; ++a; }
+                const int c = a + q;
+                for (int i = 0; i < 11; ++i) v += Js[a * 11 + i] * Ws[i] * Js[c * 11 + i];
+                v += (a == c ? A.lm : 0.0);
+            }
+            Rk[e] = v;
+        }
+    } else {
+        const double* J = A.JyN + (size_t)b * 40;  // [10][4]
+        const double* Wn = A.WN + (size_t)b * 4;
+        const double* yn = A.yN + (size_t)b * 4;
+        const double* rn = A.yNref + (size_t)b * 4;
+        for (int e = threadIdx.x; e < REC; e += 256) {
+            double v = 0.0;
+            if (e >= R_G && e < R_G + 10) {
+                const int a = e - R_G;
+                for (int i = 0; i < 4; ++i) v += J[a * 4 + i] * Wn[i] * (yn[i] - rn[i]);
+            } else if (e >= R_CH && e < R_H) {
+                v = Jh[e - R_CH];
+            } else if (e >= R_H && e < R_H + 55) {
+                int q = e - R_H, a = 0;
+                while (q >= 10 - a) { q -= 10 - a; ++a; }
+                const int c = a + q;
+                for (int i = 0; i < 4; ++i) v += J[a * 4 + i] * Wn[i] * J[c * 4 + i];
+                v += (a == c ? A.lm : 0.0);
+            }
+            Rk[e] = v;
+        }
+    }
+}
 
 #ifdef QP_STAMPS  // diagnostic build only: per-phase cycle accounting (never in the product build)
 #define STAMP_DECL long long st_t0 = clock64(), st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -100,150 +181,176 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     const int b = blockIdx.x, lane = threadIdx.x;
     const int N = A.N, N1 = N + 1, m = 8 * N + 12 * N1;
     Smem s = carve((ldsd*)lds_q, N);
-    double* R = A.work + (size_t)b * qp_work_doubles(N);  // [N+1][REC] stage records
-    double* F = R + (size_t)N1 * REC;                     // [N+1][FREC] factor records
-    const double* ub = A.u + (size_t)b * N * 4;
-    const double* hh = A.h + (size_t)b * N1 * 3;
+    const double* R = A.work + (size_t)b * qp_work_doubles(N);  // [N+1][REC] stage records
+    double* F = A.work + (size_t)b * qp_work_doubles(N) + (size_t)N1 * REC;  // [N+1][FREC]
 
-    // ------------------------------------------------------------ setup: pack the stage records
-    // (AB, c = xn_k - xbar_{k+1}, g, C = J_h, H = s_k J^T W J + lm I upper triangle); terminal:
-    // H_N = J_N^T W_N J_N + lm I (10x10 upper in the H field), g_N (first 10 of g), C_N.
-    for (int k = 0; k < N1; ++k) {
-        double* Rk = R + (size_t)k * REC;
-        const double sk = (A.cost_scaling && k < N) ? A.dt[k] : 1.0;
-        const double* Jh = A.Jh + ((size_t)b * N1 + k) * 30;
-        if (k < N) {
-            const double* AB = A.AB + ((size_t)b * N + k) * 140;
-            const double* J = A.Jy + ((size_t)b * N + k) * 154;
-            const double* Wk = A.W + ((size_t)b * N + k) * 11;
-            const double* yk = A.y + ((size_t)b * N + k) * 11;
-            const double* rk = A.yref + ((size_t)b * N + k) * 11;
-            const double* xn = A.xn + ((size_t)b * N + k) * 10;
-            const double* xb1 = A.x + ((size_t)b * N1 + k + 1) * 10;
-            for (int e = lane; e < REC; e += 64) {
-                double v = 0.0;
-                if (e < R_C) {
-                    v = AB[e];
-                } else if (e < R_G) {
-                    v = xn[e - R_C] - xb1[e - R_C];
-                } else if (e < R_CH) {
-                    const int a = e - R_G;
-                    for (int i = 0; i < 11; ++i) v += J[a * 11 + i] * Wk[i] * (yk[i] - rk[i]);
-                    v *= sk;
-                } else if (e < R_H) {
-                    v = Jh[e - R_CH];
-                } else if (e < R_H + 105) {
-                    int q = e - R_H, a = 0;
-                    while (q >= 14 - a) { q -= 14 - a; ++a; }
-                    const int c = a + q;
-                    for (int i = 0; i < 11; ++i) v += J[a * 11 + i] * Wk[i] * J[c * 11 + i];
-                    v = sk * v + (a == c ? A.lm : 0.0);
-                }
-                Rk[e] = v;
-            }
-        } else {
-            const double* J = A.JyN + (size_t)b * 40;  // [10][4]
-            const double* Wn = A.WN + (size_t)b * 4;
-            const double* yn = A.yN + (size_t)b * 4;
-            const double* rn = A.yNref + (size_t)b * 4;
-            for (int e = lane; e < REC; e += 64) {
-                double v = 0.0;
-                if (e >= R_G && e < R_G + 10) {
-                    const int a = e - R_G;
-                    for (int i = 0; i < 4; ++i) v += J[a * 4 + i] * Wn[i] * (yn[i] - rn[i]);
-                } else if (e >= R_CH && e < R_H) {
-                    v = Jh[e - R_CH];
-                } else if (e >= R_H && e < R_H + 55) {
-                    int q = e - R_H, a = 0;
-                    while (q >= 10 - a) { q -= 10 - a; ++a; }
-                    const int c = a + q;
-                    for (int i = 0; i < 4; ++i) v += J[a * 4 + i] * Wn[i] * J[c * 4 + i];
-                    v += (a == c ? A.lm : 0.0);
-                }
-                Rk[e] = v;
-            }
-        }
-    }
-    __syncthreads();  // records are re-read below by other lanes of this wave (same CU: L1/L2 coherent)
-    STAMP(0);
-
-    // ------------------------------------------------------------ record streaming (register ring)
-    double nxt[PF_REC];  // record in flight (filled one stage ahead; static indexing keeps it in VGPRs)
-    auto fetch = [&](double* dst, int k, int n) {
+    // ------------------------------------------------------------ record stream
+    // stream index j: [0, N1) initial forward (k = j); then per IPM iteration 4 sweeps of N1 records:
+    // backward-factor (full record), forward (record + Y, L, kff), backward-corrector (record + F),
+    // forward.  Slot j % PD of the register ring holds record j; consuming j issues j + PD.
+    double rr[PD][RR], fr[PD];
+    auto decode = [&](int j, int& k, int& n, int& nf) {
+        if (j < N1) { k = j; n = R_H; nf = 0; return; }
+        const int jj = j - N1, q = jj % N1, t = (jj / N1) & 3;
+        k = (t & 1) ? q : N - q;
+        n = t == 0 ? REC : R_H;
+        nf = t == 0 ? 0 : (t == 2 ? FREC : F_PC);
+    };
+    // every issue is the same RR + 1 unpredicated loads (clamped addresses): a data-dependent load
+    // count would make the compiler's wait counters conservative (vmcnt(0) at every commit)
+    auto issue_to = [&](double* rd, double& fd, int j) {
+        int k, n, nf;
+        decode(j, k, n, nf);
         const double* src = R + (size_t)k * REC;
 #pragma unroll
-        for (int i = 0; i < PF_REC; ++i) {
+        for (int i = 0; i < RR; ++i) {
             const int e = lane + 64 * i;
-            dst[i] = (e < n) ? src[e] : 0.0;
+            rd[i] = src[e < REC ? e : REC - 1];
         }
+        fd = F[(size_t)k * FREC + lane];
     };
-    auto commit = [&](ldsd* lds, const double* reg, int n) {
+    auto commit_from = [&](const double* rd, double fd) {
 #pragma unroll
-        for (int i = 0; i < PF_REC; ++i) {
+        for (int i = 0; i < RR; ++i) {
             const int e = lane + 64 * i;
-            if (e < n) lds[e] = reg[i];
+            if (e < REC) s.rec[e] = rd[i];
         }
+        s.frc[lane] = fd;
     };
-    double fnxt[PF_F];
-    auto ffetch = [&](double* dst, int k, int n) {
-        const double* src = F + (size_t)k * FREC;
+    int pos = 0;
+    auto advance = [&]() {  // commit record `pos` to LDS, refill its slot with record pos + PD
+        const int sl = pos % PD;
+        if (sl == 0) { commit_from(rr[0], fr[0]); issue_to(rr[0], fr[0], pos + PD); }
+        else if (sl == 1) { commit_from(rr[1], fr[1]); issue_to(rr[1], fr[1], pos + PD); }
+        else { commit_from(rr[2], fr[2]); issue_to(rr[2], fr[2], pos + PD); }
+        ++pos;
+    };
+    issue_to(rr[0], fr[0], 0);
+    issue_to(rr[1], fr[1], 1);
+    issue_to(rr[2], fr[2], 2);
+
+    // ------------------------------------------------------------ per-node constants into LDS
+    for (int e = lane; e < N * NU; e += 64) {
+        s.uu[e] = A.u[(size_t)b * N * NU + e];
+        s.du[e] = 0.0;
+    }
+    for (int e = lane; e < N1 * NS; e += 64) s.hv[e] = A.h[(size_t)b * N1 * NS + e];
+    {
+        double v = 0.0;  // constant indices: scalar loads of the kernel arguments
 #pragma unroll
-        for (int i = 0; i < PF_F; ++i) {
-            const int e = lane + 64 * i;
-            dst[i] = (e < n) ? src[e] : 0.0;
+        for (int i = 0; i < 4; ++i) {
+            if (lane == i) v = A.lbu[i];
+            if (lane == 4 + i) v = A.ubu[i];
         }
-    };
-    auto fcommit = [&](ldsd* lds, const double* reg, int n) {
 #pragma unroll
-        for (int i = 0; i < PF_F; ++i) {
-            const int e = lane + 64 * i;
-            if (e < n) lds[e] = reg[i];
+        for (int j = 0; j < 3; ++j) {
+            if (lane == 8 + j) v = A.lh[j];
+            if (lane == 11 + j) v = A.uh[j];
+            if (lane == 14 + j) v = A.zl[j];
+            if (lane == 17 + j) v = A.Zl[j];
+        }
+        if (lane < 20) s.cst[lane] = v;
+    }
+    for (int e = lane; e < N1; e += 64) s.skv[e] = (A.cost_scaling && e < N) ? A.dt[e] : 1.0;
+    if (lane < NX) s.dx[lane] = A.x0[(size_t)b * 10 + lane] - A.x[(size_t)b * N1 * 10 + lane];
+    __syncthreads();
+    STAMP(0);
+
+    // per-lane output maps of the three factor steps (fixed for the whole solve)
+    // step 1: W[i][j] = P[i,:] . [A B c][:, j], e = i * 15 + j < 150
+    const int e1b = lane + 64, e1c = (lane + 128 < 150) ? lane + 128 : 149;
+    const int w_i0 = lane / 15, w_j0 = lane % 15, w_i1 = e1b / 15, w_j1 = e1b % 15, w_i2 = e1c / 15, w_j2 = e1c % 15;
+    // step 2: (a, c), a <= c < 14 (M upper, row-major) then (a, 14) = m
+    auto m_map = [](int e, int& a, int& c) {
+        if (e >= 105) { a = e - 105; c = 14; return; }
+        int q = e;
+        a = 0;
+        while (q >= 14 - a) { q -= 14 - a; ++a; }
+        c = a + q;
+    };
+    int m_a0, m_c0, m_a1, m_c1;
+    m_map(lane, m_a0, m_c0);
+    m_map(lane + 64 < 119 ? lane + 64 : 118, m_a1, m_c1);
+    const bool m_has1 = lane + 64 < 119;
+    // step 3: e < 100: P[a][c]; e >= 100: p[e - 100]
+    const int p_a0 = lane / 10, p_c0 = lane % 10;
+    const int p_e1 = (lane + 64 < 110) ? lane + 64 : 109;
+    const int p_a1 = p_e1 < 100 ? p_e1 / 10 : p_e1 - 100, p_c1 = p_e1 < 100 ? p_e1 % 10 : -1;
+    const bool p_has1 = lane + 64 < 110;
+
+    // box rows (k, i, up): t = +-du + d, d = (u - lbu) | (ubu - u)
+    auto box_d = [&](int k, int i, int up) -> double {
+        const double u = s.uu[k * 4 + i];
+        return up ? s.cst[4 + i] - u : u - s.cst[0 + i];
+    };
+
+    // ------------------------------------------------------------ forward sweep (1 barrier per stage)
+    // mode 0: initial iterate (u = 0); mode 1: u_k = k_ff - L^-T (Y x_k).  x_{k+1} = A x_k + B u_k + c_k,
+    // cx = C x.  Factor data of nodes < PD comes from fsave (written late in the backward sweep).
+    auto forward = [&](int mode, ldsd* dxo, ldsd* duo, ldsd* cxo) {
+        if (lane < NX) dxo[lane] = s.dx[lane];
+        for (int k = 0; k < N1; ++k) {
+            advance();
+            __syncthreads();
+            const ldsd* rk = s.rec;
+            const ldsd* fk = (k < PD) ? s.fsave + k * FREC : s.frc;
+            const ldsd* x = dxo + k * NX;
+            if (lane >= 16 && lane < 16 + NS) {
+                const int j = lane - 16;
+                double v = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) v += rk[R_CH + l * 3 + j] * x[l];
+                cxo[k * NS + j] = v;
+            }
+            if (k < N && lane < NX) {
+                double xv[NX];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) xv[l] = x[l];
+                double u[4] = {0.0, 0.0, 0.0, 0.0};
+                if (mode) {
+                    double yx[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        double v = 0.0;
+#pragma unroll
+                        for (int l = 0; l < NX; ++l) v += fk[F_Y + i * 10 + l] * xv[l];
+                        yx[i] = v;
+                    }
+#pragma unroll
+                    for (int i = 3; i >= 0; --i) {
+                        double v = yx[i];
+#pragma unroll
+                        for (int q = i + 1; q < 4; ++q) v -= fk[F_L + ltri4(q, i)] * u[q];
+                        u[i] = v * fk[F_L + ltri4(i, i)];
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) u[i] = fk[F_K + i] - u[i];
+                }
+                double v = rk[R_C + lane];
+#pragma unroll
+                for (int j = 0; j < NX; ++j) v += rk[R_AB + j * 10 + lane] * xv[j];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v += rk[R_AB + (NX + i) * 10 + lane] * u[i];
+                dxo[(k + 1) * NX + lane] = v;
+                if (mode && lane < 4) duo[k * NU + lane] = u[lane];
+            }
+            __syncthreads();
         }
     };
 
     // ------------------------------------------------------------ initial iterate (dynamics-feasible):
-    // du = sl = su = 0, dx_0 = x0 - xbar_0, dx_{k+1} = A dx_k + c_k, cx = C dx
-    for (int e = lane; e < N * NU; e += 64) s.du[e] = 0.0;
-    for (int e = lane; e < N1 * NS; e += 64) { s.sl[e] = 0.0; s.su[e] = 0.0; }
-    if (lane < NX) s.dx[lane] = A.x0[(size_t)b * 10 + lane] - A.x[(size_t)b * N1 * 10 + lane];
-    fetch(nxt, 0, R_H);
-    __syncthreads();
-    for (int k = 0; k < N1; ++k) {
-        ldsd* rk = (k & 1) ? s.rec1 : s.rec0;
-        commit(rk, nxt, R_H);
-        if (k + 1 < N1) fetch(nxt, k + 1, R_H);
-        __syncthreads();
-        if (lane < NX && k < N) {
-            double v = rk[R_C + lane];
-            for (int j = 0; j < NX; ++j) v += rk[R_AB + j * 10 + lane] * s.dx[k * NX + j];
-            s.dx[(k + 1) * NX + lane] = v;
-        }
-        if (lane >= 16 && lane < 16 + NS) {
-            const int j = lane - 16;
-            double v = 0.0;
-            for (int l = 0; l < NX; ++l) v += rk[R_CH + l * 3 + j] * s.dx[k * NX + l];
-            s.cx[k * NS + j] = v;
-        }
-        __syncthreads();
-    }
-
-    // box rows (k, i, up): t = +-du + d, d = (u - lbu) | (ubu - u)
-    auto box_d = [&](int k, int i, int up) -> double {
-        const double u = ub[k * 4 + i];
-        return up ? A.ubu[i] - u : u - A.lbu[i];
-    };
+    // du = sl = su = 0, dx_0 = x0 - xbar_0, dx_{k+1} = A dx_k + c_k
+    forward(0, s.dx, nullptr, s.cxa);
     double rp = 0.0;
     for (int r = lane; r < m; r += 64) {
         double v;
         if (r < 8 * N) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
-            v = (up ? -s.du[k * NU + i] : s.du[k * NU + i]) + box_d(k, i, up);
+            v = box_d(k, i, up);
         } else {
             const int q = r - 8 * N, k = q / 12, w = q - 12 * k, j = w >> 2, kind = w & 3;
-            const double h = hh[k * 3 + j];
-            v = kind == 0 ? s.cx[k * NS + j] + (h - A.lh[j]) + s.sl[k * NS + j]
-              : kind == 1 ? -s.cx[k * NS + j] + (A.uh[j] - h) + s.su[k * NS + j]
-              : kind == 2 ? s.sl[k * NS + j] : s.su[k * NS + j];
+            const double h = s.hv[k * 3 + j];
+            v = kind == 0 ? s.cxa[k * NS + j] + (h - s.cst[8 + j]) : kind == 1 ? -s.cxa[k * NS + j] + (s.cst[11 + j] - h) : 0.0;
         }
         const double t = fmax(v, 1.0);
         s.t[r] = t;
@@ -261,24 +368,24 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     auto group = [&](int k, int j, int phase, double sigmu) -> Grp {
         Grp g;
         const int r0 = 8 * N + 12 * k + 4 * j;
-        const double sk = (A.cost_scaling && k < N) ? A.dt[k] : 1.0;
+        const double sk = s.skv[k];
         const double t1 = s.t[r0], t2 = s.t[r0 + 1], t3 = s.t[r0 + 2], t4 = s.t[r0 + 3];
         const double l1 = s.lam[r0], l2 = s.lam[r0 + 1], l3 = s.lam[r0 + 2], l4 = s.lam[r0 + 3];
         g.s1 = l1 / t1; g.s3 = l2 / t2; g.s2 = l3 / t3; g.s4 = l4 / t4;
-        const double h = hh[k * 3 + j];
-        g.v1 = g.s1 * (t1 - (h - A.lh[j]));
-        g.v3 = g.s3 * (t2 - (A.uh[j] - h));
+        const double h = s.hv[k * 3 + j];
+        g.v1 = g.s1 * (t1 - (h - s.cst[8 + j]));
+        g.v3 = g.s3 * (t2 - (s.cst[11 + j] - h));
         g.v2 = g.s2 * t3;
         g.v4 = g.s4 * t4;
-        const double Zs = sk * A.Zl[j], zs = sk * A.zl[j];
+        const double Zs = sk * s.cst[17 + j], zs = sk * s.cst[14 + j];
         g.Hl = Zs + g.s1 + g.s2;
         g.Hu = Zs + g.s3 + g.s4;
         if (phase) {  // corrector: affine deltas of the four rows, recomputed from the affine solution
             const double cxa = s.cxa[k * NS + j];
             const double sla = -((zs - g.v1 - g.v2) + g.s1 * cxa) / g.Hl;
             const double sua = -((zs - g.v3 - g.v4) - g.s3 * cxa) / g.Hu;
-            const double d1 = cxa + (h - A.lh[j]) + sla - t1;
-            const double d2 = -cxa + (A.uh[j] - h) + sua - t2;
+            const double d1 = cxa + (h - s.cst[8 + j]) + sla - t1;
+            const double d2 = -cxa + (s.cst[11 + j] - h) + sua - t2;
             const double d3 = sla - t3, d4 = sua - t4;
             g.v1 -= (d1 * (-g.s1 * d1 - l1) - sigmu) / t1;
             g.v3 -= (d2 * (-g.s3 * d2 - l2) - sigmu) / t2;
@@ -299,291 +406,261 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
         return v;
     };
-    auto fold_node = [&](int k, int phase, double sigmu) {  // lanes 0..2: soft rows of node k
-        if (lane < NS) {
-            const Grp g = group(k, lane, phase, sigmu);
-            s.fold[lane] = g.s1 * (g.Hl - g.s1) / g.Hl + g.s3 * (g.Hu - g.s3) / g.Hu;
-            s.fold[3 + lane] = -(g.v1 + g.s1 * g.gl / g.Hl) + (g.v3 + g.s3 * g.gu / g.Hu);
+    // all nodes at once, before a backward sweep: fw = w_j (factor only), fg = gamma_j, box diag / v
+    auto terms = [&](int phase, double sigmu) {
+        for (int e = lane; e < N1 * NS; e += 64) {
+            const int k = e / NS, j = e - NS * k;
+            const Grp g = group(k, j, phase, sigmu);
+            const double iHl = 1.0 / g.Hl, iHu = 1.0 / g.Hu;
+            if (!phase) s.fw[e] = g.s1 * (g.Hl - g.s1) * iHl + g.s3 * (g.Hu - g.s3) * iHu;
+            s.fg[e] = -(g.v1 + g.s1 * g.gl * iHl) + (g.v3 + g.s3 * g.gu * iHu);
         }
+        for (int e = lane; e < N * NU; e += 64) {
+            const int k = e >> 2, i = e & 3;
+            if (!phase) s.bd[e] = s.lam[8 * k + i] / s.t[8 * k + i] + s.lam[8 * k + 4 + i] / s.t[8 * k + 4 + i];
+            s.bv[e] = -box_v(k, i, 0, phase, sigmu) + box_v(k, i, 1, phase, sigmu);
+        }
+        __syncthreads();
     };
 
-    // ------------------------------------------------------------ backward sweep
-    // factor: factorisation + predictor gradient (3 barriers per stage);
-    // corrector: stored factors + corrector gradient (1 barrier per stage)
-    auto backward = [&](bool factor, int phase, double sigmu) {
-        const int nrec = factor ? REC : R_H;
-        int cur = 0;
-        fetch(nxt, N, REC);
-        fold_node(N, phase, sigmu);
-        commit(s.rec0, nxt, REC);
-        fetch(nxt, N - 1, nrec);
-        if (!factor) ffetch(fnxt, N - 1, FREC);
-        __syncthreads();
-        {  // terminal node: P_N = H_N + sum_j w_j C_j^T C_j, p_N = g_N + sum_j gamma_j C_j^T
-            const ldsd* rN = s.rec0;
-            for (int e = lane; e < 110; e += 64) {
-                if (e < 100) {
-                    if (!factor) continue;
-                    const int a = e / 10, c = e % 10;
-                    double v = rN[R_H + tri10(a < c ? a : c, a < c ? c : a)];
-                    for (int j = 0; j < NS; ++j) v += s.fold[j] * rN[R_CH + a * 3 + j] * rN[R_CH + c * 3 + j];
-                    s.P0[e] = v;
-                } else {
-                    const int a = e - 100;
-                    double v = rN[R_G + a];
-                    for (int j = 0; j < NS; ++j) v += s.fold[3 + j] * rN[R_CH + a * 3 + j];
-                    s.p0[a] = v;
-                }
-            }
-        }
-        __syncthreads();
-        for (int k = N - 1; k >= 0; --k) {
-            const int slot = (N - k) & 1;
-            ldsd* rk = slot ? s.rec1 : s.rec0;
-            ldsd* fk = slot ? s.frc1 : s.frc0;
-            commit(rk, nxt, nrec);
-            if (!factor) fcommit(fk, fnxt, FREC);
-            if (k >= 1) {
-                fetch(nxt, k - 1, nrec);
-                if (!factor) ffetch(fnxt, k - 1, FREC);
-            }
-            fold_node(k, phase, sigmu);
+    // ------------------------------------------------------------ backward sweep, factor (3 barriers / stage)
+    auto backward_factor = [&]() {
+        for (int q = 0; q < N1; ++q) {
+            const int k = N - q;
+            advance();
             __syncthreads();
-            const ldsd* Pk1 = cur ? s.P1 : s.P0;
-            const ldsd* pk1 = cur ? s.p1 : s.p0;
-            ldsd* pn = cur ? s.p0 : s.p1;
-            if (factor) {
-                // ---- step 1: W = P [A B] (10 x 14), Pb = P c + p
-                for (int e = lane; e < 150; e += 64) {
-                    if (e < 140) {
-                        const int i = e / 14, j = e % 14;
-                        double acc = 0.0;
-#pragma unroll
-                        for (int l = 0; l < NX; ++l) acc += Pk1[i * 10 + l] * rk[R_AB + j * 10 + l];
-                        s.W[e] = acc;
-                    } else {
-                        const int i = e - 140;
-                        double acc = pk1[i];
-#pragma unroll
-                        for (int l = 0; l < NX; ++l) acc += Pk1[i * 10 + l] * rk[R_C + l];
-                        s.Pb[i] = acc;
-                    }
-                }
-                __syncthreads();
-                // ---- step 2: M = H~ + [A B]^T W (from the upper triangle), m = g~ + [A B]^T Pb
-                for (int e = lane; e < 119; e += 64) {
-                    if (e < 105) {
-                        int q = e, a = 0;
-                        while (q >= 14 - a) { q -= 14 - a; ++a; }
-                        const int c = a + q;
-                        double v = rk[R_H + e];
-#pragma unroll
-                        for (int l = 0; l < NX; ++l) v += rk[R_AB + a * 10 + l] * s.W[l * 14 + c];
-                        if (c < NX) {
-                            for (int j = 0; j < NS; ++j) v += s.fold[j] * rk[R_CH + a * 3 + j] * rk[R_CH + c * 3 + j];
-                        } else if (a == c) {
-                            const int r0 = 8 * k + (a - NX);
-                            v += s.lam[r0] / s.t[r0] + s.lam[r0 + 4] / s.t[r0 + 4];
-                        }
-                        s.M[a * 14 + c] = v;
-                        s.M[c * 14 + a] = v;
-                    } else {
-                        const int a = e - 105;
-                        double v = rk[R_G + a];
-#pragma unroll
-                        for (int l = 0; l < NX; ++l) v += rk[R_AB + a * 10 + l] * s.Pb[l];
-                        if (a < NX) {
-                            for (int j = 0; j < NS; ++j) v += s.fold[3 + j] * rk[R_CH + a * 3 + j];
-                        } else {
-                            const int i = a - NX;
-                            v += -box_v(k, i, 0, phase, sigmu) + box_v(k, i, 1, phase, sigmu);
-                        }
-                        s.m[a] = v;
-                    }
-                }
-                __syncthreads();
-                // ---- step 3: L = chol(R^) (every lane, registers), y_a = L^-1 S[:, a], w = L^-1 m_u;
-                //      P_k = Q^ - Y^T Y, p_k = m_x - Y^T w; factor record (Y, L, k_ff, P_{k+1})
-                double L[4][4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-#pragma unroll
-                    for (int j = 0; j <= i; ++j) {
-                        double v = s.M[(NX + i) * 14 + NX + j];
-#pragma unroll
-                        for (int q = 0; q < j; ++q) v -= L[i][q] * L[j][q];
-                        L[i][j] = (i == j) ? sqrt(v) : v / L[j][j];
-                    }
-                // y = L^-1 col (forward substitution with the reciprocal diagonal)
-                const double id0 = 1.0 / L[0][0], id1 = 1.0 / L[1][1], id2 = 1.0 / L[2][2], id3 = 1.0 / L[3][3];
-#define FSUB(col, stride, y)                                                                  \
-    do {                                                                                      \
-        y[0] = (col)[0] * id0;                                                                \
-        y[1] = ((col)[(stride)] - L[1][0] * y[0]) * id1;                                      \
-        y[2] = ((col)[2 * (stride)] - L[2][0] * y[0] - L[2][1] * y[1]) * id2;                 \
-        y[3] = ((col)[3 * (stride)] - L[3][0] * y[0] - L[3][1] * y[1] - L[3][2] * y[2]) * id3; \
-    } while (0)
-                double w[4];
-                FSUB(s.m + NX, 1, w);
-                ldsd* Pn = cur ? s.P0 : s.P1;
-                double* Fk = F + (size_t)k * FREC;
+            const ldsd* rk = s.rec;
+            if (q == 0) {  // P_N = H_N + sum_j w_j C_j^T C_j, p_N = g_N + sum_j gamma_j C_j^T
                 for (int e = lane; e < 110; e += 64) {
                     if (e < 100) {
                         const int a = e / 10, c = e % 10;
-                        double ya[4], yc[4];
-                        FSUB(s.M + NX * 14 + a, 14, ya);
-                        FSUB(s.M + NX * 14 + c, 14, yc);
-                        double v = s.M[a * 14 + c];
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) v -= ya[i] * yc[i];
-                        Pn[e] = v;
-                        if (a <= c) Fk[F_P + tri10(a, c)] = Pk1[e];
-                        if (a == 0) {
-#pragma unroll
-                            for (int i = 0; i < 4; ++i) Fk[F_Y + i * 10 + c] = yc[i];
-                        }
+                        double v = rk[R_H + tri10(a < c ? a : c, a < c ? c : a)];
+                        for (int j = 0; j < NS; ++j) v += s.fw[N * NS + j] * rk[R_CH + a * 3 + j] * rk[R_CH + c * 3 + j];
+                        s.P[e] = v;
                     } else {
                         const int a = e - 100;
-                        double ya[4];
-                        FSUB(s.M + NX * 14 + a, 14, ya);
-                        double v = s.m[a];
-#pragma unroll
-                        for (int i = 0; i < 4; ++i) v -= ya[i] * w[i];
-                        pn[a] = v;
+                        double v = rk[R_G + a];
+                        for (int j = 0; j < NS; ++j) v += s.fg[N * NS + j] * rk[R_CH + a * 3 + j];
+                        s.p[a] = v;
                     }
                 }
-                if (lane == 0) {
+                __syncthreads();
+                continue;
+            }
+            double* Fk = F + (size_t)k * FREC;
+            ldsd* Fs = s.fsave + k * FREC;  // meaningful for k < PD only
+            // ---- step 1: W = P [A B c] (10 x 15); column 14 -> P c (factor record) and P c + p
+            {
+                double a0 = 0.0, a1 = 0.0, a2 = 0.0;
 #pragma unroll
-                    for (int i = 0; i < 4; ++i)
-#pragma unroll
-                        for (int j = 0; j <= i; ++j) Fk[F_L + ltri4(i, j)] = L[i][j];
+                for (int l = 0; l < NX; ++l) {
+                    a0 += s.P[w_i0 * 10 + l] * rk[w_j0 * 10 + l];
+                    a1 += s.P[w_i1 * 10 + l] * rk[w_j1 * 10 + l];
+                    a2 += s.P[w_i2 * 10 + l] * rk[w_j2 * 10 + l];
                 }
-                if (lane >= 48 && lane < 52) {  // k_ff = -L^-T w
-                    double kf[4];
+                if (w_j0 == 14) { Fk[F_PC + w_i0] = a0; if (k < PD) Fs[F_PC + w_i0] = a0; a0 += s.p[w_i0]; }
+                if (w_j1 == 14) { Fk[F_PC + w_i1] = a1; if (k < PD) Fs[F_PC + w_i1] = a1; a1 += s.p[w_i1]; }
+                if (w_j2 == 14) { Fk[F_PC + w_i2] = a2; if (k < PD) Fs[F_PC + w_i2] = a2; a2 += s.p[w_i2]; }
+                s.W[lane] = a0;
+                s.W[e1b] = a1;
+                if (lane + 128 < 150) s.W[lane + 128] = a2;
+            }
+            __syncthreads();
+            // ---- step 2: M = H~ + [A B]^T W (upper), m = g~ + [A B]^T (P c + p), plus soft folds / box terms
+            {
+                const int fk3 = k * NS, bk4 = k * 4;
+                auto mval = [&](int a, int c, double acc) -> double {
+                    double v = acc;
+                    if (c < 14) {
+                        v += rk[R_H + a * 14 - a * (a - 1) / 2 + (c - a)];
+                        if (c < NX) {
 #pragma unroll
-                    for (int i = 3; i >= 0; --i) {
-                        double v = w[i];
+                            for (int j = 0; j < NS; ++j) v += s.fw[fk3 + j] * rk[R_CH + a * 3 + j] * rk[R_CH + c * 3 + j];
+                        } else if (a == c) {
+                            v += s.bd[bk4 + a - NX];
+                        }
+                    } else {
+                        v += rk[R_G + a];
+                        if (a < NX) {
 #pragma unroll
-                        for (int q = i + 1; q < 4; ++q) v -= L[q][i] * kf[q];
-                        kf[i] = v / L[i][i];
+                            for (int j = 0; j < NS; ++j) v += s.fg[fk3 + j] * rk[R_CH + a * 3 + j];
+                        } else {
+                            v += s.bv[bk4 + a - NX];
+                        }
                     }
-                    Fk[F_K + lane - 48] = -kf[lane - 48];
+                    return v;
+                };
+                double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+                for (int l = 0; l < NX; ++l) {
+                    a0 += rk[m_a0 * 10 + l] * s.W[l * 15 + m_c0];
+                    a1 += rk[m_a1 * 10 + l] * s.W[l * 15 + m_c1];
                 }
-#undef FSUB
-            } else {
-                // ---- corrector: every lane forms Pb = P_{k+1} c + p and m_u, w = L^-1 m_u;
-                //      lane a < 10: p_k[a] = m_x[a] - Y[:, a]^T w; lanes 16..19: k_ff = -L^-T w
-                const ldsd* Pf = fk + F_P;
-                double Pb[NX];
-#pragma unroll
-                for (int i = 0; i < NX; ++i) {
-                    double acc = pk1[i];
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) acc += Pf[tri10(i < l ? i : l, i < l ? l : i)] * rk[R_C + l];
-                    Pb[i] = acc;
-                }
-                double w[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    double v = rk[R_G + NX + i];
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) v += rk[R_AB + (NX + i) * 10 + l] * Pb[l];
-                    v += -box_v(k, i, 0, phase, sigmu) + box_v(k, i, 1, phase, sigmu);
-#pragma unroll
-                    for (int q = 0; q < i; ++q) v -= fk[F_L + ltri4(i, q)] * w[q];
-                    w[i] = v / fk[F_L + ltri4(i, i)];
-                }
-                if (lane < NX) {
-                    const int a = lane;
-                    double v = rk[R_G + a];
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) v += rk[R_AB + a * 10 + l] * Pb[l];
-                    for (int j = 0; j < NS; ++j) v += s.fold[3 + j] * rk[R_CH + a * 3 + j];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) v -= fk[F_Y + i * 10 + a] * w[i];
-                    pn[a] = v;
-                }
-                if (lane >= 16 && lane < 20) {
-                    double kf[4];
-#pragma unroll
-                    for (int i = 3; i >= 0; --i) {
-                        double v = w[i];
-#pragma unroll
-                        for (int q = i + 1; q < 4; ++q) v -= fk[F_L + ltri4(q, i)] * kf[q];
-                        kf[i] = v / fk[F_L + ltri4(i, i)];
-                    }
-                    F[(size_t)k * FREC + F_K + lane - 16] = -kf[lane - 16];
+                const double v0 = mval(m_a0, m_c0, a0), v1 = mval(m_a1, m_c1, a1);
+                if (m_c0 < 14) { s.M[m_a0 * 14 + m_c0] = v0; s.M[m_c0 * 14 + m_a0] = v0; } else { s.m[m_a0] = v0; }
+                if (m_has1) {
+                    if (m_c1 < 14) { s.M[m_a1 * 14 + m_c1] = v1; s.M[m_c1 * 14 + m_a1] = v1; } else { s.m[m_a1] = v1; }
                 }
             }
-            cur ^= 1;
+            __syncthreads();
+            // ---- step 3: L = chol(R^) (every lane, registers), y_a = L^-1 S[:, a], w = L^-1 m_u;
+            //      P_k = Q^ - Y^T Y, p_k = m_x - Y^T w (in place); factor record (Y, L, k_ff)
+            double L[4][4], id[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+#pragma unroll
+                for (int j = 0; j <= i; ++j) {
+                    double v = s.M[(NX + i) * 14 + NX + j];
+#pragma unroll
+                    for (int q2 = 0; q2 < j; ++q2) v -= L[i][q2] * L[j][q2];
+                    if (i == j) {
+                        id[i] = rsqrt_nr(v);
+                        L[i][i] = v * id[i];
+                    } else {
+                        L[i][j] = v * id[j];
+                    }
+                }
+            auto fsub = [&](const ldsd* col, int stride, double* y) {
+                y[0] = col[0] * id[0];
+                y[1] = (col[stride] - L[1][0] * y[0]) * id[1];
+                y[2] = (col[2 * stride] - L[2][0] * y[0] - L[2][1] * y[1]) * id[2];
+                y[3] = (col[3 * stride] - L[3][0] * y[0] - L[3][1] * y[1] - L[3][2] * y[2]) * id[3];
+            };
+            double w[4], ya0[4], yc0[4], ya1[4], yc1[4];
+            fsub(s.m + NX, 1, w);
+            fsub(s.M + NX * 14 + p_a0, 14, ya0);
+            fsub(s.M + NX * 14 + p_c0, 14, yc0);
+            fsub(s.M + NX * 14 + p_a1, 14, ya1);
+            if (p_c1 >= 0) {
+                fsub(s.M + NX * 14 + p_c1, 14, yc1);
+            } else {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) yc1[i] = w[i];
+            }
+            double v0 = s.M[p_a0 * 14 + p_c0];
+            double v1 = p_c1 >= 0 ? s.M[p_a1 * 14 + p_c1] : s.m[p_a1];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                v0 -= ya0[i] * yc0[i];
+                v1 -= ya1[i] * yc1[i];
+            }
+            s.P[lane] = v0;
+            if (p_has1) {
+                if (p_c1 >= 0) s.P[p_e1] = v1; else s.p[p_a1] = v1;
+            }
+            if (lane < NX) {  // Y[:, c] with c = lane (a = 0)
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    Fk[F_Y + i * 10 + lane] = yc0[i];
+                    if (k < PD) Fs[F_Y + i * 10 + lane] = yc0[i];
+                }
+            }
+            if (lane >= 16 && lane < 26) {  // L, diagonal stored as 1/L_ii
+                const int e = lane - 16;
+                const int i = e >= 6 ? 3 : e >= 3 ? 2 : e >= 1 ? 1 : 0, j = e - i * (i + 1) / 2;
+                double v = 0.0;
+#pragma unroll
+                for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+                    for (int jj = 0; jj <= ii; ++jj)
+                        if (ii == i && jj == j) v = (ii == jj) ? id[ii] : L[ii][jj];
+                Fk[F_L + e] = v;
+                if (k < PD) Fs[F_L + e] = v;
+            }
+            if (lane >= 48 && lane < 52) {  // k_ff = -L^-T w
+                double kf[4];
+#pragma unroll
+                for (int i = 3; i >= 0; --i) {
+                    double v = w[i];
+#pragma unroll
+                    for (int q2 = i + 1; q2 < 4; ++q2) v -= L[q2][i] * kf[q2];
+                    kf[i] = v * id[i];
+                }
+                double v = 0.0;
+#pragma unroll
+                for (int i = 0; i < 4; ++i) if (lane - 48 == i) v = -kf[i];
+                Fk[F_K + lane - 48] = v;
+                if (k < PD) Fs[F_K + lane - 48] = v;
+            }
             __syncthreads();
         }
     };
 
-    // ------------------------------------------------------------ forward sweep (1 barrier per stage)
-    // u_k = k_ff - L^-T (Y x_k), x_{k+1} = A x_k + B u_k + c_k; cx = C x
-    auto forward = [&](ldsd* dxo, ldsd* duo, ldsd* cxo) {
-        if (lane < NX) dxo[lane] = s.dx[lane];
-        fetch(nxt, 0, R_H);
-        ffetch(fnxt, 0, F_P);
-        for (int k = 0; k < N1; ++k) {
-            ldsd* rk = (k & 1) ? s.rec1 : s.rec0;
-            ldsd* fk = (k & 1) ? s.frc1 : s.frc0;
-            commit(rk, nxt, R_H);
-            fcommit(fk, fnxt, F_P);
-            if (k + 1 < N1) {
-                fetch(nxt, k + 1, R_H);
-                ffetch(fnxt, k + 1, F_P);
-            }
+    // ------------------------------------------------------------ backward sweep, corrector (1 barrier / stage)
+    // stored factors + corrector gradient: Pb = P c + p, w = L^-1 m_u, p_k = m_x - Y^T w, k_ff = -L^-T w
+    auto backward_corrector = [&]() {
+        for (int q = 0; q < N1; ++q) {
+            const int k = N - q;
+            advance();
             __syncthreads();
-            const ldsd* x = dxo + k * NX;
-            if (lane >= 16 && lane < 16 + NS) {
-                const int j = lane - 16;
-                double v = 0.0;
-#pragma unroll
-                for (int l = 0; l < NX; ++l) v += rk[R_CH + l * 3 + j] * x[l];
-                cxo[k * NS + j] = v;
-            }
-            if (k < N && lane < NX) {
-                double yx[4], u[4];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    double v = 0.0;
-#pragma unroll
-                    for (int l = 0; l < NX; ++l) v += fk[F_Y + i * 10 + l] * x[l];
-                    yx[i] = v;
+            const ldsd* rk = s.rec;
+            if (q == 0) {
+                if (lane < NX) {
+                    double v = rk[R_G + lane];
+                    for (int j = 0; j < NS; ++j) v += s.fg[N * NS + j] * rk[R_CH + lane * 3 + j];
+                    s.p[lane] = v;
                 }
+                __syncthreads();
+                continue;
+            }
+            const ldsd* fk = s.frc;
+            double Pb[NX];
+#pragma unroll
+            for (int l = 0; l < NX; ++l) Pb[l] = fk[F_PC + l] + s.p[l];
+            double mu[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double v = rk[R_G + NX + i] + s.bv[k * 4 + i];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) v += rk[R_AB + (NX + i) * 10 + l] * Pb[l];
+                mu[i] = v;
+            }
+            double w[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                double v = mu[i];
+#pragma unroll
+                for (int q2 = 0; q2 < i; ++q2) v -= fk[F_L + ltri4(i, q2)] * w[q2];
+                w[i] = v * fk[F_L + ltri4(i, i)];
+            }
+            if (lane < NX) {
+                const int a = lane;
+                double v = rk[R_G + a];
+#pragma unroll
+                for (int l = 0; l < NX; ++l) v += rk[R_AB + a * 10 + l] * Pb[l];
+#pragma unroll
+                for (int j = 0; j < NS; ++j) v += s.fg[k * NS + j] * rk[R_CH + a * 3 + j];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) v -= fk[F_Y + i * 10 + a] * w[i];
+                s.p[a] = v;
+            }
+            if (lane >= 16 && lane < 20) {
+                double kf[4];
 #pragma unroll
                 for (int i = 3; i >= 0; --i) {
-                    double v = yx[i];
+                    double v = w[i];
 #pragma unroll
-                    for (int q = i + 1; q < 4; ++q) v -= fk[F_L + ltri4(q, i)] * u[q];
-                    u[i] = v / fk[F_L + ltri4(i, i)];
+                    for (int q2 = i + 1; q2 < 4; ++q2) v -= fk[F_L + ltri4(q2, i)] * kf[q2];
+                    kf[i] = v * fk[F_L + ltri4(i, i)];
                 }
+                double v = 0.0;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) u[i] = fk[F_K + i] - u[i];
-                double v = rk[R_C + lane];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) v += rk[R_AB + j * 10 + lane] * x[j];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v += rk[R_AB + (NX + i) * 10 + lane] * u[i];
-                dxo[(k + 1) * NX + lane] = v;
-                if (lane < 4) duo[k * NU + lane] = u[lane];
+                for (int i = 0; i < 4; ++i) if (lane - 16 == i) v = -kf[i];
+                F[(size_t)k * FREC + F_K + lane - 16] = v;
+                if (k < PD) s.fsave[k * FREC + F_K + lane - 16] = v;
             }
             __syncthreads();
         }
     };
 
     // row values of a soft group (k, j) at an LQR solution with C dx = cxs, and its slacks
-    auto soft_vals = [&](const Grp& g, int k, int j, double cxs, double* v, double* slo, double* suo) {
-        const double h = hh[k * 3 + j];
+    auto soft_vals = [&](const Grp& g, int k, int j, double cxs, double* v) {
+        const double h = s.hv[k * 3 + j];
         const double sl = -(g.gl + g.s1 * cxs) / g.Hl, su = -(g.gu - g.s3 * cxs) / g.Hu;
-        v[0] = cxs + (h - A.lh[j]) + sl;
-        v[1] = -cxs + (A.uh[j] - h) + su;
+        v[0] = cxs + (h - s.cst[8 + j]) + sl;
+        v[1] = -cxs + (s.cst[11 + j] - h) + su;
         v[2] = sl;
         v[3] = su;
-        if (slo) *slo = sl;
-        if (suo) *suo = su;
     };
 
     // ------------------------------------------------------------ IPM iterations
@@ -598,9 +675,10 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         if (mu < A.tol && rp < A.tol) break;
         // -------- predictor: factorise, solve, affine step length and mu_aff
         STAMP(7);
-        backward(true, 0, 0.0);
+        terms(0, 0.0);
+        backward_factor();
         STAMP(2);
-        forward(s.dxc, s.dua, s.cxa);
+        forward(1, s.dxc, s.dua, s.cxa);
         STAMP(3);
         double amax = 1.0;
         auto bound = [&](double t, double l, double dt, double dl) {
@@ -617,7 +695,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
             const Grp g = group(k, j, 0, 0.0);
             double v[4];
-            soft_vals(g, k, j, s.cxa[e], v, nullptr, nullptr);
+            soft_vals(g, k, j, s.cxa[e], v);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q], dt = v[q] - t;
@@ -636,7 +714,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
             const Grp g = group(k, j, 0, 0.0);
             double v[4];
-            soft_vals(g, k, j, s.cxa[e], v, nullptr, nullptr);
+            soft_vals(g, k, j, s.cxa[e], v);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q], dt = v[q] - t;
@@ -648,9 +726,10 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double sigmu = sig * mu;
         // -------- corrector: same factorisation, new gradient
         STAMP(4);
-        backward(false, 1, sigmu);
+        terms(1, sigmu);
+        backward_corrector();
         STAMP(5);
-        forward(s.dxc, s.duc, s.cxc);
+        forward(1, s.dxc, s.duc, s.cxc);
         STAMP(3);
         // direction of row r: dt = val(z_c) - t, dl = -sigma dt - l - (dt_a dl_a - sigma mu) / t
         amax = 1.0;
@@ -665,8 +744,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
             const Grp ga = group(k, j, 0, 0.0), gc = group(k, j, 1, sigmu);
             double va[4], vc[4];
-            soft_vals(ga, k, j, s.cxa[e], va, nullptr, nullptr);
-            soft_vals(gc, k, j, s.cxc[e], vc, nullptr, nullptr);
+            soft_vals(ga, k, j, s.cxa[e], va);
+            soft_vals(gc, k, j, s.cxc[e], vc);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q];
@@ -691,9 +770,9 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         for (int e = lane; e < N1 * NS; e += 64) {
             const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
             const Grp ga = group(k, j, 0, 0.0), gc = group(k, j, 1, sigmu);
-            double va[4], vc[4], slc, suc;
-            soft_vals(ga, k, j, s.cxa[e], va, nullptr, nullptr);
-            soft_vals(gc, k, j, s.cxc[e], vc, &slc, &suc);
+            double va[4], vc[4];
+            soft_vals(ga, k, j, s.cxa[e], va);
+            soft_vals(gc, k, j, s.cxc[e], vc);
             double tn[4], ln[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -709,9 +788,6 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
                 s.t[r0 + q] = tn[q];
                 s.lam[r0 + q] = ln[q];
             }
-            s.sl[e] += al * (slc - s.sl[e]);
-            s.su[e] += al * (suc - s.su[e]);
-            s.cx[e] += al * (s.cxc[e] - s.cx[e]);
         }
         for (int e = lane; e < N1 * NX; e += 64) s.dx[e] += al * (s.dxc[e] - s.dx[e]);
         for (int e = lane; e < N * NU; e += 64) s.du[e] += al * (s.duc[e] - s.du[e]);
@@ -724,10 +800,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // ------------------------------------------------------------ outputs
     for (int e = lane; e < N1 * NX; e += 64) A.dx[(size_t)b * N1 * NX + e] = s.dx[e];
     for (int e = lane; e < N * NU; e += 64) A.du[(size_t)b * N * NU + e] = s.du[e];
-    if (A.slack)
+    if (A.slack)  // slacks = the t of rows sl >= 0, su >= 0 (equal to the iterate's sl, su up to r_p)
         for (int e = lane; e < N1 * NS; e += 64) {
-            A.slack[((size_t)b * N1 * NS + e) * 2] = s.sl[e];
-            A.slack[((size_t)b * N1 * NS + e) * 2 + 1] = s.su[e];
+            const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
+            A.slack[((size_t)b * N1 * NS + e) * 2] = s.t[r0 + 2];
+            A.slack[((size_t)b * N1 * NS + e) * 2 + 1] = s.t[r0 + 3];
         }
     if (lane == 0) {
         A.iters[b] = it;
@@ -760,8 +837,11 @@ hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx
 
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rti_qp_pack_kernel, dim3((unsigned)(a.B * (a.N + 1))), dim3(256), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
     const size_t lds = qp_lds_bytes(a.N);
-    hipError_t e = hipFuncSetAttribute((const void*)rti_qp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    e = hipFuncSetAttribute((const void*)rti_qp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rti_qp_kernel, dim3(a.B), dim3(64), lds, s, a);
     return hipGetLastError();

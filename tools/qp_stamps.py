@@ -28,7 +28,7 @@ for k, s in sh.items():
 torch.cuda.synchronize()
 _lib.linearize(ctx, net, _lib.quad_model(cfg), B, N, prob["p"].shape[-1], t)
 ctx.synchronize()
-path = os.path.join(ROOT, "gpurun_out", "qp_in.bin")
+path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "qp_in.bin")
 os.makedirs(os.path.dirname(path), exist_ok=True)
 with open(path, "wb") as f:
     f.write(np.array([B, N], np.int32).tobytes())
