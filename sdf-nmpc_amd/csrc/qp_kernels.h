@@ -25,7 +25,7 @@ struct QpArgs {
 };
 
 constexpr int QP_REC = 300;   // stage record: [A B | c | g | C | H upper]          (rti_qp.hip)
-constexpr int QP_FREC = 64;   // factor record: [Y | chol(R^) (1/diag) | k_ff | P_{k+1} c_k]
+constexpr int QP_FREC = 216;  // factor record: [A~|b~ | K|k_ff | Y | chol(R^) (1/diag) | P_{k+1} c_k | 2 spare]
 constexpr int QP_RING = 3;    // records in flight per wavefront
 
 // global workspace per instance: stage records and factor records for nodes 0..N
@@ -37,13 +37,12 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
            + 2 * N1 * 10            // dx, dxc
            + 3 * (size_t)N * 4      // du, dua, duc
            + 2 * N1 * 3             // cxa, cxc
-           + QP_REC + QP_FREC       // committed stage / factor record
-           + QP_RING * QP_FREC      // factor records of nodes 0..RING-1 (written late in a backward sweep)
-           + 100 + 10               // P, p
-           + 150 + 196 + 14         // W = P [A B c], M, m
+           + QP_REC + 192           // committed stage record / factor-record window
+           + QP_RING * 154          // [A~|b~ K|k_ff] of nodes 0..RING-1 (written late in a backward sweep)
+           + 16                     // corrector p
            + 4 * (size_t)N + 4 * N1 // u, (h, s_k)
-           + 6 * N1 + 8 * (size_t)N   // soft-row folds (w, gamma), box terms (diag, v)
-           + 20;                      // box / soft-row constants
+           + 6 * N1 + 8 * (size_t)N // soft-row folds (w, gamma), box terms (diag, v)
+           + 20;                    // box / soft-row constants
 }
 __host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N) * sizeof(double); }
 

@@ -13,15 +13,24 @@
 //   * soft-constraint slacks (diagonal Hessian) are eliminated per row: a rank-3 update of the
 //     node's state block; these folds and the box terms are formed for all nodes in one parallel
 //     pass before each sweep, so the serial sweeps hold no division
-//   * one factorisation per iteration serves predictor and corrector:
-//       Y = L^-1 S, P <- Q^ - Y^T Y, p <- m_x - Y^T (L^-1 m_u), K = -L^-T Y, k = -L^-T L^-1 m_u
-//     with L = chol(R^) (rsq + Newton; the reciprocal diagonal is what is stored)
+//   * one factorisation per iteration serves predictor and corrector.  With G = [A B c] (10 x 15),
+//     the factor stage runs on f64 MFMA 16x16x4 tiles held in registers:
+//         W  = P G                      (P c -> factor record; p added to column 14)
+//         M' = G_ab^T W + [H | g] + C^T diag(w) [C | gamma] + box terms       ([R^ S; S^T Q^ | m])
+//         L  = chol(R^), [Y | w] = L^-1 [S | m_u], [K | k_ff] = -L^-T [Y | w]
+//         [P | p] <- M' - Y^T [Y | w],  [A~ | b~] = [A | c] + B [K | k_ff]
+//     P is symmetric, so the accumulator of one stage is the A operand of the next with no lane
+//     movement (C/D lane (g, c) holds rows g + 4r of column c; A/B lane (g, c) holds k = 4s + g).
+//     The forward sweep is then one 17-row matvec per stage: [A~; K; C^T] x + [b~; k_ff; 0].
 // Memory: rti_qp_pack_kernel packs per-stage records [A B | c | g | C | H] into a global workspace
-// (a wide launch, one block per stage).  Each IPM iteration then walks the records in a fixed order
-// -- backward (factor), forward, backward (corrector), forward -- so they form one stream that is
-// prefetched QP_RING records ahead through registers, across sweep boundaries.  Iterate, duals and
-// stage scratch live in LDS (< 40 KB at N = 40: 4 instances per CU, one round for B = 1024).
+// (a wide launch, one block per stage).  Each IPM iteration walks the records in a fixed order --
+// backward (factor), forward, backward (corrector), forward -- so they form one stream prefetched
+// QP_RING records ahead through registers, across sweep boundaries (each sweep loads a fixed window
+// of the stage record and of the factor record).  Iterate, duals and stage scratch live in LDS
+// (< 40 KB at N = 40: 4 instances per CU, one round for B = 1024).
 #include <hip/hip_runtime.h>
+
+#include <type_traits>
 
 #include "qp_kernels.h"
 
@@ -32,18 +41,20 @@ namespace {
 // LDS pointers must keep address space 3: a generic pointer compiles to flat_load/store, whose waits
 // (vmcnt(0) AND lgkmcnt(0)) drain every global prefetch in flight at each LDS access.
 typedef __attribute__((address_space(3))) double ldsd;
+typedef double d4 __attribute__((ext_vector_type(4)));
 
 constexpr int NX = 10, NU = 4, NS = 3;
 // stage record (doubles): [AB 140 (column j = d xn / d (x,u)_j) | c 10 | g 14 | C 30 | H 105 upper]
 constexpr int R_AB = 0, R_C = 140, R_G = 150, R_CH = 164, R_H = 194, REC = QP_REC;
-constexpr int RR = (REC + 63) / 64;  // prefetch registers per lane per record
-// factor record: [Y 40 (4x10 row-major) | L 10 (lower packed, diagonal holds 1/L_ii) | kff 4 | P c 10]
-constexpr int F_Y = 0, F_L = 40, F_K = 50, F_PC = 54, FREC = QP_FREC;
+// factor record: [A~|b~ 10 x 11 | K|k_ff 4 x 11 | Y 4 x 10 | L 10 (lower packed, diagonal 1/L_ii) | P c 10 | 2 spare]
+constexpr int F_AB = 0, F_K = 110, F_Y = 154, F_L = 194, F_PC = 204, FREC = QP_FREC;
+constexpr int F_FW = 154;             // forward sweeps read [0, F_FW); the corrector reads [F_FW, FREC)
+constexpr int RW = 5, FW = 3;         // ring window per record: RW * 64 stage, FW * 64 factor doubles
 constexpr int PD = QP_RING;
-static_assert(FREC <= 64 && PD == 3, "ring layout");
+static_assert(FREC == 216 && PD == 3 && RW * 64 >= REC && FW * 64 >= F_FW, "record layout");
 
 __device__ __forceinline__ int tri10(int a, int c) { return a * 10 - a * (a - 1) / 2 + (c - a); }  // a <= c
-__device__ __forceinline__ int ltri4(int i, int j) { return i * (i + 1) / 2 + j; }                  // j <= i
+__device__ __forceinline__ int tri14(int a, int c) { return a * 14 - a * (a - 1) / 2 + (c - a); }  // a <= c
 
 __device__ __forceinline__ double wsum(double v) {
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
@@ -57,13 +68,21 @@ __device__ __forceinline__ double wmin(double v) {
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
     return v;
 }
-// 1/sqrt(v), v > 0: hardware estimate + two Newton steps (full double precision)
+// value of lane l (wave-uniform l) in every lane, via scalar registers
+__device__ __forceinline__ double rdlane(double v, int l) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
+    const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+// 1/sqrt(v), v > 0: hardware estimate + one Newton step
 __device__ __forceinline__ double rsqrt_nr(double v) {
     double y = __builtin_amdgcn_rsq(v);
     const double h = 0.5 * v;
-    y = y * fma(-h * y, y, 1.5);
-    y = y * fma(-h * y, y, 1.5);
-    return y;
+    return y * fma(-h * y, y, 1.5);
 }
 
 struct Smem {
@@ -71,9 +90,8 @@ struct Smem {
     ldsd *dx, *dxc;                // iterate dx; sweep solution (x of predictor, then corrector)
     ldsd *du, *dua, *duc;          // iterate du; affine / corrector du
     ldsd *cxa, *cxc;               // C dx of the affine / corrector solution
-    ldsd *rec, *frc, *fsave;       // committed stage record, factor record; F records of nodes < PD
-    ldsd *P, *p;                   // Riccati P (full 10x10), p (updated in place, one wavefront)
-    ldsd *W, *M, *m;               // W = P [A B c] (10 x 15), M (14 x 14), m (14)
+    ldsd *rec, *frc, *fsave;       // committed stage record / factor-record window; [A~|b~ K|k_ff] of nodes < PD
+    ldsd* p;                       // corrector Riccati vector p (the factor sweep keeps p in registers)
     ldsd *uu, *hv, *skv;           // u (box constants), h, cost scaling per node
     ldsd *fw, *fg, *bd, *bv;       // soft folds [N+1][3] (w, gamma), box terms [N][4] (diag, v)
     ldsd* cst;                     // lbu 4 | ubu 4 | lh 3 | uh 3 | zl 3 | Zl 3 (lane-indexed kernel arguments
@@ -88,9 +106,8 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubl
     s.dx = take(N1 * NX); s.dxc = take(N1 * NX);
     s.du = take(N * NU); s.dua = take(N * NU); s.duc = take(N * NU);
     s.cxa = take(N1 * NS); s.cxc = take(N1 * NS);
-    s.rec = take(REC); s.frc = take(FREC); s.fsave = take(PD * FREC);
-    s.P = take(100); s.p = take(10);
-    s.W = take(150); s.M = take(196); s.m = take(14);
+    s.rec = take(REC); s.frc = take(FW * 64); s.fsave = take(PD * F_FW);
+    s.p = take(16);
     s.uu = take(N * NU); s.hv = take(N1 * NS); s.skv = take(N1);
     s.fw = take(N1 * NS); s.fg = take(N1 * NS); s.bd = take(N * NU); s.bv = take(N * NU);
     s.cst = take(20);
@@ -166,9 +183,9 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
 }
 
 #ifdef QP_STAMPS  // diagnostic build only: per-phase cycle accounting (never in the product build)
-#define STAMP_DECL long long st_t0 = clock64(), st_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP_DECL long long st_t0 = clock64(), st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define STAMP(i) do { const long long t1_ = clock64(); st_acc[i] += t1_ - st_t0; st_t0 = t1_; } while (0)
-#define STAMP_OUT if (lane == 0 && A.stamps) for (int i_ = 0; i_ < 8; ++i_) A.stamps[(size_t)b * 8 + i_] = (double)st_acc[i_];
+#define STAMP_OUT if (lane == 0 && A.stamps) for (int i_ = 0; i_ < 12; ++i_) A.stamps[(size_t)b * 12 + i_] = (double)st_acc[i_];
 #else
 #define STAMP_DECL
 #define STAMP(i)
@@ -178,56 +195,58 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
 __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     extern __shared__ __align__(16) double lds_q[];
     STAMP_DECL
-    const int b = blockIdx.x, lane = threadIdx.x;
+    const int b = blockIdx.x, lane = threadIdx.x, lg = lane >> 4, lc = lane & 15;
     const int N = A.N, N1 = N + 1, m = 8 * N + 12 * N1;
     Smem s = carve((ldsd*)lds_q, N);
     const double* R = A.work + (size_t)b * qp_work_doubles(N);  // [N+1][REC] stage records
     double* F = A.work + (size_t)b * qp_work_doubles(N) + (size_t)N1 * REC;  // [N+1][FREC]
 
     // ------------------------------------------------------------ record stream
-    // stream index j: [0, N1) initial forward (k = j); then per IPM iteration 4 sweeps of N1 records:
-    // backward-factor (full record), forward (record + Y, L, kff), backward-corrector (record + F),
-    // forward.  Slot j % PD of the register ring holds record j; consuming j issues j + PD.
-    double rr[PD][RR], fr[PD];
-    auto decode = [&](int j, int& k, int& n, int& nf) {
-        if (j < N1) { k = j; n = R_H; nf = 0; return; }
-        const int jj = j - N1, q = jj % N1, t = (jj / N1) & 3;
-        k = (t & 1) ? q : N - q;
-        n = t == 0 ? REC : R_H;
-        nf = t == 0 ? 0 : (t == 2 ? FREC : F_PC);
+    // sweep types: 0 initial forward, then per IPM iteration 1 backward-factor, 2 forward,
+    // 3 backward-corrector, 4 forward.  Each sweep takes NP = N+1 rounded up to a multiple of PD
+    // stream positions (the tail positions load a clamped record and are skipped), so every sweep
+    // starts at ring slot 0 and the sweep loop, unrolled by PD, indexes the register ring
+    // statically: the compiler then waits only for the slot being committed (vmcnt of the two
+    // younger slots) instead of draining the stream.  Window per type: stage record from r0,
+    // factor record from f0; every issue is the same RW + FW unpredicated loads (clamped addresses).
+    const int NP = (N1 + PD - 1) / PD * PD;
+    struct Pos { int t, q; };
+    auto next = [&](Pos& p) {
+        if (++p.q == NP) { p.q = 0; p.t = p.t == 4 ? 1 : p.t + 1; }
     };
-    // every issue is the same RR + 1 unpredicated loads (clamped addresses): a data-dependent load
-    // count would make the compiler's wait counters conservative (vmcnt(0) at every commit)
-    auto issue_to = [&](double* rd, double& fd, int j) {
-        int k, n, nf;
-        decode(j, k, n, nf);
+    auto win_r = [](int t) { return (t == 2 || t == 4) ? R_CH : 0; };
+    auto win_f = [](int t) { return t == 3 ? F_FW : 0; };
+    double rr[PD][RW], fr[PD][FW];
+    auto issue_to = [&](double* rd, double* fd, const Pos& p) {
+        const int qq = p.q < N ? p.q : N;
+        const int k = (p.t == 1 || p.t == 3) ? N - qq : qq, r0 = win_r(p.t), f0 = win_f(p.t);
         const double* src = R + (size_t)k * REC;
+        const double* fsrc = F + (size_t)k * FREC;
 #pragma unroll
-        for (int i = 0; i < RR; ++i) {
-            const int e = lane + 64 * i;
+        for (int i = 0; i < RW; ++i) {
+            const int e = r0 + lane + 64 * i;
             rd[i] = src[e < REC ? e : REC - 1];
         }
-        fd = F[(size_t)k * FREC + lane];
-    };
-    auto commit_from = [&](const double* rd, double fd) {
 #pragma unroll
-        for (int i = 0; i < RR; ++i) {
-            const int e = lane + 64 * i;
+        for (int i = 0; i < FW; ++i) {
+            const int e = f0 + lane + 64 * i;
+            fd[i] = fsrc[e < FREC ? e : FREC - 1];
+        }
+    };
+    auto commit_from = [&](const double* rd, const double* fd, int t) {
+        const int r0 = win_r(t);
+#pragma unroll
+        for (int i = 0; i < RW; ++i) {
+            const int e = r0 + lane + 64 * i;
             if (e < REC) s.rec[e] = rd[i];
         }
-        s.frc[lane] = fd;
+#pragma unroll
+        for (int i = 0; i < FW; ++i) s.frc[lane + 64 * i] = fd[i];
     };
-    int pos = 0;
-    auto advance = [&]() {  // commit record `pos` to LDS, refill its slot with record pos + PD
-        const int sl = pos % PD;
-        if (sl == 0) { commit_from(rr[0], fr[0]); issue_to(rr[0], fr[0], pos + PD); }
-        else if (sl == 1) { commit_from(rr[1], fr[1]); issue_to(rr[1], fr[1], pos + PD); }
-        else { commit_from(rr[2], fr[2]); issue_to(rr[2], fr[2], pos + PD); }
-        ++pos;
-    };
-    issue_to(rr[0], fr[0], 0);
-    issue_to(rr[1], fr[1], 1);
-    issue_to(rr[2], fr[2], 2);
+    Pos pi{0, 0};
+    issue_to(rr[0], fr[0], pi); next(pi);
+    issue_to(rr[1], fr[1], pi); next(pi);
+    issue_to(rr[2], fr[2], pi); next(pi);
 
     // ------------------------------------------------------------ per-node constants into LDS
     for (int e = lane; e < N * NU; e += 64) {
@@ -256,28 +275,6 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     __syncthreads();
     STAMP(0);
 
-    // per-lane output maps of the three factor steps (fixed for the whole solve)
-    // step 1: W[i][j] = P[i,:] . [A B c][:, j], e = i * 15 + j < 150
-    const int e1b = lane + 64, e1c = (lane + 128 < 150) ? lane + 128 : 149;
-    const int w_i0 = lane / 15, w_j0 = lane % 15, w_i1 = e1b / 15, w_j1 = e1b % 15, w_i2 = e1c / 15, w_j2 = e1c % 15;
-    // step 2: (a, c), a <= c < 14 (M upper, row-major) then (a, 14) = m
-    auto m_map = [](int e, int& a, int& c) {
-        if (e >= 105) { a = e - 105; c = 14; return; }
-        int q = e;
-        a = 0;
-        while (q >= 14 - a) { q -= 14 - a; ++a; }
-        c = a + q;
-    };
-    int m_a0, m_c0, m_a1, m_c1;
-    m_map(lane, m_a0, m_c0);
-    m_map(lane + 64 < 119 ? lane + 64 : 118, m_a1, m_c1);
-    const bool m_has1 = lane + 64 < 119;
-    // step 3: e < 100: P[a][c]; e >= 100: p[e - 100]
-    const int p_a0 = lane / 10, p_c0 = lane % 10;
-    const int p_e1 = (lane + 64 < 110) ? lane + 64 : 109;
-    const int p_a1 = p_e1 < 100 ? p_e1 / 10 : p_e1 - 100, p_c1 = p_e1 < 100 ? p_e1 % 10 : -1;
-    const bool p_has1 = lane + 64 < 110;
-
     // box rows (k, i, up): t = +-du + d, d = (u - lbu) | (ubu - u)
     auto box_d = [&](int k, int i, int up) -> double {
         const double u = s.uu[k * 4 + i];
@@ -285,62 +282,31 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     };
 
     // ------------------------------------------------------------ forward sweep (1 barrier per stage)
-    // mode 0: initial iterate (u = 0); mode 1: u_k = k_ff - L^-T (Y x_k).  x_{k+1} = A x_k + B u_k + c_k,
-    // cx = C x.  Factor data of nodes < PD comes from fsave (written late in the backward sweep).
-    auto forward = [&](int mode, ldsd* dxo, ldsd* duo, ldsd* cxo) {
-        if (lane < NX) dxo[lane] = s.dx[lane];
-        for (int k = 0; k < N1; ++k) {
-            advance();
-            __syncthreads();
-            const ldsd* rk = s.rec;
-            const ldsd* fk = (k < PD) ? s.fsave + k * FREC : s.frc;
-            const ldsd* x = dxo + k * NX;
-            if (lane >= 16 && lane < 16 + NS) {
-                const int j = lane - 16;
-                double v = 0.0;
+    // lane r computes row r of [A~; K] x + [b~; k_ff] (r < 14) or (C^T x)_{r-14} (r = 14..16);
+    // mode 0 (initial iterate, u = 0): rows r < 10 of A x + c from the stage record.
+    // Factor data of nodes < PD comes from fsave (written late in the backward sweeps).
+    const int fw_cx = (lane >= 14 && lane < 17) ? lane - 14 : 0;
+    ldsd* const ljunk = s.p + 15;  // spare LDS double: stores of inactive lanes
+    const int fw_r = lane < NX ? lane : 0;
+    auto fw_stage = [&](int k, int mode, ldsd* dxo, ldsd* duo, ldsd* cxo) {
+        const ldsd* fk = (k < PD) ? s.fsave + k * F_FW : s.frc;
+        const ldsd* crow = s.rec + R_CH + fw_cx;
+        const ldsd* row = lane >= 14 ? crow : mode ? fk + lane * 11 : s.rec + fw_r;
+        const int stride = lane >= 14 ? 3 : mode ? 1 : 10;
+        const double o = mode ? row[10] : s.rec[R_C + fw_r];
+        double v = lane >= 14 ? 0.0 : o;
+        const ldsd* x = dxo + k * NX;
 #pragma unroll
-                for (int l = 0; l < NX; ++l) v += rk[R_CH + l * 3 + j] * x[l];
-                cxo[k * NS + j] = v;
-            }
-            if (k < N && lane < NX) {
-                double xv[NX];
-#pragma unroll
-                for (int l = 0; l < NX; ++l) xv[l] = x[l];
-                double u[4] = {0.0, 0.0, 0.0, 0.0};
-                if (mode) {
-                    double yx[4];
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        double v = 0.0;
-#pragma unroll
-                        for (int l = 0; l < NX; ++l) v += fk[F_Y + i * 10 + l] * xv[l];
-                        yx[i] = v;
-                    }
-#pragma unroll
-                    for (int i = 3; i >= 0; --i) {
-                        double v = yx[i];
-#pragma unroll
-                        for (int q = i + 1; q < 4; ++q) v -= fk[F_L + ltri4(q, i)] * u[q];
-                        u[i] = v * fk[F_L + ltri4(i, i)];
-                    }
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) u[i] = fk[F_K + i] - u[i];
-                }
-                double v = rk[R_C + lane];
-#pragma unroll
-                for (int j = 0; j < NX; ++j) v += rk[R_AB + j * 10 + lane] * xv[j];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v += rk[R_AB + (NX + i) * 10 + lane] * u[i];
-                dxo[(k + 1) * NX + lane] = v;
-                if (mode && lane < 4) duo[k * NU + lane] = u[lane];
-            }
-            __syncthreads();
-        }
+        for (int l = 0; l < NX; ++l) v += row[l * stride] * x[l];
+        ldsd* dst = (lane >= 14 && lane < 17) ? cxo + k * NS + fw_cx
+                  : (k < N && lane < NX) ? dxo + (k + 1) * NX + lane
+                  : (mode && k < N && lane >= NX && lane < 14) ? duo + k * NU + lane - NX : ljunk;
+        *dst = v;
     };
 
     // ------------------------------------------------------------ initial iterate (dynamics-feasible):
-    // du = sl = su = 0, dx_0 = x0 - xbar_0, dx_{k+1} = A dx_k + c_k
-    forward(0, s.dx, nullptr, s.cxa);
+    // du = sl = su = 0, dx_0 = x0 - xbar_0, dx_{k+1} = A dx_k + c_k (sweep 0), then the rows
+    auto rows_init = [&]() -> double {
     double rp = 0.0;
     for (int r = lane; r < m; r += 64) {
         double v;
@@ -357,9 +323,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         s.lam[r] = 1.0;
         rp = fmax(rp, fabs(v - t));
     }
-    rp = wmax(rp);
-    __syncthreads();
-    STAMP(1);
+    return wmax(rp);
+    };
 
     // soft group (k, j) = rows (hl, hu, sl, su): barrier weights, v's, eliminated slack block
     struct Grp {
@@ -423,234 +388,189 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         __syncthreads();
     };
 
-    // ------------------------------------------------------------ backward sweep, factor (3 barriers / stage)
-    auto backward_factor = [&]() {
-        for (int q = 0; q < N1; ++q) {
-            const int k = N - q;
-            advance();
-            __syncthreads();
-            const ldsd* rk = s.rec;
-            if (q == 0) {  // P_N = H_N + sum_j w_j C_j^T C_j, p_N = g_N + sum_j gamma_j C_j^T
-                for (int e = lane; e < 110; e += 64) {
-                    if (e < 100) {
-                        const int a = e / 10, c = e % 10;
-                        double v = rk[R_H + tri10(a < c ? a : c, a < c ? c : a)];
-                        for (int j = 0; j < NS; ++j) v += s.fw[N * NS + j] * rk[R_CH + a * 3 + j] * rk[R_CH + c * 3 + j];
-                        s.P[e] = v;
-                    } else {
-                        const int a = e - 100;
-                        double v = rk[R_G + a];
-                        for (int j = 0; j < NS; ++j) v += s.fg[N * NS + j] * rk[R_CH + a * 3 + j];
-                        s.p[a] = v;
-                    }
-                }
-                __syncthreads();
-                continue;
+
+    // ------------------------------------------------------------ backward sweep, factor (MFMA tiles)
+    // Lane maps (fixed for the solve): accumulator rows a_r = lg + 4 r of column lc; operand k-step s
+    // covers k = 4 s + lg.  Everything lane-dependent is precomputed as (valid LDS index, flag) pairs
+    // and applied with selects, and stores of inactive lanes go to junk slots: no divergent branches
+    // (each costs a string of exec-mask SALU work per stage).
+    const int JUNK = FREC - 2;                          // two spare doubles per factor record
+    int hsrc[4], tsrc[4], abi[4], sab[3], spc[3];
+    bool hok[4], tok[4], abok[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int a = lg + 4 * r, c = lc, lo = a < c ? a : c, hi = a < c ? c : a;
+        hok[r] = a < 14 && c <= 14;
+        hsrc[r] = !hok[r] ? 0 : c < 14 ? R_H + tri14(lo, hi) : R_G + a;
+        tok[r] = a < NX && (c < NX || c == 14);
+        tsrc[r] = !tok[r] ? 0 : c < NX ? R_H + tri10(lo, hi) : R_G + a;
+        abok[r] = (c < NX || c == 14) && a < NX;
+        abi[r] = abok[r] ? (c < NX ? c : 14) * 10 + a : 0;
+    }
+    const bool xcol = lc < NX || lc == 14;        // columns of [P | p], [A | c], [K | k_ff]
+    const int xcol_o = lc < NX ? lc : 10;         // their column in the 11-wide factor-record rows
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int a = lg + 4 * r;
+        sab[r] = (xcol && a < NX) ? F_AB + a * 11 + xcol_o : JUNK;
+        spc[r] = (lc == 14 && a < NX) ? F_PC + a : JUNK;
+    }
+    const int sk_ = xcol ? F_K + lg * 11 + xcol_o : JUNK;
+    const int sy_ = lc < NX ? F_Y + lg * 10 + lc : JUNK;
+    const int sl_ = lane < 10 ? F_L + lane : JUNK;
+    int ogi[3];
+    bool ogok[3], paok[3];
+#pragma unroll
+    for (int st = 0; st < 3; ++st) {
+        const int kk = 4 * st + lg;
+        ogok[st] = lc < 15 && kk < NX;              // G = [A B c]: 15 columns, 10 rows
+        ogi[st] = ogok[st] ? lc * 10 + kk : 0;
+        paok[st] = lc < NX && kk < NX;
+    }
+    const bool cgok = lc < NX && lg < NS;
+    const int cgi = cgok ? R_CH + lc * 3 + lg : 0, lg3 = lg < NS ? lg : 0;
+    const int bmi = (NX + lg) * 10 + (lc < NX ? lc : 0);  // B[lc][lg] for the closed loop
+    const double eye = lc == NX + lg ? 1.0 : 0.0;          // A operand of the box-term product
+    auto fs_at = [&](int k, int e) -> ldsd* { return e < F_FW ? s.fsave + k * F_FW + e : ljunk; };
+
+    d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
+    auto bf_stage = [&](int q) {
+        const int k = N - q;
+        const ldsd* rk = s.rec;
+        // fold (rank 3): A[a][j] = C[a][j], B[j][c] = w_j C[c][j] (c < 10) | gamma_j (c = 14)
+        const double cgv = rk[cgi], cg = cgok ? cgv : 0.0;
+        const double fwj = s.fw[k * NS + lg3], fgj = s.fg[k * NS + lg3];
+        const double fb = lg >= NS ? 0.0 : lc < NX ? fwj * cg : (lc == 14 ? fgj : 0.0);
+        if (q == 0) {  // [P_N | p_N] = [H_N | g_N] + fold
+            d4 base;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const double v = rk[tsrc[r]];
+                base[r] = tok[r] ? v : 0.0;
             }
-            double* Fk = F + (size_t)k * FREC;
-            ldsd* Fs = s.fsave + k * FREC;  // meaningful for k < PD only
-            // ---- step 1: W = P [A B c] (10 x 15); column 14 -> P c (factor record) and P c + p
-            {
-                double a0 = 0.0, a1 = 0.0, a2 = 0.0;
+            Pa = mfma(cg, fb, base);
+            return;
+        }
+        double* Fk = F + (size_t)k * FREC;
+        // ---- W = P G (K = 10: k-steps 0..2, rows k >= 10 zero); column 14 -> P c, then + p
+        double og[3];
 #pragma unroll
-                for (int l = 0; l < NX; ++l) {
-                    a0 += s.P[w_i0 * 10 + l] * rk[w_j0 * 10 + l];
-                    a1 += s.P[w_i1 * 10 + l] * rk[w_j1 * 10 + l];
-                    a2 += s.P[w_i2 * 10 + l] * rk[w_j2 * 10 + l];
-                }
-                if (w_j0 == 14) { Fk[F_PC + w_i0] = a0; if (k < PD) Fs[F_PC + w_i0] = a0; a0 += s.p[w_i0]; }
-                if (w_j1 == 14) { Fk[F_PC + w_i1] = a1; if (k < PD) Fs[F_PC + w_i1] = a1; a1 += s.p[w_i1]; }
-                if (w_j2 == 14) { Fk[F_PC + w_i2] = a2; if (k < PD) Fs[F_PC + w_i2] = a2; a2 += s.p[w_i2]; }
-                s.W[lane] = a0;
-                s.W[e1b] = a1;
-                if (lane + 128 < 150) s.W[lane + 128] = a2;
-            }
-            __syncthreads();
-            // ---- step 2: M = H~ + [A B]^T W (upper), m = g~ + [A B]^T (P c + p), plus soft folds / box terms
-            {
-                const int fk3 = k * NS, bk4 = k * 4;
-                auto mval = [&](int a, int c, double acc) -> double {
-                    double v = acc;
-                    if (c < 14) {
-                        v += rk[R_H + a * 14 - a * (a - 1) / 2 + (c - a)];
-                        if (c < NX) {
+        for (int st = 0; st < 3; ++st) {
+            const double v = rk[ogi[st]];
+            og[st] = ogok[st] ? v : 0.0;
+        }
+        d4 W = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                            for (int j = 0; j < NS; ++j) v += s.fw[fk3 + j] * rk[R_CH + a * 3 + j] * rk[R_CH + c * 3 + j];
-                        } else if (a == c) {
-                            v += s.bd[bk4 + a - NX];
-                        }
-                    } else {
-                        v += rk[R_G + a];
-                        if (a < NX) {
+        for (int st = 0; st < 3; ++st) W = mfma(paok[st] ? Pa[st] : 0.0, og[st], W);
 #pragma unroll
-                            for (int j = 0; j < NS; ++j) v += s.fg[fk3 + j] * rk[R_CH + a * 3 + j];
-                        } else {
-                            v += s.bv[bk4 + a - NX];
-                        }
-                    }
-                    return v;
-                };
-                double a0 = 0.0, a1 = 0.0;
+        for (int r = 0; r < 3; ++r) Fk[spc[r]] = W[r];
+        const bool c14 = lc == 14;
 #pragma unroll
-                for (int l = 0; l < NX; ++l) {
-                    a0 += rk[m_a0 * 10 + l] * s.W[l * 15 + m_c0];
-                    a1 += rk[m_a1 * 10 + l] * s.W[l * 15 + m_c1];
-                }
-                const double v0 = mval(m_a0, m_c0, a0), v1 = mval(m_a1, m_c1, a1);
-                if (m_c0 < 14) { s.M[m_a0 * 14 + m_c0] = v0; s.M[m_c0 * 14 + m_a0] = v0; } else { s.m[m_a0] = v0; }
-                if (m_has1) {
-                    if (m_c1 < 14) { s.M[m_a1 * 14 + m_c1] = v1; s.M[m_c1 * 14 + m_a1] = v1; } else { s.m[m_a1] = v1; }
-                }
-            }
-            __syncthreads();
-            // ---- step 3: L = chol(R^) (every lane, registers), y_a = L^-1 S[:, a], w = L^-1 m_u;
-            //      P_k = Q^ - Y^T Y, p_k = m_x - Y^T w (in place); factor record (Y, L, k_ff)
-            double L[4][4], id[4];
+        for (int r = 0; r < 4; ++r) W[r] += c14 ? Pa[r] : 0.0;
+        // ---- M' = G_ab^T W + [H | g] + fold + box terms (identity rows 10..13 times [diag | v])
+        d4 M;
 #pragma unroll
-            for (int i = 0; i < 4; ++i)
+        for (int r = 0; r < 4; ++r) {
+            const double v = rk[hsrc[r]];
+            M[r] = hok[r] ? v : 0.0;
+        }
+        const double bdv = s.bd[k * 4 + lg], bvv = s.bv[k * 4 + lg];
+        M = mfma(eye, lc == NX + lg ? bdv : (c14 ? bvv : 0.0), M);
+        M = mfma(cg, fb, M);
 #pragma unroll
-                for (int j = 0; j <= i; ++j) {
-                    double v = s.M[(NX + i) * 14 + NX + j];
+        for (int st = 0; st < 3; ++st) M = mfma(lc < 14 ? og[st] : 0.0, W[st], M);
+        // ---- rows 10..13 of M' ([S | R^ | m_u]) of column lc into every lane of that column
+        const double s0 = __shfl(M[2], 32 + lc), s1 = __shfl(M[2], 48 + lc);
+        const double s2 = __shfl(M[3], lc), s3 = __shfl(M[3], 16 + lc);
+        // L = chol(R^): R^[i][j] is s_i of lane 10 + j (uniform, scalar registers)
+        const double r00 = rdlane(s0, 10), r10 = rdlane(s1, 10), r20 = rdlane(s2, 10), r30 = rdlane(s3, 10);
+        const double r11 = rdlane(s1, 11), r21 = rdlane(s2, 11), r31 = rdlane(s3, 11);
+        const double r22 = rdlane(s2, 12), r32 = rdlane(s3, 12), r33 = rdlane(s3, 13);
+        const double i0 = rsqrt_nr(r00);
+        const double l10 = r10 * i0, l20 = r20 * i0, l30 = r30 * i0;
+        const double i1 = rsqrt_nr(r11 - l10 * l10);
+        const double l21 = (r21 - l20 * l10) * i1, l31 = (r31 - l30 * l10) * i1;
+        const double i2 = rsqrt_nr(r22 - l20 * l20 - l21 * l21);
+        const double l32 = (r32 - l30 * l20 - l31 * l21) * i2;
+        const double i3 = rsqrt_nr(r33 - l30 * l30 - l31 * l31 - l32 * l32);
+        // column lc of [Y | w] = L^-1 [S | m_u] and of [K | k_ff] = -L^-T [Y | w]
+        const double y0 = s0 * i0;
+        const double y1 = (s1 - l10 * y0) * i1;
+        const double y2 = (s2 - l20 * y0 - l21 * y1) * i2;
+        const double y3 = (s3 - l30 * y0 - l31 * y1 - l32 * y2) * i3;
+        const double k3 = -y3 * i3;
+        const double k2 = (-y2 - l32 * k3) * i2;
+        const double k1 = (-y1 - l21 * k2 - l31 * k3) * i1;
+        const double k0 = (-y0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
+        const double yg = lg == 0 ? y0 : lg == 1 ? y1 : lg == 2 ? y2 : y3;
+        const double kg = lg == 0 ? k0 : lg == 1 ? k1 : lg == 2 ? k2 : k3;
+        // ---- [P | p] <- M' - Y^T [Y | w];  [A~ | b~] = [A | c] + B [K | k_ff]
+        Pa = mfma(-yg, yg, M);
+        d4 Ab;
 #pragma unroll
-                    for (int q2 = 0; q2 < j; ++q2) v -= L[i][q2] * L[j][q2];
-                    if (i == j) {
-                        id[i] = rsqrt_nr(v);
-                        L[i][i] = v * id[i];
-                    } else {
-                        L[i][j] = v * id[j];
-                    }
-                }
-            auto fsub = [&](const ldsd* col, int stride, double* y) {
-                y[0] = col[0] * id[0];
-                y[1] = (col[stride] - L[1][0] * y[0]) * id[1];
-                y[2] = (col[2 * stride] - L[2][0] * y[0] - L[2][1] * y[1]) * id[2];
-                y[3] = (col[3 * stride] - L[3][0] * y[0] - L[3][1] * y[1] - L[3][2] * y[2]) * id[3];
-            };
-            double w[4], ya0[4], yc0[4], ya1[4], yc1[4];
-            fsub(s.m + NX, 1, w);
-            fsub(s.M + NX * 14 + p_a0, 14, ya0);
-            fsub(s.M + NX * 14 + p_c0, 14, yc0);
-            fsub(s.M + NX * 14 + p_a1, 14, ya1);
-            if (p_c1 >= 0) {
-                fsub(s.M + NX * 14 + p_c1, 14, yc1);
-            } else {
+        for (int r = 0; r < 4; ++r) {
+            const double v = rk[abi[r]];
+            Ab[r] = abok[r] ? v : 0.0;
+        }
+        const double bm = rk[bmi];
+        Ab = mfma(lc < NX ? bm : 0.0, kg, Ab);
+        // ---- factor record (and its LDS copy for the first forward stages)
+        const double lv = lane == 0 ? i0 : lane == 1 ? l10 : lane == 2 ? i1 : lane == 3 ? l20 : lane == 4 ? l21
+                        : lane == 5 ? i2 : lane == 6 ? l30 : lane == 7 ? l31 : lane == 8 ? l32 : i3;
 #pragma unroll
-                for (int i = 0; i < 4; ++i) yc1[i] = w[i];
-            }
-            double v0 = s.M[p_a0 * 14 + p_c0];
-            double v1 = p_c1 >= 0 ? s.M[p_a1 * 14 + p_c1] : s.m[p_a1];
+        for (int r = 0; r < 3; ++r) Fk[sab[r]] = Ab[r];
+        Fk[sk_] = kg;
+        Fk[sy_] = yg;
+        Fk[sl_] = lv;
+        if (k < PD) {
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                v0 -= ya0[i] * yc0[i];
-                v1 -= ya1[i] * yc1[i];
-            }
-            s.P[lane] = v0;
-            if (p_has1) {
-                if (p_c1 >= 0) s.P[p_e1] = v1; else s.p[p_a1] = v1;
-            }
-            if (lane < NX) {  // Y[:, c] with c = lane (a = 0)
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    Fk[F_Y + i * 10 + lane] = yc0[i];
-                    if (k < PD) Fs[F_Y + i * 10 + lane] = yc0[i];
-                }
-            }
-            if (lane >= 16 && lane < 26) {  // L, diagonal stored as 1/L_ii
-                const int e = lane - 16;
-                const int i = e >= 6 ? 3 : e >= 3 ? 2 : e >= 1 ? 1 : 0, j = e - i * (i + 1) / 2;
-                double v = 0.0;
-#pragma unroll
-                for (int ii = 0; ii < 4; ++ii)
-#pragma unroll
-                    for (int jj = 0; jj <= ii; ++jj)
-                        if (ii == i && jj == j) v = (ii == jj) ? id[ii] : L[ii][jj];
-                Fk[F_L + e] = v;
-                if (k < PD) Fs[F_L + e] = v;
-            }
-            if (lane >= 48 && lane < 52) {  // k_ff = -L^-T w
-                double kf[4];
-#pragma unroll
-                for (int i = 3; i >= 0; --i) {
-                    double v = w[i];
-#pragma unroll
-                    for (int q2 = i + 1; q2 < 4; ++q2) v -= L[q2][i] * kf[q2];
-                    kf[i] = v * id[i];
-                }
-                double v = 0.0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) if (lane - 48 == i) v = -kf[i];
-                Fk[F_K + lane - 48] = v;
-                if (k < PD) Fs[F_K + lane - 48] = v;
-            }
-            __syncthreads();
+            for (int r = 0; r < 3; ++r) *fs_at(k, sab[r]) = Ab[r];
+            *fs_at(k, sk_) = kg;
         }
     };
 
     // ------------------------------------------------------------ backward sweep, corrector (1 barrier / stage)
-    // stored factors + corrector gradient: Pb = P c + p, w = L^-1 m_u, p_k = m_x - Y^T w, k_ff = -L^-T w
-    auto backward_corrector = [&]() {
-        for (int q = 0; q < N1; ++q) {
-            const int k = N - q;
-            advance();
-            __syncthreads();
-            const ldsd* rk = s.rec;
-            if (q == 0) {
-                if (lane < NX) {
-                    double v = rk[R_G + lane];
-                    for (int j = 0; j < NS; ++j) v += s.fg[N * NS + j] * rk[R_CH + lane * 3 + j];
-                    s.p[lane] = v;
-                }
-                __syncthreads();
-                continue;
-            }
-            const ldsd* fk = s.frc;
-            double Pb[NX];
+    // stored factors + corrector gradient: Pb = P c + p, z = [g_x + A^T Pb + fold | g_u + B^T Pb + box],
+    // w = L^-1 z_u, p_k = z_x - Y^T w, k_ff = -L^-T w, b~ = c + B k_ff.  Lane r < 14 owns row r of z.
+    const int bc_r = lane < 14 ? lane : 0, bc_x = bc_r < NX ? bc_r : 0, bc_u = bc_r >= NX ? bc_r - NX : 0;
+    const int bc_st = lane < NX ? F_AB + lane * 11 + 10 : lane < 14 ? F_K + (lane - NX) * 11 + 10 : JUNK;
+    ldsd* const bc_p = lane < NX ? s.p + lane : ljunk;
+    auto bc_stage = [&](int q) {
+        const int k = N - q, r = bc_r;
+        const ldsd* rk = s.rec;
+        double fold = 0.0;
 #pragma unroll
-            for (int l = 0; l < NX; ++l) Pb[l] = fk[F_PC + l] + s.p[l];
-            double mu[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double v = rk[R_G + NX + i] + s.bv[k * 4 + i];
-#pragma unroll
-                for (int l = 0; l < NX; ++l) v += rk[R_AB + (NX + i) * 10 + l] * Pb[l];
-                mu[i] = v;
-            }
-            double w[4];
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                double v = mu[i];
-#pragma unroll
-                for (int q2 = 0; q2 < i; ++q2) v -= fk[F_L + ltri4(i, q2)] * w[q2];
-                w[i] = v * fk[F_L + ltri4(i, i)];
-            }
-            if (lane < NX) {
-                const int a = lane;
-                double v = rk[R_G + a];
-#pragma unroll
-                for (int l = 0; l < NX; ++l) v += rk[R_AB + a * 10 + l] * Pb[l];
-#pragma unroll
-                for (int j = 0; j < NS; ++j) v += s.fg[k * NS + j] * rk[R_CH + a * 3 + j];
-#pragma unroll
-                for (int i = 0; i < 4; ++i) v -= fk[F_Y + i * 10 + a] * w[i];
-                s.p[a] = v;
-            }
-            if (lane >= 16 && lane < 20) {
-                double kf[4];
-#pragma unroll
-                for (int i = 3; i >= 0; --i) {
-                    double v = w[i];
-#pragma unroll
-                    for (int q2 = i + 1; q2 < 4; ++q2) v -= fk[F_L + ltri4(q2, i)] * kf[q2];
-                    kf[i] = v * fk[F_L + ltri4(i, i)];
-                }
-                double v = 0.0;
-#pragma unroll
-                for (int i = 0; i < 4; ++i) if (lane - 16 == i) v = -kf[i];
-                F[(size_t)k * FREC + F_K + lane - 16] = v;
-                if (k < PD) s.fsave[k * FREC + F_K + lane - 16] = v;
-            }
-            __syncthreads();
+        for (int j = 0; j < NS; ++j) fold += s.fg[k * NS + j] * rk[R_CH + bc_x * 3 + j];
+        if (q == 0) {  // p_N = g_N + sum_j gamma_j C_j^T
+            *bc_p = rk[R_G + bc_x] + fold;
+            return;
         }
+        const ldsd* fk = s.frc - F_FW;  // factor-record window starts at F_FW
+        double z = rk[R_G + r];
+#pragma unroll
+        for (int l = 0; l < NX; ++l) z += rk[r * 10 + l] * (fk[F_PC + l] + s.p[l]);
+        const double bvv = s.bv[k * 4 + bc_u];
+        z += r < NX ? fold : bvv;
+        const double z0 = rdlane(z, 10), z1 = rdlane(z, 11), z2 = rdlane(z, 12), z3 = rdlane(z, 13);
+        const double i0 = fk[F_L + 0], l10 = fk[F_L + 1], i1 = fk[F_L + 2], l20 = fk[F_L + 3], l21 = fk[F_L + 4];
+        const double i2 = fk[F_L + 5], l30 = fk[F_L + 6], l31 = fk[F_L + 7], l32 = fk[F_L + 8], i3 = fk[F_L + 9];
+        const double w0 = z0 * i0;
+        const double w1 = (z1 - l10 * w0) * i1;
+        const double w2 = (z2 - l20 * w0 - l21 * w1) * i2;
+        const double w3 = (z3 - l30 * w0 - l31 * w1 - l32 * w2) * i3;
+        const double k3 = -w3 * i3;
+        const double k2 = (-w2 - l32 * k3) * i2;
+        const double k1 = (-w1 - l21 * k2 - l31 * k3) * i1;
+        const double k0 = (-w0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
+        const double pn = z - fk[F_Y + bc_x] * w0 - fk[F_Y + 10 + bc_x] * w1 - fk[F_Y + 20 + bc_x] * w2 -
+                          fk[F_Y + 30 + bc_x] * w3;
+        const double bb = rk[R_C + bc_x] + rk[(NX + 0) * 10 + bc_x] * k0 + rk[(NX + 1) * 10 + bc_x] * k1 +
+                          rk[(NX + 2) * 10 + bc_x] * k2 + rk[(NX + 3) * 10 + bc_x] * k3;
+        const double kv = bc_u == 0 ? k0 : bc_u == 1 ? k1 : bc_u == 2 ? k2 : k3;
+        const double fv = lane < NX ? bb : kv;
+        *bc_p = pn;
+        F[(size_t)k * FREC + bc_st] = fv;
+        if (k < PD) *fs_at(k, bc_st) = fv;
     };
 
     // row values of a soft group (k, j) at an LQR solution with C dx = cxs, and its slacks
@@ -663,23 +583,10 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         v[3] = su;
     };
 
-    // ------------------------------------------------------------ IPM iterations
-    int it = 0;
-    double mu;
-    {
-        double lmu = 0.0;
-        for (int r = lane; r < m; r += 64) lmu += s.t[r] * s.lam[r];
-        mu = wsum(lmu) / m;
-    }
-    for (it = 0; it < A.max_iter; ++it) {
-        if (mu < A.tol && rp < A.tol) break;
-        // -------- predictor: factorise, solve, affine step length and mu_aff
-        STAMP(7);
-        terms(0, 0.0);
-        backward_factor();
-        STAMP(2);
-        forward(1, s.dxc, s.dua, s.cxa);
-        STAMP(3);
+    // ------------------------------------------------------------ IPM: sweep driver
+    // predictor rows: affine step length, mu_aff -> sigma mu (Mehrotra)
+    double mu = 0.0, rp = 0.0;
+    auto rows_pred = [&]() -> double {
         double amax = 1.0;
         auto bound = [&](double t, double l, double dt, double dl) {
             if (dt < 0.0) amax = fmin(amax, -t / dt);
@@ -723,14 +630,15 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
         const double mua = wsum(lmua) / m;
         const double sig = (mua / mu) * (mua / mu) * (mua / mu);
-        const double sigmu = sig * mu;
-        // -------- corrector: same factorisation, new gradient
-        STAMP(4);
-        terms(1, sigmu);
-        backward_corrector();
-        STAMP(5);
-        forward(1, s.dxc, s.duc, s.cxc);
-        STAMP(3);
+        return sig * mu;
+    };
+    // corrector rows: step length, update of (t, lambda, du, dx), mu and the primal residual
+    auto rows_update = [&](double sigmu) {
+        double amax = 1.0;
+        auto bound = [&](double t, double l, double dt, double dl) {
+            if (dt < 0.0) amax = fmin(amax, -t / dt);
+            if (dl < 0.0) amax = fmin(amax, -l / dl);
+        };
         // direction of row r: dt = val(z_c) - t, dl = -sigma dt - l - (dt_a dl_a - sigma mu) / t
         amax = 1.0;
         for (int r = lane; r < 8 * N; r += 64) {
@@ -793,8 +701,59 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         for (int e = lane; e < N * NU; e += 64) s.du[e] += al * (s.duc[e] - s.du[e]);
         mu = wsum(lmu) / m;
         rp *= (1.0 - al);
+    };
+
+    int it = 0, kind = 0;
+    double sigmu = 0.0;
+    for (;;) {
+        // ---- before the sweep
+        if (kind == 1) {
+            if ((mu < A.tol && rp < A.tol) || it >= A.max_iter) break;
+            terms(0, 0.0);
+        } else if (kind == 3) {
+            sigmu = rows_pred();
+            terms(1, sigmu);
+        }
+        if ((kind == 2 || kind == 4) && lane < NX) s.dxc[lane] = s.dx[lane];
+        __syncthreads();
+        STAMP(4);
+        const int mode = kind != 0;
+        ldsd* dxo = kind == 0 ? s.dx : s.dxc;
+        ldsd* duo = kind == 4 ? s.duc : s.dua;
+        ldsd* cxo = kind == 4 ? s.cxc : s.cxa;
+        // ---- the sweep: NP stream positions, PD per trip with static ring slots
+        auto stage = [&](auto slot, int q) {
+            constexpr int S = decltype(slot)::value;
+            commit_from(rr[S], fr[S], kind);
+            issue_to(rr[S], fr[S], pi);
+            next(pi);
+            __syncthreads();
+            if (q < N1) {
+                if (kind == 1) bf_stage(q);
+                else if (kind == 3) bc_stage(q);
+                else fw_stage(q, mode, dxo, duo, cxo);
+            }
+            __syncthreads();
+        };
+        for (int q0 = 0; q0 < NP; q0 += PD) {
+            stage(std::integral_constant<int, 0>{}, q0);
+            stage(std::integral_constant<int, 1>{}, q0 + 1);
+            stage(std::integral_constant<int, 2>{}, q0 + 2);
+        }
+        STAMP(kind == 1 ? 2 : kind == 3 ? 5 : kind == 0 ? 1 : 3);
+        // ---- after the sweep
+        if (kind == 0) {
+            rp = rows_init();
+            double lmu = 0.0;
+            for (int r = lane; r < m; r += 64) lmu += s.t[r] * s.lam[r];
+            mu = wsum(lmu) / m;
+        } else if (kind == 4) {
+            rows_update(sigmu);
+            ++it;
+        }
         __syncthreads();
         STAMP(6);
+        kind = kind == 4 ? 1 : kind + 1;
     }
     STAMP_OUT
     // ------------------------------------------------------------ outputs
