@@ -8,10 +8,12 @@
 A "step" is one pass of the hot path over one batch: for every one of the B instances on this GPU,
 the SQP-RTI preparation phase over all N+1 shooting nodes (SDF forward + position-Jacobian,
 ERK4 + forward sensitivities, NONLINEAR_LS residual/Jacobian, h = [hfov, vfov, sdf] and its
-Jacobian); the JSON's config.phase says whether the QP feedback phase is inside the step.  Inputs
-are resident in HBM before the timed region.  value = instances x steps / time over ALL ranks (weak scaling: B
-instances per GPU).  One process per GPU; instances never interact, so there is no data-path
-collective; RCCL broadcasts the packed weights once at init and gathers u_0 per step.
+Jacobian) -- SURVEY.md §8(d)'s unit of work.  Inputs are resident in HBM before the timed region.
+value = instances x steps / time over ALL ranks (weak scaling: B instances per GPU).  The full RTI
+iteration (preparation + batched QP feedback phase + iterate update, i.e. one acados SQP_RTI
+solve) is timed in its own loop with the same barrier / max-over-ranks protocol and reported in
+"full_rti".  One process per GPU; instances never interact, so there is no data-path collective;
+RCCL broadcasts the packed weights once at init.
 """
 import argparse
 import json
@@ -48,6 +50,7 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=64, help="instances in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quiet", action="store_true")
+    ap.add_argument("--rti-steps", type=int, default=10, help="timed full-RTI steps (0: skip)")
     args = ap.parse_args()
 
     import torch
@@ -96,29 +99,50 @@ def main():
         bufs[k] = torch.empty(s, dtype=torch.float64, device=dev)
     bufs["sdf"] = torch.empty((B, N + 1, 4), dtype=torch.float32, device=dev)
     np_ = prob["p"].shape[-1]
+    # feedback-phase (QP) inputs/outputs: x0 near the first node, references, weights
+    from sdf_nmpc_amd.model import Quad
+    quad = Quad(cfg)
+    x0 = prob["x"][:, 0] + np.random.default_rng(2000 + rank).normal(0, 0.05, (B, 10))
+    for k, v in dict(x0=x0, yref=prob["yref"], W=prob["W"], yNref=prob["yN"], WN=prob["WN"]).items():
+        bufs[k] = torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+    for k, sh in dict(dx=(B, N + 1, 10), du=(B, N, 4), res=(B, 2)).items():
+        bufs[k] = torch.empty(sh, dtype=torch.float64, device=dev)
+    bufs["status"] = torch.empty(B, dtype=torch.int32, device=dev)
+    bufs["iters"] = torch.empty(B, dtype=torch.int32, device=dev)
+    u0 = torch.empty((B, 4), dtype=torch.float64, device=dev)
+    qopts = _lib.qp_opts(quad)
 
     def step():
         _lib.linearize(ctx, net, model, B, N, np_, bufs)
+
+    def rti_step():  # one SQP-RTI solve: preparation, feedback (QP), iterate update + u_0
+        _lib.linearize(ctx, net, model, B, N, np_, bufs)
+        _lib.qp_solve(ctx, qopts, B, N, bufs)
+        _lib.rti_apply(ctx, B, N, bufs["x"], bufs["u"], bufs["dx"], bufs["du"], u0)
 
     def barrier():
         if world > 1:
             dist.barrier()
 
+    def timed(fn, k):
+        torch.cuda.synchronize(dev)
+        barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
     for _ in range(args.warmup):
         step()
-    torch.cuda.synchronize(dev)
-    barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(step, args.steps)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * B * args.steps / elapsed
 
@@ -145,6 +169,26 @@ def main():
     achieved = sdf_flop / (kms["sdf_mlp"] * 1e-3) / 1e12
     lin_b = B * lin_bytes_per_instance(N)
     lin_gbs = lin_b / (kms["linearize"] * 1e-3) / 1e9
+
+    # full SQP-RTI iteration (preparation + QP + update); the iterate evolves step to step
+    full = None
+    if args.rti_steps > 0:
+        for _ in range(2):
+            rti_step()
+        rel = timed(rti_step, args.rti_steps)
+        ctx.enable_timing(True)
+        ctx.reset_stats()
+        rti_step()
+        qst = ctx.kernel_stats("rti_qp")
+        ctx.enable_timing(False)
+        it = bufs["iters"].cpu().numpy()
+        st = bufs["status"].cpu().numpy()
+        full = {"value": world * B * args.rti_steps / rel, "unit": "instance-RTI-solves/s (prep + QP + update)",
+                "ms_per_step": rel / args.rti_steps * 1e3, "steps": args.rti_steps,
+                "qp_kernel_ms": qst[0] / qst[1] if qst[1] else None,
+                "qp_iters_mean": float(it.mean()), "qp_iters_max": int(it.max()),
+                "qp_converged_frac": float((st == 0).mean()),
+                "qp": "batched Riccati IPM, one wavefront per instance (rti_qp.hip); tol 1e-8, max_iter 100"}
 
     # traffic from the committed PMC profile of this same command (profiles/)
     traffic = None
@@ -198,7 +242,7 @@ def main():
         "data": "synthetic (seeded x0/latent/waypoints, SIREN-init weights seed 0; real weights are LFS pointers)",
         "config": {"workload": f"C3/C4: batch={B} instances per GPU x N={N}, RTI preparation phase "
                                "(SDF fwd+d/dpos, ERK4+sens, NLS, h+J_h), 'att' model, default flags",
-                   "phase": "preparation (acados rti_phase=1 semantics; QP feedback not in this step)",
+                   "phase": "preparation (acados rti_phase=1 semantics); full RTI with the QP in full_rti",
                    "global_batch": world * B, "horizon": N, "parallelism": f"instances sharded over {world} GPU(s)",
                    "tile_rows": args.tile_rows},
         "p50_step_ms": p50,
@@ -209,6 +253,7 @@ def main():
         "roofline_linearize": {"bound": "hbm", "achieved": lin_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": lin_gbs / HBM_PEAK_GBS, "bytes_per_launch": lin_b},
         "cpu_baseline": cpu,
+        "full_rti": full,
     }
     if rank == 0:
         print(json.dumps(out))
