@@ -113,6 +113,13 @@ def load():
     return lib
 
 
+def l4c_path() -> str:
+    """Path of the CasADi external-function shim (include/sdf_l4c.h); raises if it has not been built."""
+    if not os.path.exists(L4C_PATH):
+        raise SdfnmpcError(f"{L4C_PATH} not built")
+    return L4C_PATH
+
+
 def _check(rc):
     if rc != 0:
         raise SdfnmpcError(f"sdfnmpc error {rc}: {load().sdfnmpc_last_error().decode()}")

@@ -1,0 +1,161 @@
+"""Batched GPU counterpart of the reference controller (sdf_nmpc/controller.py:Nmpc).
+
+Same methods, argument meaning and array layouts as the reference; every per-instance array gains
+an optional leading batch dimension (``batch`` instances solved together, one SQP-RTI iteration per
+``solve``).  With ``batch=1`` the shapes are exactly the reference's.
+
+  reset()                              controller.py:35    p, y, yN, W, WN zeroed, flag off, latent reset
+  set_sdf_flag(flag)                   controller.py:47
+  set_latent(latent, W_p_Bo, W_R_Bo)   controller.py:52    W_p_Co, W_R_Co (row-major 3x3), latent in p
+  reset_latent()                       controller.py:59
+  set_x0(x0)                           controller.py:67    first call initialises the OCP
+  solve()                              controller.py:74    shift + one RTI iteration; returns fail_count
+  get_matrices(), get_u(), get_cmd_acc(), get_cmd_TRPYr(), get_openloop_traj(), eval(k), set_ref(ref, k)
+
+``get_cmd_props`` exists in the reference only for the 'props' model; this build is the 'att' model
+(model.Quad), where the reference raises AttributeError too.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .model import Quad
+
+
+class Nmpc:
+    """Wrapper around the NMPC controller with range image-based collision prediction (batched)."""
+
+    def __init__(self, cfg, rebuild=False, batch: int = 1, device: int = 0, weights=None, ocp=None):
+        from .ocp import Ocp
+
+        self.cfg = cfg
+        self.model = Quad(cfg)
+        self.T = cfg.mpc.T
+        self.N = int(cfg.mpc.N)
+        self.B = int(batch)
+        self.ocp = ocp if ocp is not None else Ocp(self.model, build=rebuild, batch=batch, device=device,
+                                                  weights=weights)
+        lim = cfg.robot.limits
+        self.cmd_acc_hover = np.array([0, 0, 0, 0])
+        self.cmd_acc_min = [-lim.ax, -lim.ay, -lim.az, -lim.wz]
+        self.cmd_acc_max = [lim.ax, lim.ay, lim.az, lim.wz]
+        self.cmd_TRPYr_hover = np.array([cfg.robot.mass * self.model.g, 0, 0, 0])
+        self.cmd_TRPYr_min = [0, -lim.roll, -lim.pitch, -lim.wz]
+        self.cmd_TRPYr_max = [lim.gamma, lim.roll, lim.pitch, lim.wz]
+        self.reset()
+
+    # ---- state of the controller (host arrays, batch-leading; B == 1 keeps the reference's shapes)
+    def _shape(self, *s):
+        return s if self.B == 1 else (self.B,) + s
+
+    def reset(self):
+        """Reset internal matrices to default values (controller.py:35-44)."""
+        m = self.model
+        self.x0 = None
+        self.p = np.zeros(self._shape(self.N + 1, m.np))
+        self.y = np.zeros(self._shape(self.N, m.ny))
+        self.yN = np.zeros(self._shape(m.nyN))
+        self.W = np.zeros(self._shape(self.N, m.ny))
+        self.WN = np.zeros(self._shape(m.nyN))
+        self.fail_count = 0
+        self.set_sdf_flag(False)
+        self.reset_latent()
+
+    # ---- parameter setters
+    def set_sdf_flag(self, flag):
+        """Enable/disable the sdf constraint (controller.py:47-49); flag: scalar or [B]."""
+        f = np.asarray(flag, dtype=float)
+        self.p[..., self.cfg.mpc.p_idx.flag] = f[..., None] if f.ndim else f
+
+    def set_latent(self, latent, W_p_Bo, W_R_Bo):
+        """Latent and camera pose at the time of the image (controller.py:52-56), batched over a leading dim."""
+        idx = self.cfg.mpc.p_idx
+        W_R_Bo = np.asarray(W_R_Bo, dtype=float)
+        W_p_Co = W_R_Bo @ np.asarray(self.cfg.sensor.B_p_C, dtype=float).ravel() + W_p_Bo
+        W_R_Co = (W_R_Bo @ np.asarray(self.cfg.sensor.B_R_C, dtype=float)).reshape(W_R_Bo.shape[:-2] + (9,))
+        self.p[..., idx.W_p_Co] = np.asarray(W_p_Co)[..., None, :]
+        self.p[..., idx.W_R_Co] = W_R_Co[..., None, :]
+        self.p[..., idx.latent:] = np.asarray(latent, dtype=float)[..., None, :]
+
+    def reset_latent(self):
+        """controller.py:59-63."""
+        idx = self.cfg.mpc.p_idx
+        self.p[..., idx.W_p_Co] = 0
+        self.p[..., idx.W_R_Co] = 0
+        self.p[..., idx.latent:] = 0
+
+    # ---- control iteration
+    def set_x0(self, x0):
+        """Current state feedback (controller.py:67-71); the first call initialises the OCP iterate."""
+        x0 = np.asarray(x0, dtype=float)[..., : self.model.nx]
+        if self.x0 is None:
+            self.ocp.init(x0)
+        self.x0 = x0
+
+    def solve(self):
+        """One SQP-RTI iteration for every instance (controller.py:74-83)."""
+        try:
+            self.ocp.shift(self.cfg.mpc.shift)
+            self.ocp.solve(self.x0, self.y, self.yN, self.W, self.WN, self.p)
+            self.fail_count = 0
+        except Exception as e:  # same contract as the reference: report, count, keep running
+            print("solver failed:", e)
+            self.fail_count += 1
+        return self.fail_count
+
+    # ---- getters
+    def get_matrices(self):
+        """x [.., N+1, nx], u [.., N, nu] of the current iterate (controller.py:87-96)."""
+        x = self.ocp.bufs["x"].cpu().numpy()
+        u = self.ocp.bufs["u"].cpu().numpy()
+        return (x[0], u[0]) if self.B == 1 else (x, u)
+
+    def get_u(self):
+        """Last computed MPC inputs (controller.py:99-101)."""
+        return self.ocp.get_u()
+
+    def get_cmd_acc(self):
+        """controller.py:104-106."""
+        return np.clip(self.model.u_to_acc(self.x0, self.get_u()), self.cmd_acc_min, self.cmd_acc_max)
+
+    def get_cmd_TRPYr(self):
+        """controller.py:109-111."""
+        return np.clip(self.model.u_to_TRPYr(self.x0, self.get_u()), self.cmd_TRPYr_min, self.cmd_TRPYr_max)
+
+    def get_openloop_traj(self):
+        """Predicted (position, quaternion) path, node 0 = x0 (controller.py:119-125); batched: per instance."""
+        x, _ = self.get_matrices()
+        x = x if self.B > 1 else x[None]
+        x0 = self.x0 if self.B > 1 else self.x0[None]
+        paths = []
+        for b in range(x.shape[0]):
+            path = [(x0[b][[0, 1, 2]], x0[b][[3, 4, 5, 6]])]
+            for k in range(1, self.N + 1):
+                path.append((x[b, k][[0, 1, 2]], x[b, k][[3, 4, 5, 6]]))
+            paths.append(path)
+        return paths[0] if self.B == 1 else paths
+
+    def eval(self, k):
+        """The model's evaluation vector at node k: the SDF value with flag = 1 (gen_model.py:64,
+        controller.py:128-133), at the current iterate, computed by the HIP SDF kernel."""
+        idx = self.cfg.mpc.p_idx
+        x = self.ocp.bufs["x"][:, k].cpu().numpy()
+        p = self.p if self.B > 1 else self.p[None]
+        pk = p[:, k]
+        W_R_Co = pk[:, idx.W_R_Co].reshape(-1, 3, 3)
+        Co_p_B = np.einsum("bji,bj->bi", W_R_Co, x[:, :3] - pk[:, idx.W_p_Co])
+        df, _ = self.ocp.net.eval_host(np.concatenate([Co_p_B, pk[:, idx.latent:]], axis=1), want_grad=False)
+        return df[:1] if self.B == 1 else df[:, None]
+
+    def set_ref(self, ref, k, b=None):
+        """y, W and q_d of node k from a reference object (controller.py:136-142); b selects one instance
+        of a batch (None: all)."""
+        sel = () if self.B == 1 else (slice(None),) if b is None else (b,)
+        self.p[sel + (k, self.cfg.mpc.p_idx.q_d)] = ref.q
+        y, W = self.model.formate_ref(ref)
+        if k < self.N:
+            self.y[sel + (k,)] = y
+            self.W[sel + (k,)] = W
+        else:
+            self.WN[sel] = W[: self.model.nyN]
+            self.yN[sel] = y[: self.model.nyN]

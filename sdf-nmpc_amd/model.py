@@ -18,6 +18,25 @@ class UnsupportedConfig(ValueError):
     pass
 
 
+def quat2rot(q):
+    """[qw qx qy qz] -> rotation matrix, batched over leading dims (reference utils/math.py:7-23)."""
+    q = np.asarray(q, dtype=float)
+    w, x, y, z = q[..., 0], q[..., 1], q[..., 2], q[..., 3]
+    R = np.stack([w * w + x * x - y * y - z * z, 2 * (x * y - w * z), 2 * (x * z + w * y),
+                  2 * (x * y + w * z), w * w - x * x + y * y - z * z, 2 * (y * z - w * x),
+                  2 * (x * z - w * y), 2 * (y * z + w * x), w * w - x * x - y * y + z * z], axis=-1)
+    return R.reshape(q.shape[:-1] + (3, 3))
+
+
+def euler2rot_b(roll, pitch, yaw):
+    """Z1Y2X3 euler angles -> rotation matrix, batched (reference utils/math.py:26-54)."""
+    sr, cr, sp, cp, sy, cy = np.sin(roll), np.cos(roll), np.sin(pitch), np.cos(pitch), np.sin(yaw), np.cos(yaw)
+    R = np.stack([cp * cy, sr * sp * cy - cr * sy, cr * sp * cy + sr * sy,
+                  cp * sy, sr * sp * sy + cr * cy, cr * sp * sy - sr * cy,
+                  -sp, sr * cp, cr * cp], axis=-1)
+    return R.reshape(np.shape(roll) + (3, 3))
+
+
 class Quad:
     """'att' model + the SDF/FOV constraint set of gen_model.get_model_from_cfg (default flags)."""
 
@@ -57,6 +76,30 @@ class Quad:
         self.zl = np.array([sf[0], sf[0], sd[0]], dtype=float)
         self.Zl = np.array([sf[1], sf[1], sd[1]], dtype=float)
         self.extra_W = np.array([])
+
+    # ---- input -> command maps (quad_rollpitchyawrate.py:37-45): batched over leading dims of x, u
+    def _att(self, u):
+        lim = self.cfg.robot.limits
+        u = np.asarray(u, dtype=float)
+        return u[..., 0] * lim.gamma, u[..., 1] * lim.roll, u[..., 2] * lim.pitch, u[..., 3] * lim.wz
+
+    def u_to_TRPYr(self, x, u, p=None):
+        """[thrust, roll, pitch, yaw rate] (quad_rollpitchyawrate.py:45)."""
+        gamma, roll, pitch, wz = self._att(u)
+        return np.stack([gamma * self.cfg.robot.mass, roll, pitch, wz], axis=-1)
+
+    def u_to_acc(self, x, u, p=None):
+        """[W_R_B^T W_a, wz] (quad_rollpitchyawrate.py:44): body-frame acceleration and yaw rate."""
+        x = np.asarray(x, dtype=float)
+        gamma, roll, pitch, wz = self._att(u)
+        q = x[..., 3:7] / np.linalg.norm(x[..., 3:7], axis=-1, keepdims=True)
+        th = np.arctan2(q[..., 3], q[..., 0])
+        W_R_V = quat2rot(np.stack([np.cos(th), 0 * th, 0 * th, np.sin(th)], axis=-1))
+        V_R_B = euler2rot_b(roll, pitch, 0 * roll)
+        W_R_B = W_R_V @ V_R_B
+        W_a = W_R_B[..., :, 2] * gamma[..., None] - np.array([0.0, 0.0, self.g])
+        acc = np.einsum("...ji,...j->...i", W_R_B, W_a)
+        return np.concatenate([acc, wz[..., None]], axis=-1)
 
     def formate_ref(self, ref):
         """(y_ref, W) in the residual layout y = [p, q_e[3], v, roll, pitch, wz, W_a[2]]."""

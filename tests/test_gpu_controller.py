@@ -1,0 +1,109 @@
+"""The controller mirror end to end on the GPU: Nmpc.set_x0 / set_latent / set_ref / solve (one
+SQP-RTI iteration per instance) against the CPU pipeline oracle.linearize_batch + qp_oracle
+(dense Mehrotra IPM) from the same iterate; Ocp.init / shift semantics (ocp.py:148-160)."""
+import numpy as np
+import pytest
+
+from sdf_nmpc_amd import weights as W
+from sdf_nmpc_amd.config import Config
+from sdf_nmpc_amd.controller import Nmpc
+from sdf_nmpc_amd.reference import Ref, yaw2quat
+
+pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("ignore:no SDF weights")]
+
+U0_ATOL = 2e-5   # fp32 SDF rows differ from the oracle's by ~1e-7 rel; the QP solutions agree to ~1e-6
+
+
+def scenario(n, rng):
+    """Random but feasible-looking control problems through the reference API."""
+    B, N = max(n.B, 1), n.N
+    x0 = np.zeros((B, 10))
+    x0[:, :3] = rng.uniform(-1, 1, (B, 3))
+    x0[:, 3:7] = np.stack([yaw2quat(y) for y in rng.uniform(-np.pi, np.pi, B)])
+    x0[:, 7:] = rng.normal(0, 0.3, (B, 3))
+    lat = rng.normal(0, 1, (B, 128))
+    pos = x0[:, :3] + rng.normal(0, 0.2, (B, 3))
+    R = np.stack([np.eye(3)] * B)
+    goal = x0[:, :3] + rng.uniform(-3, 3, (B, 3))
+    sq = (lambda a: a[0]) if n.B == 1 else (lambda a: a)
+    n.set_sdf_flag(1.0)
+    n.set_latent(sq(lat), sq(pos), sq(R))
+    for b in range(B):
+        for k in range(N + 1):
+            r = Ref(n.cfg)
+            r.p, r.q = goal[b], yaw2quat(0.3 * b)
+            r.use_weights(r.W_on)
+            n.set_ref(r, k, b=None if n.B == 1 else b)
+    return sq(x0)
+
+
+def oracle_u0(n, x0, oracle_lib):
+    import qp_oracle
+    O = oracle_lib
+    B, N = max(n.B, 1), n.N
+    x0 = np.atleast_2d(x0)
+    xbar = np.repeat(x0[:, None], N + 1, axis=1)
+    ubar = np.broadcast_to(n.model.u_hover, (B, N, 4)).copy()
+    p = n.p if n.B > 1 else n.p[None]
+    y, Wt, yN, WN = (a if n.B > 1 else a[None] for a in (n.y, n.W, n.yN, n.WN))
+    onet = O.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed=0))
+    lin = O.linearize_batch(O.quad_model(n.cfg), onet, xbar, ubar, p, n.ocp.dt)
+    u0 = []
+    for b in range(B):
+        q = qp_oracle.stage_qp({k: v[b] for k, v in lin.items() if k != "sdf"}, xbar[b], ubar[b], x0[b], y[b], Wt[b],
+                               yN[b], WN[b], n.ocp.dt, n.model, float(n.cfg.mpc.lm_reg))
+        u0.append(ubar[b, 0] + qp_oracle.solve_dense(q)["du"][0])
+    return np.array(u0)
+
+
+@pytest.mark.parametrize("B", [1, 3])
+def test_nmpc_rti_step_matches_oracle(oracle_lib, B):
+    n = Nmpc(Config(), batch=B)
+    x0 = scenario(n, np.random.default_rng(10 + B))
+    n.set_x0(x0)
+    assert n.solve() == 0
+    assert (n.ocp.status == 0).all()
+    u = np.atleast_2d(n.get_u())
+    np.testing.assert_allclose(u, oracle_u0(n, x0, oracle_lib), rtol=0, atol=U0_ATOL)
+    assert (u >= n.model.lbu - 1e-9).all() and (u <= n.model.ubu + 1e-9).all()
+    x, uu = n.get_matrices()
+    np.testing.assert_array_equal(np.atleast_2d(u), np.atleast_2d(uu[..., 0, :]))
+    np.testing.assert_allclose(x[..., 0, :], x0, atol=1e-12)
+    assert np.atleast_1d(n.eval(3)).shape == ((1,) if B == 1 else (B, 1))
+    n.ocp.close()
+
+
+def test_batch_equals_single_instances():
+    rng = np.random.default_rng(5)
+    nb = Nmpc(Config(), batch=3)
+    x0 = scenario(nb, rng)
+    nb.set_x0(x0)
+    nb.solve()
+    ub = nb.get_u()
+    for b in range(3):
+        n1 = Nmpc(Config(), batch=1)
+        n1.p, n1.y, n1.W, n1.yN, n1.WN = (a[b].copy() for a in (nb.p, nb.y, nb.W, nb.yN, nb.WN))
+        n1.set_x0(x0[b])
+        n1.solve()
+        np.testing.assert_allclose(n1.get_u(), ub[b], rtol=0, atol=1e-12)
+        n1.ocp.close()
+    nb.ocp.close()
+
+
+def test_ocp_init_and_shift():
+    import torch
+    n = Nmpc(Config(mpc__shift=2), batch=2)
+    x0 = np.arange(20.0).reshape(2, 10)
+    n.set_x0(x0)
+    o = n.ocp
+    np.testing.assert_array_equal(o.bufs["x"].cpu().numpy(), np.repeat(x0[:, None], n.N + 1, 1))
+    np.testing.assert_array_equal(o.bufs["u"].cpu().numpy(), np.broadcast_to(n.model.u_hover, (2, n.N, 4)))
+    xs = torch.randn_like(o.bufs["x"])
+    us = torch.randn_like(o.bufs["u"])
+    o.bufs["x"].copy_(xs)
+    o.bufs["u"].copy_(us)
+    o.shift(2)
+    X, U, x_, u_ = o.bufs["x"].cpu(), o.bufs["u"].cpu(), xs.cpu(), us.cpu()
+    assert torch.equal(X[:, : n.N - 2], x_[:, 2: n.N]) and torch.equal(X[:, n.N - 2:], x_[:, n.N - 2:])
+    assert torch.equal(U[:, : n.N - 2], u_[:, 2:]) and torch.equal(U[:, n.N - 2:], u_[:, n.N - 2:])
+    o.close()
