@@ -44,7 +44,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU")
+    ap.add_argument("--batch", type=int, default=1024, help="instances per GPU (weak scaling)")
+    ap.add_argument("--global-batch", type=int, default=0,
+                    help="if > 0: this many instances in total, split by shard.instance_range (strong scaling)")
     ap.add_argument("--horizon", type=int, default=40)
     ap.add_argument("--tile-rows", type=int, default=32)
     ap.add_argument("--cpu-sample", type=int, default=64, help="instances in the CPU-baseline sample")
@@ -68,24 +70,23 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import sdf_nmpc_amd  # noqa: F401
-    from sdf_nmpc_amd import _lib, synth, weights as W
+    from sdf_nmpc_amd import _lib, shard, synth, weights as W
     from sdf_nmpc_amd.config import Config
 
     cfg = Config()
-    B, N = args.batch, args.horizon
+    N = args.horizon
+    if args.global_batch > 0:
+        lo, hi = shard.instance_range(args.global_batch, world, rank)
+        B = hi - lo
+    else:
+        B = args.batch
     stream = torch.cuda.current_stream(dev).cuda_stream
     ctx = _lib.Context(local, stream=stream, tile_rows=args.tile_rows)
 
     # weights: rank 0 packs the SIREN-init network; RCCL broadcasts the blob (init-time collective)
     blob = W.pack(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed=0)) if rank == 0 else None
     if world > 1:
-        n = torch.tensor([len(blob) if rank == 0 else 0], device=dev, dtype=torch.int64)
-        dist.broadcast(n, 0)
-        buf = torch.empty(int(n.item()), dtype=torch.uint8, device=dev)
-        if rank == 0:
-            buf.copy_(torch.frombuffer(bytearray(blob), dtype=torch.uint8))
-        dist.broadcast(buf, 0)
-        blob = bytes(buf.cpu().numpy().tobytes())
+        blob = shard.broadcast_blob(blob, dev)
     net = _lib.Net.from_blob(ctx, blob)
     model = _lib.quad_model(cfg)
 
@@ -134,17 +135,14 @@ def main():
         torch.cuda.synchronize(dev)
         barrier()
         el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el], device=dev, dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
+        return shard.max_over_ranks(el, dev) if world > 1 else el
 
     for _ in range(args.warmup):
         step()
     elapsed = timed(step, args.steps)
     ms_per_step = elapsed / args.steps * 1e3
-    value = world * B * args.steps / elapsed
+    total = args.global_batch if args.global_batch > 0 else world * B
+    value = total * args.steps / elapsed
 
     # per-step latency distribution (each step synchronised on its own) and B=1 latency (config C2)
     lat = []
@@ -183,7 +181,7 @@ def main():
         ctx.enable_timing(False)
         it = bufs["iters"].cpu().numpy()
         st = bufs["status"].cpu().numpy()
-        full = {"value": world * B * args.rti_steps / rel, "unit": "instance-RTI-solves/s (prep + QP + update)",
+        full = {"value": total * args.rti_steps / rel, "unit": "instance-RTI-solves/s (prep + QP + update)",
                 "ms_per_step": rel / args.rti_steps * 1e3, "steps": args.rti_steps,
                 "qp_kernel_ms": qst[0] / qst[1] if qst[1] else None,
                 "qp_iters_mean": float(it.mean()), "qp_iters_max": int(it.max()),
@@ -236,14 +234,14 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.global_batch > 0 else "weak",
         "vs_baseline": None,
         "dtype": "f32 (SDF MLP, MFMA) + f64 (linearisation)",
         "data": "synthetic (seeded x0/latent/waypoints, SIREN-init weights seed 0; real weights are LFS pointers)",
         "config": {"workload": f"C3/C4: batch={B} instances per GPU x N={N}, RTI preparation phase "
                                "(SDF fwd+d/dpos, ERK4+sens, NLS, h+J_h), 'att' model, default flags",
                    "phase": "preparation (acados rti_phase=1 semantics); full RTI with the QP in full_rti",
-                   "global_batch": world * B, "horizon": N, "parallelism": f"instances sharded over {world} GPU(s)",
+                   "global_batch": total, "horizon": N, "parallelism": f"instances sharded over {world} GPU(s)",
                    "tile_rows": args.tile_rows},
         "p50_step_ms": p50,
         "kernel_ms": kms,
