@@ -37,7 +37,7 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
            + 2 * N1 * 10            // dx, dxc
            + 3 * (size_t)N * 4      // du, dua, duc
            + 2 * N1 * 3             // cxa, cxc
-           + QP_REC + 192           // committed stage record / factor-record window
+           + 320 + 192              // committed stage-record / factor-record windows
            + QP_RING * 154          // [A~|b~ K|k_ff] of nodes 0..RING-1 (written late in a backward sweep)
            + 16                     // corrector p
            + 4 * (size_t)N + 4 * N1 // u, (h, s_k)

@@ -90,7 +90,8 @@ struct Smem {
     ldsd *dx, *dxc;                // iterate dx; sweep solution (x of predictor, then corrector)
     ldsd *du, *dua, *duc;          // iterate du; affine / corrector du
     ldsd *cxa, *cxc;               // C dx of the affine / corrector solution
-    ldsd *rec, *frc, *fsave;       // committed stage record / factor-record window; [A~|b~ K|k_ff] of nodes < PD
+    ldsd *recw, *rec, *frc, *fsave; // committed stage-record window, its record base (recw - r0), factor-record
+                                   // window; [A~|b~ K|k_ff] of nodes < PD
     ldsd* p;                       // corrector Riccati vector p (the factor sweep keeps p in registers)
     ldsd *uu, *hv, *skv;           // u (box constants), h, cost scaling per node
     ldsd *fw, *fg, *bd, *bv;       // soft folds [N+1][3] (w, gamma), box terms [N][4] (diag, v)
@@ -106,7 +107,7 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubl
     s.dx = take(N1 * NX); s.dxc = take(N1 * NX);
     s.du = take(N * NU); s.dua = take(N * NU); s.duc = take(N * NU);
     s.cxa = take(N1 * NS); s.cxc = take(N1 * NS);
-    s.rec = take(REC); s.frc = take(FW * 64); s.fsave = take(PD * F_FW);
+    s.recw = take(RW * 64); s.rec = s.recw; s.frc = take(FW * 64); s.fsave = take(PD * F_FW);
     s.p = take(16);
     s.uu = take(N * NU); s.hv = take(N1 * NS); s.skv = take(N1);
     s.fw = take(N1 * NS); s.fg = take(N1 * NS); s.bd = take(N * NU); s.bv = take(N * NU);
@@ -183,9 +184,9 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
 }
 
 #ifdef QP_STAMPS  // diagnostic build only: per-phase cycle accounting (never in the product build)
-#define STAMP_DECL long long st_t0 = clock64(), st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define STAMP_DECL long long st_t0 = clock64(), st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define STAMP(i) do { const long long t1_ = clock64(); st_acc[i] += t1_ - st_t0; st_t0 = t1_; } while (0)
-#define STAMP_OUT if (lane == 0 && A.stamps) for (int i_ = 0; i_ < 12; ++i_) A.stamps[(size_t)b * 12 + i_] = (double)st_acc[i_];
+#define STAMP_OUT if (lane == 0 && A.stamps) for (int i_ = 0; i_ < 16; ++i_) A.stamps[(size_t)b * 16 + i_] = (double)st_acc[i_];
 #else
 #define STAMP_DECL
 #define STAMP(i)
@@ -233,13 +234,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             fd[i] = fsrc[e < FREC ? e : FREC - 1];
         }
     };
-    auto commit_from = [&](const double* rd, const double* fd, int t) {
-        const int r0 = win_r(t);
+    // the committed window lands at s.recw[0, RW*64) unconditionally; stage code addresses the record
+    // through s.rec = s.recw - r0 (set per sweep), so no lane-dependent write predicate is needed
+    auto commit_from = [&](const double* rd, const double* fd) {
 #pragma unroll
-        for (int i = 0; i < RW; ++i) {
-            const int e = r0 + lane + 64 * i;
-            if (e < REC) s.rec[e] = rd[i];
-        }
+        for (int i = 0; i < RW; ++i) s.recw[lane + 64 * i] = rd[i];
 #pragma unroll
         for (int i = 0; i < FW; ++i) s.frc[lane + 64 * i] = fd[i];
     };
@@ -302,6 +301,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
                   : (k < N && lane < NX) ? dxo + (k + 1) * NX + lane
                   : (mode && k < N && lane >= NX && lane < 14) ? duo + k * NU + lane - NX : ljunk;
         *dst = v;
+        STAMP(14);
     };
 
     // ------------------------------------------------------------ initial iterate (dynamics-feasible):
@@ -467,6 +467,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const bool c14 = lc == 14;
 #pragma unroll
         for (int r = 0; r < 4; ++r) W[r] += c14 ? Pa[r] : 0.0;
+        STAMP(9);
         // ---- M' = G_ab^T W + [H | g] + fold + box terms (identity rows 10..13 times [diag | v])
         d4 M;
 #pragma unroll
@@ -479,6 +480,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         M = mfma(cg, fb, M);
 #pragma unroll
         for (int st = 0; st < 3; ++st) M = mfma(lc < 14 ? og[st] : 0.0, W[st], M);
+        STAMP(10);
         // ---- rows 10..13 of M' ([S | R^ | m_u]) of column lc into every lane of that column
         const double s0 = __shfl(M[2], 32 + lc), s1 = __shfl(M[2], 48 + lc);
         const double s2 = __shfl(M[3], lc), s3 = __shfl(M[3], 16 + lc);
@@ -504,6 +506,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double k0 = (-y0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
         const double yg = lg == 0 ? y0 : lg == 1 ? y1 : lg == 2 ? y2 : y3;
         const double kg = lg == 0 ? k0 : lg == 1 ? k1 : lg == 2 ? k2 : k3;
+        STAMP(11);
         // ---- [P | p] <- M' - Y^T [Y | w];  [A~ | b~] = [A | c] + B [K | k_ff]
         Pa = mfma(-yg, yg, M);
         d4 Ab;
@@ -514,6 +517,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
         const double bm = rk[bmi];
         Ab = mfma(lc < NX ? bm : 0.0, kg, Ab);
+        STAMP(12);
         // ---- factor record (and its LDS copy for the first forward stages)
         const double lv = lane == 0 ? i0 : lane == 1 ? l10 : lane == 2 ? i1 : lane == 3 ? l20 : lane == 4 ? l21
                         : lane == 5 ? i2 : lane == 6 ? l30 : lane == 7 ? l31 : lane == 8 ? l32 : i3;
@@ -527,6 +531,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             for (int r = 0; r < 3; ++r) *fs_at(k, sab[r]) = Ab[r];
             *fs_at(k, sk_) = kg;
         }
+        STAMP(13);
     };
 
     // ------------------------------------------------------------ backward sweep, corrector (1 barrier / stage)
@@ -571,6 +576,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         *bc_p = pn;
         F[(size_t)k * FREC + bc_st] = fv;
         if (k < PD) *fs_at(k, bc_st) = fv;
+        STAMP(15);
     };
 
     // row values of a soft group (k, j) at an LQR solution with C dx = cxs, and its slacks
@@ -718,16 +724,18 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         __syncthreads();
         STAMP(4);
         const int mode = kind != 0;
+        s.rec = s.recw - win_r(kind);
         ldsd* dxo = kind == 0 ? s.dx : s.dxc;
         ldsd* duo = kind == 4 ? s.duc : s.dua;
         ldsd* cxo = kind == 4 ? s.cxc : s.cxa;
         // ---- the sweep: NP stream positions, PD per trip with static ring slots
         auto stage = [&](auto slot, int q) {
             constexpr int S = decltype(slot)::value;
-            commit_from(rr[S], fr[S], kind);
+            commit_from(rr[S], fr[S]);
             issue_to(rr[S], fr[S], pi);
             next(pi);
             __syncthreads();
+            STAMP(8);
             if (q < N1) {
                 if (kind == 1) bf_stage(q);
                 else if (kind == 3) bc_stage(q);

@@ -1,0 +1,44 @@
+"""profiles/pmc_summary.json from rocprofv3 FETCH_SIZE / WRITE_SIZE passes (csv output).
+
+FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (rocprofv3 derived metrics, TCC_EA0 requests).
+gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half of the bytes of 16-B-per-lane
+streaming reads -> doubled; WRITE_SIZE is exact for 16-B stores, uncalibrated for narrower ones.
+Usage: python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> B N tile_rows
+"""
+import collections
+import csv
+import json
+import os
+import sys
+
+
+def per_kernel(path, counter):
+    acc = collections.defaultdict(list)
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if row["Counter_Name"] == counter:
+                name = row["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0]
+                acc[name].append(float(row["Counter_Value"]) * 1024.0)
+    return {k: sum(v) / len(v) for k, v in acc.items()}
+
+
+def main():
+    fetch, write, B, N, tile = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4]), int(sys.argv[5])
+    fb, wb = per_kernel(fetch, "FETCH_SIZE"), per_kernel(write, "WRITE_SIZE")
+    out = {"B": B, "N": N, "tile_rows": tile, "source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE (separate passes)",
+           "correction": "fetch bytes = 2 x FETCH_SIZE (gfx950 16-B streaming reads); write bytes = WRITE_SIZE",
+           "kernels": {}}
+    for k in sorted(set(fb) | set(wb)):
+        f2 = 2.0 * fb.get(k, 0.0)
+        out["kernels"][k.split("::")[-1].replace("_kernel", "")] = {
+            "fetch_bytes_per_launch": f2, "write_bytes_per_launch": wb.get(k, 0.0),
+            "hbm_bytes_per_launch": f2 + wb.get(k, 0.0)}
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    with open(os.path.join(root, "profiles", "pmc_summary.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    for k, v in out["kernels"].items():
+        print(f"{k:28s} fetch {v['fetch_bytes_per_launch'] / 1e6:10.3f} MB  write {v['write_bytes_per_launch'] / 1e6:10.3f} MB")
+
+
+if __name__ == "__main__":
+    main()

@@ -16,14 +16,14 @@ int main(int argc, char** argv) {
   for(int i=0;i<4;++i){q.lbu[i]=opt[i];q.ubu[i]=opt[4+i];} for(int i=0;i<3;++i){q.lh[i]=opt[8+i];q.uh[i]=opt[11+i];q.zl[i]=opt[14+i];q.Zl[i]=opt[17+i];}
   q.lm=opt[20]; q.tol=opt[21]; q.max_iter=100; q.cost_scaling=1;
   hipMalloc(&q.dx,8*B*(N+1)*10); hipMalloc(&q.du,8*B*N*4); hipMalloc(&q.status,4*B); hipMalloc(&q.iters,4*B); hipMalloc(&q.res,16*B);
-  hipMalloc(&q.work,8*B*qp_work_doubles(N)); hipMalloc(&q.stamps,8*B*12);
+  hipMalloc(&q.work,8*B*qp_work_doubles(N)); hipMalloc(&q.stamps,8*B*16);
   for (int r=0;r<3;++r) launch_rti_qp(q,0);
   hipEvent_t a,b; hipEventCreate(&a); hipEventCreate(&b); hipEventRecord(a); launch_rti_qp(q,0); hipEventRecord(b); hipEventSynchronize(b);
   float ms; hipEventElapsedTime(&ms,a,b);
-  std::vector<double> st(B*12); hipMemcpy(st.data(),q.stamps,8*B*12,hipMemcpyDeviceToHost);
+  std::vector<double> st(B*16); hipMemcpy(st.data(),q.stamps,8*B*16,hipMemcpyDeviceToHost);
   std::vector<int> it(B); hipMemcpy(it.data(),q.iters,4*B,hipMemcpyDeviceToHost);
-  double tot[12]={0}; int mx=0; for(int i=0;i<B;++i){for(int j=0;j<12;++j) tot[j]+=st[i*12+j]; if(it[i]>mx)mx=it[i];}
-  const char* ph[]={"setup","init","bwd-factor","fwd(x2)","rows-pred","bwd-corr","rows-corr+upd","loop-top","-","-","-","-"};
-  printf("kernel %.3f ms, max iters %d\n", ms, mx); double s=0; for(int j=0;j<12;++j) s+=tot[j];
-  for(int j=0;j<10;++j) printf("  %-14s %8.0f cycles/instance (%.1f%%)\n", ph[j], tot[j]/B, 100*tot[j]/s);
+  double tot[16]={0}; int mx=0; for(int i=0;i<B;++i){for(int j=0;j<16;++j) tot[j]+=st[i*16+j]; if(it[i]>mx)mx=it[i];}
+  const char* ph[]={"setup","init","bwd-factor","fwd(x2)","rows-pred","bwd-corr","rows-corr+upd","loop-top","commit+issue+sync","bf:W","bf:M","bf:gather+chol+solves","bf:P,Ab mfma","bf:stores","fw:matvec+store","bc:all"};
+  printf("kernel %.3f ms, max iters %d\n", ms, mx); double s=0; for(int j=0;j<16;++j) s+=tot[j];
+  for(int j=0;j<16;++j) printf("  %-14s %8.0f cycles/instance (%.1f%%)\n", ph[j], tot[j]/B, 100*tot[j]/s);
   return 0; }
