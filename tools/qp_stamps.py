@@ -16,8 +16,9 @@ cfg = Config(); model = Quad(cfg)
 dev = torch.device("cuda:0")
 ctx = _lib.Context(0, stream=torch.cuda.current_stream().cuda_stream)
 net = _lib.Net.siren(ctx, 0)
-prob = synth.make_problem(cfg, B, N, seed=5)
-x0 = prob["x"][:, 0] + np.random.default_rng(1).normal(0, 0.05, (B, 10))
+SEED, NOISE = int(os.environ.get("SEED", 5)), float(os.environ.get("NOISE", 0.05))
+prob = synth.make_problem(cfg, B, N, seed=SEED)
+x0 = prob["x"][:, 0] + np.random.default_rng(SEED + 1).normal(0, NOISE, (B, 10))
 t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
      dict(x=prob["x"], u=prob["u"], p=prob["p"], dt=prob["dt"], x0=x0, yref=prob["yref"], W=prob["W"],
           yNref=prob["yN"], WN=prob["WN"]).items()}
