@@ -14,20 +14,26 @@
 //     node's state block; these folds and the box terms are formed for all nodes in one parallel
 //     pass before each sweep, so the serial sweeps hold no division
 //   * one factorisation per iteration serves predictor and corrector.  With G = [A B c] (10 x 15),
-//     the factor stage runs on f64 MFMA 16x16x4 tiles held in registers:
+//     the factor stage's critical chain runs on f64 MFMA 16x16x4 tiles held in registers:
 //         W  = P G                      (P c -> factor record; p added to column 14)
 //         M' = G_ab^T W + [H | g] + C^T diag(w) [C | gamma] + box terms       ([R^ S; S^T Q^ | m])
-//         L  = chol(R^), [Y | w] = L^-1 [S | m_u], [K | k_ff] = -L^-T [Y | w]
-//         [P | p] <- M' - Y^T [Y | w],  [A~ | b~] = [A | c] + B [K | k_ff]
+//         L  = chol(R^), Y = L^-1 S,  [P | p] <- M' - Y^T [Y | w]
 //     P is symmetric, so the accumulator of one stage is the A operand of the next with no lane
 //     movement (C/D lane (g, c) holds rows g + 4r of column c; A/B lane (g, c) holds k = 4s + g).
-//     The forward sweep is then one 17-row matvec per stage: [A~; K; C^T] x + [b~; k_ff; 0].
-// Memory: rti_qp_pack_kernel packs per-stage records [A B | c | g | C | H] into a global workspace
-// (a wide launch, one block per stage).  Each IPM iteration walks the records in a fixed order --
-// backward (factor), forward, backward (corrector), forward -- so they form one stream prefetched
-// QP_RING records ahead through registers, across sweep boundaries (each sweep loads a fixed window
-// of the stage record and of the factor record).  Iterate, duals and stage scratch live in LDS
-// (< 40 KB at N = 40: 4 instances per CU, one round for B = 1024).
+//     Off that chain, on the VALU: the fold and box terms, [K | k_ff] = -L^-T [Y | w] and the closed
+//     loop [A~ | b~] = [A | c] + B [K | k_ff].
+//   * forward sweep: one 17-row matvec per stage, [A~; K; C^T] x + [b~; k_ff; 0].
+//   * corrector backward sweep: the closed-loop recursion p_k = A~^T (P c + p_{k+1}) + g_x + K^T g_u
+//     (g with the corrector's fold / box terms); k_ff = -R^-1 (g_u + B^T (P c + p_{k+1})) and b~ hang
+//     off it.
+// Memory: rti_qp_pack_kernel packs per-stage records [A B | c | g | C^T | H | 0] into a global
+// workspace (a wide launch, one block per stage).  Each IPM iteration walks the records in a fixed
+// order -- backward (factor), forward, backward (corrector), forward -- so they form one stream
+// prefetched QP_RING positions ahead through registers, across sweep boundaries.  Every sweep kind has
+// its own loop, its own window of the stage / factor records and straight-line stages whose lane
+// selections are precomputed LDS addresses (zero / junk slots for inactive lanes): no divergent branch
+// and no per-stage address arithmetic beyond a node offset.  Iterate, duals and stage scratch live in
+// LDS (< 40 KB at N = 40: 4 instances per CU, one round for B = 1024).
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
@@ -41,16 +47,33 @@ namespace {
 // LDS pointers must keep address space 3: a generic pointer compiles to flat_load/store, whose waits
 // (vmcnt(0) AND lgkmcnt(0)) drain every global prefetch in flight at each LDS access.
 typedef __attribute__((address_space(3))) double ldsd;
+typedef double d2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) d2 ldsd2;
 typedef double d4 __attribute__((ext_vector_type(4)));
+template <int V>
+using IC = std::integral_constant<int, V>;
 
 constexpr int NX = 10, NU = 4, NS = 3;
-// stage record (doubles): [AB 140 (column j = d xn / d (x,u)_j) | c 10 | g 14 | C 30 | H 105 upper]
-constexpr int R_AB = 0, R_C = 140, R_G = 150, R_CH = 164, R_H = 194, REC = QP_REC;
-// factor record: [A~|b~ 10 x 11 | K|k_ff 4 x 11 | Y 4 x 10 | L 10 (lower packed, diagonal 1/L_ii) | P c 10 | 2 spare]
-constexpr int F_AB = 0, F_K = 110, F_Y = 154, F_L = 194, F_PC = 204, FREC = QP_FREC;
-constexpr int F_FW = 154;             // forward sweeps read [0, F_FW); the corrector reads [F_FW, FREC)
-constexpr int RW = 5, FW = 3;         // ring window per record: RW * 64 stage, FW * 64 factor doubles
-constexpr int PD = QP_RING;
+// stage record: [AB 140 (column j = d xn / d (x,u)_j) | c 10 | g 14 | C^T 30 (row j = d h_j / d x) | H 105 upper | 0]
+constexpr int R_AB = 0, R_C = 140, R_G = 150, R_CT = 164, R_H = 194, R_Z = 299, REC = QP_REC;
+// factor record: [A~|b~ 10 x 11 | K|k_ff 4 x 11 | Y 4 x 10 | L 10 (lower packed, diagonal 1/L_ii) | P c 10 | junk 2]
+constexpr int F_AB = 0, F_K = 110, F_Y = 154, F_L = 194, F_PC = 204, F_J = 214, FREC = QP_FREC;
+constexpr int F_FW = 154;  // forward sweeps read [0, F_FW)
+constexpr int SLOT = QP_SLOT, PD = QP_RING;
+// Window of one stream position per sweep kind: n_loads(K) loads of 64 consecutive doubles (lanes
+// clamped to the record), load j landing at window offset 64 j:
+//   0 initial forward     R[0, 256)                    AB, c, C^T in place
+//   1 backward factor     R[0, 320)                    the stage record in place (R_Z reads 0)
+//   2, 4 forward          F[0, 192) | R[164, 228)      factor rows at 0, C^T at WF_CT
+//   3 backward corrector  F[0, 256) | R[100, 228)      factor record at 0, R[i] at WB_R + i (i >= 100)
+constexpr int WF_CT = 192, WB_R = 256 - 100;
+__host__ __device__ constexpr int n_loads(int K) { return K == 1 ? 5 : K == 3 ? 6 : 4; }
+__host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K == 4) ? j < 3 : K == 3 ? j < 4 : false; }
+__host__ __device__ constexpr int load_at(int K, int j) {
+    return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 4 ? 64 * j : 100 + 64 * (j - 4));
+}
+static_assert(FREC == 216 && PD == 3 && SLOT == 6, "record layout");
+static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT, "window layout");
 // IPM starting point: t = max(row value, T0), lambda = L0.  The kernel waits for its slowest
 // instance, so these were chosen for the worst case over seeds / x0 spreads (profiles/r01/
 // qp_init_sweep.txt): (1, 3) converges every instance in <= 13 iterations where (1, 1) needs 16-17
@@ -62,7 +85,6 @@ constexpr int PD = QP_RING;
 #define QP_L0 3.0
 #endif
 constexpr double T0 = QP_T0, L0 = QP_L0;
-static_assert(FREC == 216 && PD == 3 && RW * 64 >= REC && FW * 64 >= F_FW, "record layout");
 
 __device__ __forceinline__ int tri10(int a, int c) { return a * 10 - a * (a - 1) / 2 + (c - a); }  // a <= c
 __device__ __forceinline__ int tri14(int a, int c) { return a * 14 - a * (a - 1) / 2 + (c - a); }  // a <= c
@@ -95,15 +117,24 @@ __device__ __forceinline__ double rsqrt_nr(double v) {
     const double h = 0.5 * v;
     return y * fma(-h * y, y, 1.5);
 }
+// The QP kernel runs one wavefront per workgroup, and a wave's LDS operations complete in issue
+// order: a stage hand-off only has to stop the compiler from moving LDS accesses across it (a
+// workgroup barrier would also drain lgkmcnt at every stage).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 struct Smem {
     ldsd *t, *lam;                 // [m] inequality slacks / duals
     ldsd *dx, *dxc;                // iterate dx; sweep solution (x of predictor, then corrector)
     ldsd *du, *dua, *duc;          // iterate du; affine / corrector du
     ldsd *cxa, *cxc;               // C dx of the affine / corrector solution
-    ldsd *recw, *rec, *frc, *fsave; // committed stage-record window, its record base (recw - r0), factor-record
-                                   // window; [A~|b~ K|k_ff] of nodes < PD
+    ldsd* win;                     // committed stream window
+    ldsd* fsave;                   // [A~|b~ K|k_ff] of nodes < PD
     ldsd* p;                       // corrector Riccati vector p (the factor sweep keeps p in registers)
+    ldsd *zero, *junk;             // two doubles that stay 0; two that absorb stores of inactive lanes
     ldsd *uu, *hv, *skv;           // u (box constants), h, cost scaling per node
     ldsd *fw, *fg, *bd, *bv;       // soft folds [N+1][3] (w, gamma), box terms [N][4] (diag, v)
     ldsd* cst;                     // lbu 4 | ubu 4 | lh 3 | uh 3 | zl 3 | Zl 3 (lane-indexed kernel arguments
@@ -112,14 +143,14 @@ struct Smem {
 
 __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubles()
     Smem s;
-    auto take = [&](int n) { ldsd* r = q; q += n; return r; };
+    auto take = [&](int n) { ldsd* r = q; q += (n + 1) & ~1; return r; };
     const int m = 8 * N + 12 * (N + 1), N1 = N + 1;
     s.t = take(m); s.lam = take(m);
     s.dx = take(N1 * NX); s.dxc = take(N1 * NX);
     s.du = take(N * NU); s.dua = take(N * NU); s.duc = take(N * NU);
     s.cxa = take(N1 * NS); s.cxc = take(N1 * NS);
-    s.recw = take(RW * 64); s.rec = s.recw; s.frc = take(FW * 64); s.fsave = take(PD * F_FW);
-    s.p = take(16);
+    s.win = take(SLOT * 64); s.fsave = take(PD * F_FW);
+    s.p = take(16); s.zero = take(4); s.junk = s.zero + 2;
     s.uu = take(N * NU); s.hv = take(N1 * NS); s.skv = take(N1);
     s.fw = take(N1 * NS); s.fg = take(N1 * NS); s.bd = take(N * NU); s.bv = take(N * NU);
     s.cst = take(20);
@@ -130,7 +161,7 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubl
 
 // ---------------------------------------------------------------------------------------------------
 // Stage records, one block per (instance, node): AB, c = xn_k - xbar_{k+1}, g = s_k J^T W r,
-// C = J_h, H = s_k J^T W J + lm I (upper); terminal: H_N = J_N^T W_N J_N + lm I (10x10 upper in the
+// C^T = J_h^T, H = s_k J^T W J + lm I (upper); terminal: H_N = J_N^T W_N J_N + lm I (10x10 upper in the
 // H field), g_N (first 10 of g), C_N.
 __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
     const int N = A.N, N1 = N + 1;
@@ -156,11 +187,12 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
                 v = AB[e];
             } else if (e < R_G) {
                 v = xn[e - R_C] - xb1[e - R_C];
-            } else if (e < R_CH) {
+            } else if (e < R_CT) {
                 const int a = e - R_G;
                 for (int i = 0; i < 11; ++i) v += Js[a * 11 + i] * Ws[i] * rs[i];
-            } else if (e < R_H) {
-                v = Jh[e - R_CH];
+            } else if (e < R_H) {  // C^T: row j = d h_j / d x
+                const int q = e - R_CT, j = q / 10;
+                v = Jh[(q - 10 * j) * 3 + j];
             } else if (e < R_H + 105) {
                 int q = e - R_H, a = 0;
                 while (q >= 14 - a) { q -= 14 - a; ++a; }
@@ -180,8 +212,9 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
             if (e >= R_G && e < R_G + 10) {
                 const int a = e - R_G;
                 for (int i = 0; i < 4; ++i) v += J[a * 4 + i] * Wn[i] * (yn[i] - rn[i]);
-            } else if (e >= R_CH && e < R_H) {
-                v = Jh[e - R_CH];
+            } else if (e >= R_CT && e < R_H) {
+                const int q = e - R_CT, j = q / 10;
+                v = Jh[(q - 10 * j) * 3 + j];
             } else if (e >= R_H && e < R_H + 55) {
                 int q = e - R_H, a = 0;
                 while (q >= 10 - a) { q -= 10 - a; ++a; }
@@ -207,56 +240,12 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
 __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     extern __shared__ __align__(16) double lds_q[];
     STAMP_DECL
-    const int b = blockIdx.x, lane = threadIdx.x, lg = lane >> 4, lc = lane & 15;
+    const int b = blockIdx.x, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
     const int N = A.N, N1 = N + 1, m = 8 * N + 12 * N1;
-    Smem s = carve((ldsd*)lds_q, N);
+    const Smem s = carve((ldsd*)lds_q, N);
+    ldsd* const win = s.win;
     const double* R = A.work + (size_t)b * qp_work_doubles(N);  // [N+1][REC] stage records
     double* F = A.work + (size_t)b * qp_work_doubles(N) + (size_t)N1 * REC;  // [N+1][FREC]
-
-    // ------------------------------------------------------------ record stream
-    // sweep types: 0 initial forward, then per IPM iteration 1 backward-factor, 2 forward,
-    // 3 backward-corrector, 4 forward.  Each sweep takes NP = N+1 rounded up to a multiple of PD
-    // stream positions (the tail positions load a clamped record and are skipped), so every sweep
-    // starts at ring slot 0 and the sweep loop, unrolled by PD, indexes the register ring
-    // statically: the compiler then waits only for the slot being committed (vmcnt of the two
-    // younger slots) instead of draining the stream.  Window per type: stage record from r0,
-    // factor record from f0; every issue is the same RW + FW unpredicated loads (clamped addresses).
-    const int NP = (N1 + PD - 1) / PD * PD;
-    struct Pos { int t, q; };
-    auto next = [&](Pos& p) {
-        if (++p.q == NP) { p.q = 0; p.t = p.t == 4 ? 1 : p.t + 1; }
-    };
-    auto win_r = [](int t) { return (t == 2 || t == 4) ? R_CH : 0; };
-    auto win_f = [](int t) { return t == 3 ? F_FW : 0; };
-    double rr[PD][RW], fr[PD][FW];
-    auto issue_to = [&](double* rd, double* fd, const Pos& p) {
-        const int qq = p.q < N ? p.q : N;
-        const int k = (p.t == 1 || p.t == 3) ? N - qq : qq, r0 = win_r(p.t), f0 = win_f(p.t);
-        const double* src = R + (size_t)k * REC;
-        const double* fsrc = F + (size_t)k * FREC;
-#pragma unroll
-        for (int i = 0; i < RW; ++i) {
-            const int e = r0 + lane + 64 * i;
-            rd[i] = src[e < REC ? e : REC - 1];
-        }
-#pragma unroll
-        for (int i = 0; i < FW; ++i) {
-            const int e = f0 + lane + 64 * i;
-            fd[i] = fsrc[e < FREC ? e : FREC - 1];
-        }
-    };
-    // the committed window lands at s.recw[0, RW*64) unconditionally; stage code addresses the record
-    // through s.rec = s.recw - r0 (set per sweep), so no lane-dependent write predicate is needed
-    auto commit_from = [&](const double* rd, const double* fd) {
-#pragma unroll
-        for (int i = 0; i < RW; ++i) s.recw[lane + 64 * i] = rd[i];
-#pragma unroll
-        for (int i = 0; i < FW; ++i) s.frc[lane + 64 * i] = fd[i];
-    };
-    Pos pi{0, 0};
-    issue_to(rr[0], fr[0], pi); next(pi);
-    issue_to(rr[1], fr[1], pi); next(pi);
-    issue_to(rr[2], fr[2], pi); next(pi);
 
     // ------------------------------------------------------------ per-node constants into LDS
     for (int e = lane; e < N * NU; e += 64) {
@@ -282,8 +271,36 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     }
     for (int e = lane; e < N1; e += 64) s.skv[e] = (A.cost_scaling && e < N) ? A.dt[e] : 1.0;
     if (lane < NX) s.dx[lane] = A.x0[(size_t)b * 10 + lane] - A.x[(size_t)b * N1 * 10 + lane];
+    if (lane < 4) s.zero[lane] = 0.0;
     __syncthreads();
     STAMP(0);
+
+    // ------------------------------------------------------------ record stream
+    // Stream positions: sweep 0 (initial forward), then per IPM iteration sweeps 1 (backward factor),
+    // 2 (forward), 3 (backward corrector), 4 (forward); each sweep has NP = N+1 rounded up to a
+    // multiple of PD positions (tail positions load a clamped record and compute nothing).  The ring
+    // slot of a position is static (loops unrolled by PD), so the compiler waits only for the slot it
+    // commits; the window loads of every kind are unpredicated (clamped addresses).
+    const int NP = (N1 + PD - 1) / PD * PD;
+    double ring[PD][SLOT];
+    auto issue = [&](auto KIc, double* rs, int q) {
+        constexpr int KI = decltype(KIc)::value;
+        const int qq = q < N ? q : N;
+        const int k = (KI == 1 || KI == 3) ? N - qq : qq;
+        const double* rb = R + (size_t)k * REC;
+        const double* fb = F + (size_t)k * FREC;
+#pragma unroll
+        for (int j = 0; j < n_loads(KI); ++j) {
+            const int e = load_at(KI, j) + lane;
+            if (load_f(KI, j)) rs[j] = fb[e < FREC ? e : FREC - 1];
+            else rs[j] = rb[e < REC ? e : REC - 1];
+        }
+    };
+    auto commit = [&](auto Kc, const double* rs) {
+        constexpr int K = decltype(Kc)::value;
+#pragma unroll
+        for (int j = 0; j < n_loads(K); ++j) win[lane + 64 * j] = rs[j];
+    };
 
     // box rows (k, i, up): t = +-du + d, d = (u - lbu) | (ubu - u)
     auto box_d = [&](int k, int i, int up) -> double {
@@ -291,28 +308,258 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         return up ? s.cst[4 + i] - u : u - s.cst[0 + i];
     };
 
-    // ------------------------------------------------------------ forward sweep (1 barrier per stage)
-    // lane r computes row r of [A~; K] x + [b~; k_ff] (r < 14) or (C^T x)_{r-14} (r = 14..16);
-    // mode 0 (initial iterate, u = 0): rows r < 10 of A x + c from the stage record.
-    // Factor data of nodes < PD comes from fsave (written late in the backward sweeps).
-    const int fw_cx = (lane >= 14 && lane < 17) ? lane - 14 : 0;
-    ldsd* const ljunk = s.p + 15;  // spare LDS double: stores of inactive lanes
-    const int fw_r = lane < NX ? lane : 0;
-    auto fw_stage = [&](int k, int mode, ldsd* dxo, ldsd* duo, ldsd* cxo) {
-        const ldsd* fk = (k < PD) ? s.fsave + k * F_FW : s.frc;
-        const ldsd* crow = s.rec + R_CH + fw_cx;
-        const ldsd* row = lane >= 14 ? crow : mode ? fk + lane * 11 : s.rec + fw_r;
-        const int stride = lane >= 14 ? 3 : mode ? 1 : 10;
-        const double o = mode ? row[10] : s.rec[R_C + fw_r];
-        double v = lane >= 14 ? 0.0 : o;
-        const ldsd* x = dxo + k * NX;
+    // ------------------------------------------------------------ forward stage
+    // lane r < 10: row r of A~ x + b~ (x_{k+1}); r = 10..13: row of K x + k_ff (u_k); r = 14..16:
+    // (C x)_{r-14}; kind 0 (initial iterate, u = 0): rows r < 10 of A x + c from the stage record.
+    // Factor rows of nodes < PD come from fsave (written late in the backward sweeps).
+    const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 17;
+    const int fcj = fc ? lane - 14 : 0;
+    auto fw_stage = [&](auto Kc, int k) {
+        constexpr int K = decltype(Kc)::value;
+        ldsd* const dxo = K == 0 ? s.dx : s.dxc;
+        ldsd* const duo = K == 4 ? s.duc : s.dua;
+        ldsd* const cxo = K == 4 ? s.cxc : s.cxa;
+        const ldsd2* xp = (const ldsd2*)(dxo + k * NX);
+        double row[NX], off;
+        if constexpr (K == 0) {
+            const ldsd* rp = fx ? win + R_AB + lane : fc ? win + R_CT + fcj * 10 : win;
+            const int str = fx ? 10 : 1;
 #pragma unroll
-        for (int l = 0; l < NX; ++l) v += row[l * stride] * x[l];
-        ldsd* dst = (lane >= 14 && lane < 17) ? cxo + k * NS + fw_cx
-                  : (k < N && lane < NX) ? dxo + (k + 1) * NX + lane
-                  : (mode && k < N && lane >= NX && lane < 14) ? duo + k * NU + lane - NX : ljunk;
-        *dst = v;
-        STAMP(14);
+            for (int l = 0; l < NX; ++l) row[l] = rp[l * str];
+            off = *(fx ? win + R_C + lane : s.zero);
+        } else {
+            const ldsd* fk = k < PD ? s.fsave + k * F_FW : win;
+            const ldsd* rp = lane < 14 ? fk + lane * 11 : fc ? win + WF_CT + fcj * 10 : win;
+#pragma unroll
+            for (int l = 0; l < NX; ++l) row[l] = rp[l];
+            off = *(lane < 14 ? fk + lane * 11 + 10 : s.zero);
+        }
+        double a0 = off, a1 = 0.0;
+#pragma unroll
+        for (int l = 0; l < NX / 2; ++l) {
+            const d2 x = xp[l];
+            a0 = fma(row[2 * l], x.x, a0);
+            a1 = fma(row[2 * l + 1], x.y, a1);
+        }
+        ldsd* dst = fc ? cxo + k * NS + fcj
+                  : (k < N && fx) ? dxo + (k + 1) * NX + lane
+                  : (K != 0 && k < N && fu) ? duo + k * NU + lane - NX : s.junk;
+        *dst = a0 + a1;
+    };
+
+    // ------------------------------------------------------------ backward stage, factor
+    // Lane maps (fixed for the solve): accumulator rows a_r = g + 4 r of column c; operand k-step st
+    // covers k = 4 st + g.  Every lane-dependent read is a precomputed window index (R_Z: a zero) and
+    // every store of an inactive lane goes to a junk slot.
+    int og_i[3], h_i[4], t_i[4], ab_i[3], bb_i[3][4], ct_i[4][3], cc_i[3];
+    bool pa_ok[3], p14[4];
+#pragma unroll
+    for (int st = 0; st < 3; ++st) {
+        const int kk = 4 * st + g;
+        og_i[st] = (kk < NX && c < 15) ? c * 10 + kk : R_Z;  // G = [A B c]: column 14 is c (R_C + kk)
+        pa_ok[st] = c < NX && kk < NX;
+    }
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
+        h_i[r] = (a < 14 && c < 14) ? R_H + tri14(lo, hi) : (a < 14 && c == 14) ? R_G + a : R_Z;
+        t_i[r] = (a < NX && c < NX) ? R_H + tri10(lo, hi) : (a < NX && c == 14) ? R_G + a : R_Z;
+        p14[r] = c == 14 && a < NX;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) ct_i[r][j] = a < NX ? R_CT + j * 10 + a : R_Z;
+        if (r < 3) {
+            ab_i[r] = (a < NX && (c < NX || c == 14)) ? (c < NX ? c : 14) * 10 + a : R_Z;
+#pragma unroll
+            for (int i = 0; i < NU; ++i) bb_i[r][i] = a < NX ? (NX + i) * 10 + a : R_Z;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NS; ++j) cc_i[j] = c < NX ? R_CT + j * 10 + c : R_Z;
+    const bool ga = c < 14;                        // G_ab columns (the A operand of G_ab^T W)
+    const double m14 = c == 14 ? 1.0 : 0.0;
+    // box terms: rows 10..13 of M' live in r = 2 (groups 2, 3) and r = 3 (groups 0, 1)
+    int bi[2];
+    double bxm[2], bvm[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const int a = g + 4 * (2 + h);
+        const bool in = a >= NX && a < 14;
+        bi[h] = in ? a - NX : 0;
+        bxm[h] = (in && c == a) ? 1.0 : 0.0;
+        bvm[h] = (in && c == 14) ? 1.0 : 0.0;
+    }
+    double mg[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) mg[i] = g == i ? 1.0 : 0.0;
+    // factor-record store offsets (F_J: junk)
+    const bool xcol = c < NX || c == 14;           // columns of [P | p], [A | c], [K | k_ff]
+    const int xo = c < NX ? c : 10;                // their column in the 11-wide factor-record rows
+    int spc[3], sab[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int a = g + 4 * r;
+        spc[r] = (c == 14 && a < NX) ? F_PC + a : F_J;
+        sab[r] = (xcol && a < NX) ? F_AB + a * 11 + xo : F_J;
+    }
+    const int sk_ = xcol ? F_K + g * 11 + xo : F_J;
+    const int sy_ = c < NX ? F_Y + g * 10 + c : F_J;
+    const int sl_ = lane < 10 ? F_L + lane : F_J;
+    auto fs_at = [&](int k, int e) -> ldsd* { return e < F_FW ? s.fsave + k * F_FW + e : s.junk; };
+
+    d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
+    auto bf_stage = [&](int q) {
+        const int k = N - q;
+        // fold (rank 3, VALU): fold[r] = sum_j C[a][j] (w_j C[c][j] | gamma_j)
+        double fb[NS];
+#pragma unroll
+        for (int j = 0; j < NS; ++j) fb[j] = fma(s.fw[k * NS + j], win[cc_i[j]], m14 * s.fg[k * NS + j]);
+        d4 fold;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) fold[r] = win[ct_i[r][0]] * fb[0] + win[ct_i[r][1]] * fb[1] + win[ct_i[r][2]] * fb[2];
+        if (q == 0) {  // [P_N | p_N] = [H_N | g_N] + fold
+#pragma unroll
+            for (int r = 0; r < 4; ++r) Pa[r] = win[t_i[r]] + fold[r];
+            return;
+        }
+        double* Fk = F + (size_t)k * FREC;
+        // ---- W = P G (K = 10: k-steps 0..2); column 14 -> P c, then + p
+        const double og0 = win[og_i[0]], og1 = win[og_i[1]], og2 = win[og_i[2]];
+        d4 W = {0.0, 0.0, 0.0, 0.0};
+        W = mfma(pa_ok[0] ? Pa[0] : 0.0, og0, W);
+        W = mfma(pa_ok[1] ? Pa[1] : 0.0, og1, W);
+        W = mfma(pa_ok[2] ? Pa[2] : 0.0, og2, W);
+        // ---- M' = G_ab^T W + [H | g] + fold + box terms (VALU part first, off the MFMA chain)
+        d4 M;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) M[r] = win[h_i[r]] + fold[r];
+#pragma unroll
+        for (int h = 0; h < 2; ++h)
+            M[2 + h] += bxm[h] * s.bd[k * NU + bi[h]] + bvm[h] * s.bv[k * NU + bi[h]];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) Fk[spc[r]] = W[r];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) W[r] += p14[r] ? Pa[r] : 0.0;
+        M = mfma(ga ? og0 : 0.0, W[0], M);
+        M = mfma(ga ? og1 : 0.0, W[1], M);
+        M = mfma(ga ? og2 : 0.0, W[2], M);
+        // ---- L = chol(R^): R^[i][j] = M'[10+i][10+j], read straight from the accumulator lanes
+        const double r00 = rdlane(M[2], 42), r10 = rdlane(M[2], 58), r20 = rdlane(M[3], 10), r30 = rdlane(M[3], 26);
+        const double r11 = rdlane(M[2], 59), r21 = rdlane(M[3], 11), r31 = rdlane(M[3], 27);
+        const double r22 = rdlane(M[3], 12), r32 = rdlane(M[3], 28), r33 = rdlane(M[3], 29);
+        // rows 10..13 of M' ([S | R^ | m_u]) of column c into every lane of that column
+        const double s0 = __shfl(M[2], 32 + c), s1 = __shfl(M[2], 48 + c);
+        const double s2 = __shfl(M[3], c), s3 = __shfl(M[3], 16 + c);
+        const double i0 = rsqrt_nr(r00);
+        const double l10 = r10 * i0, l20 = r20 * i0, l30 = r30 * i0;
+        const double i1 = rsqrt_nr(r11 - l10 * l10);
+        const double l21 = (r21 - l20 * l10) * i1, l31 = (r31 - l30 * l10) * i1;
+        const double i2 = rsqrt_nr(r22 - l20 * l20 - l21 * l21);
+        const double l32 = (r32 - l30 * l20 - l31 * l21) * i2;
+        const double i3 = rsqrt_nr(r33 - l30 * l30 - l31 * l31 - l32 * l32);
+        // column c of [Y | w] = L^-1 [S | m_u];  [P | p] <- M' - Y^T [Y | w]  (the critical chain ends here)
+        const double y0 = s0 * i0;
+        const double y1 = (s1 - l10 * y0) * i1;
+        const double y2 = (s2 - l20 * y0 - l21 * y1) * i2;
+        const double y3 = (s3 - l30 * y0 - l31 * y1 - l32 * y2) * i3;
+        const double yg = mg[0] * y0 + mg[1] * y1 + mg[2] * y2 + mg[3] * y3;
+        Pa = mfma(-yg, yg, M);
+        // ---- off the chain: [K | k_ff] = -L^-T [Y | w], [A~ | b~] = [A | c] + B [K | k_ff]
+        const double k3 = -y3 * i3;
+        const double k2 = (-y2 - l32 * k3) * i2;
+        const double k1 = (-y1 - l21 * k2 - l31 * k3) * i1;
+        const double k0 = (-y0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
+        const double kg = mg[0] * k0 + mg[1] * k1 + mg[2] * k2 + mg[3] * k3;
+        double Ab[3];
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            Ab[r] = win[ab_i[r]] + win[bb_i[r][0]] * k0 + win[bb_i[r][1]] * k1 + win[bb_i[r][2]] * k2 + win[bb_i[r][3]] * k3;
+        const double lv = lane == 0 ? i0 : lane == 1 ? l10 : lane == 2 ? i1 : lane == 3 ? l20 : lane == 4 ? l21
+                        : lane == 5 ? i2 : lane == 6 ? l30 : lane == 7 ? l31 : lane == 8 ? l32 : i3;
+        // ---- factor record (and its LDS copy for the first forward stages)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) Fk[sab[r]] = Ab[r];
+        Fk[sk_] = kg;
+        Fk[sy_] = yg;
+        Fk[sl_] = lv;
+        if (k < PD) {
+#pragma unroll
+            for (int r = 0; r < 3; ++r) *fs_at(k, sab[r]) = Ab[r];
+            *fs_at(k, sk_) = kg;
+        }
+    };
+
+    // ------------------------------------------------------------ backward stage, corrector
+    // v = P c + p_{k+1};  lane r < 10: p_k[r] = g~_x[r] + (K^T g~_u)[r] + (A~^T v)[r]   (the chain)
+    //                     lane 10 + i: z_u[i] = g~_u[i] + (B^T v)[i]
+    // then w = L^-1 z_u, k_ff = -L^-T w, b~ = c + B k_ff (off the chain).  g~ = g + fold | box.
+    const ldsd* bc_row = fx ? win + F_AB + lane : fu ? win + WB_R + lane * 10 : win;
+    const int bc_str = fx ? 11 : 1;
+    const ldsd* bc_ct[NS];
+    const ldsd* bc_k[NU];
+    double mu_[NU];
+#pragma unroll
+    for (int j = 0; j < NS; ++j) bc_ct[j] = fx ? win + WB_R + R_CT + j * 10 + lane : s.zero;
+#pragma unroll
+    for (int i = 0; i < NU; ++i) {
+        bc_k[i] = fx ? win + F_K + i * 11 + lane : s.zero;
+        mu_[i] = lane == NX + i ? 1.0 : 0.0;
+    }
+    const ldsd* bc_g = lane < 14 ? win + WB_R + R_G + lane : s.zero;
+    const int bc_st = lane < 14 ? lane * 11 + 10 : F_J;  // b~ rows (lanes < 10), k_ff rows (lanes 10..13)
+    ldsd* const bc_p = fx ? s.p + lane : s.junk;
+    auto bc_stage = [&](int q) {
+        const int k = N - q;
+        double off = *bc_g;
+#pragma unroll
+        for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * *bc_ct[j];
+        if (q == 0) {  // p_N = g_N + sum_j gamma_j C_j^T
+            *bc_p = off;
+            return;
+        }
+        // g~_u (uniform) and the per-lane offset of the chain
+        double gu[NU];
+#pragma unroll
+        for (int i = 0; i < NU; ++i) gu[i] = win[WB_R + R_G + NX + i] + s.bv[k * NU + i];
+#pragma unroll
+        for (int i = 0; i < NU; ++i) off += fx ? *bc_k[i] * gu[i] : mu_[i] * s.bv[k * NU + i];
+        double row[NX];
+#pragma unroll
+        for (int l = 0; l < NX; ++l) row[l] = bc_row[l * bc_str];
+        const ldsd2* pc = (const ldsd2*)(win + F_PC);
+        const ldsd2* pp = (const ldsd2*)s.p;
+        double v[NX];
+#pragma unroll
+        for (int l = 0; l < NX / 2; ++l) {
+            const d2 a = pc[l], p = pp[l];
+            v[2 * l] = a.x + p.x;
+            v[2 * l + 1] = a.y + p.y;
+        }
+        double a0 = off, a1 = 0.0;
+#pragma unroll
+        for (int l = 0; l < NX / 2; ++l) {
+            a0 = fma(row[2 * l], v[2 * l], a0);
+            a1 = fma(row[2 * l + 1], v[2 * l + 1], a1);
+        }
+        const double z = a0 + a1;
+        *bc_p = z;
+        // off the chain: k_ff, b~
+        const double z0 = rdlane(z, 10), z1 = rdlane(z, 11), z2 = rdlane(z, 12), z3 = rdlane(z, 13);
+        const double i0 = win[F_L + 0], l10 = win[F_L + 1], i1 = win[F_L + 2], l20 = win[F_L + 3], l21 = win[F_L + 4];
+        const double i2 = win[F_L + 5], l30 = win[F_L + 6], l31 = win[F_L + 7], l32 = win[F_L + 8], i3 = win[F_L + 9];
+        const double w0 = z0 * i0;
+        const double w1 = (z1 - l10 * w0) * i1;
+        const double w2 = (z2 - l20 * w0 - l21 * w1) * i2;
+        const double w3 = (z3 - l30 * w0 - l31 * w1 - l32 * w2) * i3;
+        const double k3 = -w3 * i3;
+        const double k2 = (-w2 - l32 * k3) * i2;
+        const double k1 = (-w1 - l21 * k2 - l31 * k3) * i1;
+        const double k0 = (-w0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
+        const int bx = fx ? lane : 0;
+        const double bb = win[WB_R + R_C + bx] + win[WB_R + (NX + 0) * 10 + bx] * k0 + win[WB_R + (NX + 1) * 10 + bx] * k1 +
+                          win[WB_R + (NX + 2) * 10 + bx] * k2 + win[WB_R + (NX + 3) * 10 + bx] * k3;
+        const double fv = fx ? bb : mu_[0] * k0 + mu_[1] * k1 + mu_[2] * k2 + mu_[3] * k3;
+        F[(size_t)k * FREC + bc_st] = fv;
+        if (k < PD) *fs_at(k, bc_st) = fv;
     };
 
     // ------------------------------------------------------------ initial iterate (dynamics-feasible):
@@ -396,199 +643,9 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             if (!phase) s.bd[e] = s.lam[8 * k + i] / s.t[8 * k + i] + s.lam[8 * k + 4 + i] / s.t[8 * k + 4 + i];
             s.bv[e] = -box_v(k, i, 0, phase, sigmu) + box_v(k, i, 1, phase, sigmu);
         }
-        __syncthreads();
+        wave_sync();
     };
 
-
-    // ------------------------------------------------------------ backward sweep, factor (MFMA tiles)
-    // Lane maps (fixed for the solve): accumulator rows a_r = lg + 4 r of column lc; operand k-step s
-    // covers k = 4 s + lg.  Everything lane-dependent is precomputed as (valid LDS index, flag) pairs
-    // and applied with selects, and stores of inactive lanes go to junk slots: no divergent branches
-    // (each costs a string of exec-mask SALU work per stage).
-    const int JUNK = FREC - 2;                          // two spare doubles per factor record
-    int hsrc[4], tsrc[4], abi[4], sab[3], spc[3];
-    bool hok[4], tok[4], abok[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int a = lg + 4 * r, c = lc, lo = a < c ? a : c, hi = a < c ? c : a;
-        hok[r] = a < 14 && c <= 14;
-        hsrc[r] = !hok[r] ? 0 : c < 14 ? R_H + tri14(lo, hi) : R_G + a;
-        tok[r] = a < NX && (c < NX || c == 14);
-        tsrc[r] = !tok[r] ? 0 : c < NX ? R_H + tri10(lo, hi) : R_G + a;
-        abok[r] = (c < NX || c == 14) && a < NX;
-        abi[r] = abok[r] ? (c < NX ? c : 14) * 10 + a : 0;
-    }
-    const bool xcol = lc < NX || lc == 14;        // columns of [P | p], [A | c], [K | k_ff]
-    const int xcol_o = lc < NX ? lc : 10;         // their column in the 11-wide factor-record rows
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const int a = lg + 4 * r;
-        sab[r] = (xcol && a < NX) ? F_AB + a * 11 + xcol_o : JUNK;
-        spc[r] = (lc == 14 && a < NX) ? F_PC + a : JUNK;
-    }
-    const int sk_ = xcol ? F_K + lg * 11 + xcol_o : JUNK;
-    const int sy_ = lc < NX ? F_Y + lg * 10 + lc : JUNK;
-    const int sl_ = lane < 10 ? F_L + lane : JUNK;
-    int ogi[3];
-    bool ogok[3], paok[3];
-#pragma unroll
-    for (int st = 0; st < 3; ++st) {
-        const int kk = 4 * st + lg;
-        ogok[st] = lc < 15 && kk < NX;              // G = [A B c]: 15 columns, 10 rows
-        ogi[st] = ogok[st] ? lc * 10 + kk : 0;
-        paok[st] = lc < NX && kk < NX;
-    }
-    const bool cgok = lc < NX && lg < NS;
-    const int cgi = cgok ? R_CH + lc * 3 + lg : 0, lg3 = lg < NS ? lg : 0;
-    const int bmi = (NX + lg) * 10 + (lc < NX ? lc : 0);  // B[lc][lg] for the closed loop
-    const double eye = lc == NX + lg ? 1.0 : 0.0;          // A operand of the box-term product
-    auto fs_at = [&](int k, int e) -> ldsd* { return e < F_FW ? s.fsave + k * F_FW + e : ljunk; };
-
-    d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
-    auto bf_stage = [&](int q) {
-        const int k = N - q;
-        const ldsd* rk = s.rec;
-        // fold (rank 3): A[a][j] = C[a][j], B[j][c] = w_j C[c][j] (c < 10) | gamma_j (c = 14)
-        const double cgv = rk[cgi], cg = cgok ? cgv : 0.0;
-        const double fwj = s.fw[k * NS + lg3], fgj = s.fg[k * NS + lg3];
-        const double fb = lg >= NS ? 0.0 : lc < NX ? fwj * cg : (lc == 14 ? fgj : 0.0);
-        if (q == 0) {  // [P_N | p_N] = [H_N | g_N] + fold
-            d4 base;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const double v = rk[tsrc[r]];
-                base[r] = tok[r] ? v : 0.0;
-            }
-            Pa = mfma(cg, fb, base);
-            return;
-        }
-        double* Fk = F + (size_t)k * FREC;
-        // ---- W = P G (K = 10: k-steps 0..2, rows k >= 10 zero); column 14 -> P c, then + p
-        double og[3];
-#pragma unroll
-        for (int st = 0; st < 3; ++st) {
-            const double v = rk[ogi[st]];
-            og[st] = ogok[st] ? v : 0.0;
-        }
-        d4 W = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int st = 0; st < 3; ++st) W = mfma(paok[st] ? Pa[st] : 0.0, og[st], W);
-#pragma unroll
-        for (int r = 0; r < 3; ++r) Fk[spc[r]] = W[r];
-        const bool c14 = lc == 14;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) W[r] += c14 ? Pa[r] : 0.0;
-        STAMP(9);
-        // ---- M' = G_ab^T W + [H | g] + fold + box terms (identity rows 10..13 times [diag | v])
-        d4 M;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const double v = rk[hsrc[r]];
-            M[r] = hok[r] ? v : 0.0;
-        }
-        const double bdv = s.bd[k * 4 + lg], bvv = s.bv[k * 4 + lg];
-        M = mfma(eye, lc == NX + lg ? bdv : (c14 ? bvv : 0.0), M);
-        M = mfma(cg, fb, M);
-#pragma unroll
-        for (int st = 0; st < 3; ++st) M = mfma(lc < 14 ? og[st] : 0.0, W[st], M);
-        STAMP(10);
-        // ---- rows 10..13 of M' ([S | R^ | m_u]) of column lc into every lane of that column
-        const double s0 = __shfl(M[2], 32 + lc), s1 = __shfl(M[2], 48 + lc);
-        const double s2 = __shfl(M[3], lc), s3 = __shfl(M[3], 16 + lc);
-        // L = chol(R^): R^[i][j] is s_i of lane 10 + j (uniform, scalar registers)
-        const double r00 = rdlane(s0, 10), r10 = rdlane(s1, 10), r20 = rdlane(s2, 10), r30 = rdlane(s3, 10);
-        const double r11 = rdlane(s1, 11), r21 = rdlane(s2, 11), r31 = rdlane(s3, 11);
-        const double r22 = rdlane(s2, 12), r32 = rdlane(s3, 12), r33 = rdlane(s3, 13);
-        const double i0 = rsqrt_nr(r00);
-        const double l10 = r10 * i0, l20 = r20 * i0, l30 = r30 * i0;
-        const double i1 = rsqrt_nr(r11 - l10 * l10);
-        const double l21 = (r21 - l20 * l10) * i1, l31 = (r31 - l30 * l10) * i1;
-        const double i2 = rsqrt_nr(r22 - l20 * l20 - l21 * l21);
-        const double l32 = (r32 - l30 * l20 - l31 * l21) * i2;
-        const double i3 = rsqrt_nr(r33 - l30 * l30 - l31 * l31 - l32 * l32);
-        // column lc of [Y | w] = L^-1 [S | m_u] and of [K | k_ff] = -L^-T [Y | w]
-        const double y0 = s0 * i0;
-        const double y1 = (s1 - l10 * y0) * i1;
-        const double y2 = (s2 - l20 * y0 - l21 * y1) * i2;
-        const double y3 = (s3 - l30 * y0 - l31 * y1 - l32 * y2) * i3;
-        const double k3 = -y3 * i3;
-        const double k2 = (-y2 - l32 * k3) * i2;
-        const double k1 = (-y1 - l21 * k2 - l31 * k3) * i1;
-        const double k0 = (-y0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
-        const double yg = lg == 0 ? y0 : lg == 1 ? y1 : lg == 2 ? y2 : y3;
-        const double kg = lg == 0 ? k0 : lg == 1 ? k1 : lg == 2 ? k2 : k3;
-        STAMP(11);
-        // ---- [P | p] <- M' - Y^T [Y | w];  [A~ | b~] = [A | c] + B [K | k_ff]
-        Pa = mfma(-yg, yg, M);
-        d4 Ab;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const double v = rk[abi[r]];
-            Ab[r] = abok[r] ? v : 0.0;
-        }
-        const double bm = rk[bmi];
-        Ab = mfma(lc < NX ? bm : 0.0, kg, Ab);
-        STAMP(12);
-        // ---- factor record (and its LDS copy for the first forward stages)
-        const double lv = lane == 0 ? i0 : lane == 1 ? l10 : lane == 2 ? i1 : lane == 3 ? l20 : lane == 4 ? l21
-                        : lane == 5 ? i2 : lane == 6 ? l30 : lane == 7 ? l31 : lane == 8 ? l32 : i3;
-#pragma unroll
-        for (int r = 0; r < 3; ++r) Fk[sab[r]] = Ab[r];
-        Fk[sk_] = kg;
-        Fk[sy_] = yg;
-        Fk[sl_] = lv;
-        if (k < PD) {
-#pragma unroll
-            for (int r = 0; r < 3; ++r) *fs_at(k, sab[r]) = Ab[r];
-            *fs_at(k, sk_) = kg;
-        }
-        STAMP(13);
-    };
-
-    // ------------------------------------------------------------ backward sweep, corrector (1 barrier / stage)
-    // stored factors + corrector gradient: Pb = P c + p, z = [g_x + A^T Pb + fold | g_u + B^T Pb + box],
-    // w = L^-1 z_u, p_k = z_x - Y^T w, k_ff = -L^-T w, b~ = c + B k_ff.  Lane r < 14 owns row r of z.
-    const int bc_r = lane < 14 ? lane : 0, bc_x = bc_r < NX ? bc_r : 0, bc_u = bc_r >= NX ? bc_r - NX : 0;
-    const int bc_st = lane < NX ? F_AB + lane * 11 + 10 : lane < 14 ? F_K + (lane - NX) * 11 + 10 : JUNK;
-    ldsd* const bc_p = lane < NX ? s.p + lane : ljunk;
-    auto bc_stage = [&](int q) {
-        const int k = N - q, r = bc_r;
-        const ldsd* rk = s.rec;
-        double fold = 0.0;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) fold += s.fg[k * NS + j] * rk[R_CH + bc_x * 3 + j];
-        if (q == 0) {  // p_N = g_N + sum_j gamma_j C_j^T
-            *bc_p = rk[R_G + bc_x] + fold;
-            return;
-        }
-        const ldsd* fk = s.frc - F_FW;  // factor-record window starts at F_FW
-        double z = rk[R_G + r];
-#pragma unroll
-        for (int l = 0; l < NX; ++l) z += rk[r * 10 + l] * (fk[F_PC + l] + s.p[l]);
-        const double bvv = s.bv[k * 4 + bc_u];
-        z += r < NX ? fold : bvv;
-        const double z0 = rdlane(z, 10), z1 = rdlane(z, 11), z2 = rdlane(z, 12), z3 = rdlane(z, 13);
-        const double i0 = fk[F_L + 0], l10 = fk[F_L + 1], i1 = fk[F_L + 2], l20 = fk[F_L + 3], l21 = fk[F_L + 4];
-        const double i2 = fk[F_L + 5], l30 = fk[F_L + 6], l31 = fk[F_L + 7], l32 = fk[F_L + 8], i3 = fk[F_L + 9];
-        const double w0 = z0 * i0;
-        const double w1 = (z1 - l10 * w0) * i1;
-        const double w2 = (z2 - l20 * w0 - l21 * w1) * i2;
-        const double w3 = (z3 - l30 * w0 - l31 * w1 - l32 * w2) * i3;
-        const double k3 = -w3 * i3;
-        const double k2 = (-w2 - l32 * k3) * i2;
-        const double k1 = (-w1 - l21 * k2 - l31 * k3) * i1;
-        const double k0 = (-w0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
-        const double pn = z - fk[F_Y + bc_x] * w0 - fk[F_Y + 10 + bc_x] * w1 - fk[F_Y + 20 + bc_x] * w2 -
-                          fk[F_Y + 30 + bc_x] * w3;
-        const double bb = rk[R_C + bc_x] + rk[(NX + 0) * 10 + bc_x] * k0 + rk[(NX + 1) * 10 + bc_x] * k1 +
-                          rk[(NX + 2) * 10 + bc_x] * k2 + rk[(NX + 3) * 10 + bc_x] * k3;
-        const double kv = bc_u == 0 ? k0 : bc_u == 1 ? k1 : bc_u == 2 ? k2 : k3;
-        const double fv = lane < NX ? bb : kv;
-        *bc_p = pn;
-        F[(size_t)k * FREC + bc_st] = fv;
-        if (k < PD) *fs_at(k, bc_st) = fv;
-        STAMP(15);
-    };
 
     // row values of a soft group (k, j) at an LQR solution with C dx = cxs, and its slacks
     auto soft_vals = [&](const Grp& g, int k, int j, double cxs, double* v) {
@@ -720,59 +777,72 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         rp *= (1.0 - al);
     };
 
-    int it = 0, kind = 0;
-    double sigmu = 0.0;
-    for (;;) {
-        // ---- before the sweep
-        if (kind == 1) {
-            if ((mu < A.tol && rp < A.tol) || it >= A.max_iter) break;
-            terms(0, 0.0);
-        } else if (kind == 3) {
-            sigmu = rows_pred();
-            terms(1, sigmu);
+    // ------------------------------------------------------------ IPM: sweeps over the record stream
+    auto stage = [&](auto Kc, int q) {
+        constexpr int K = decltype(Kc)::value;
+        if constexpr (K == 1) bf_stage(q);
+        else if constexpr (K == 3) bc_stage(q);
+        else fw_stage(Kc, q);
+    };
+    // one stream position: commit ring slot S (position q of this sweep), refill it with position qi
+    // of a sweep of kind KI, run the stage
+    auto position = [&](auto Kc, auto KIc, auto Sc, int q, int qi, bool live) {
+        constexpr int S = decltype(Sc)::value;
+        commit(Kc, ring[S]);
+        issue(KIc, ring[S], qi);
+        wave_sync();
+        if (live) stage(Kc, q);
+        wave_sync();
+    };
+    auto sweep = [&](auto Kc) {
+        constexpr int K = decltype(Kc)::value, KN = K == 4 ? 1 : K + 1;
+        int q0 = 0;
+        for (; q0 < NP - PD; q0 += PD) {  // every position of these trips is a node
+            position(Kc, Kc, IC<0>{}, q0, q0 + PD, true);
+            position(Kc, Kc, IC<1>{}, q0 + 1, q0 + 1 + PD, true);
+            position(Kc, Kc, IC<2>{}, q0 + 2, q0 + 2 + PD, true);
         }
-        if ((kind == 2 || kind == 4) && lane < NX) s.dxc[lane] = s.dx[lane];
-        __syncthreads();
-        STAMP(4);
-        const int mode = kind != 0;
-        s.rec = s.recw - win_r(kind);
-        ldsd* dxo = kind == 0 ? s.dx : s.dxc;
-        ldsd* duo = kind == 4 ? s.duc : s.dua;
-        ldsd* cxo = kind == 4 ? s.cxc : s.cxa;
-        // ---- the sweep: NP stream positions, PD per trip with static ring slots
-        auto stage = [&](auto slot, int q) {
-            constexpr int S = decltype(slot)::value;
-            commit_from(rr[S], fr[S]);
-            issue_to(rr[S], fr[S], pi);
-            next(pi);
-            __syncthreads();
-            STAMP(8);
-            if (q < N1) {
-                if (kind == 1) bf_stage(q);
-                else if (kind == 3) bc_stage(q);
-                else fw_stage(q, mode, dxo, duo, cxo);
-            }
-            __syncthreads();
-        };
-        for (int q0 = 0; q0 < NP; q0 += PD) {
-            stage(std::integral_constant<int, 0>{}, q0);
-            stage(std::integral_constant<int, 1>{}, q0 + 1);
-            stage(std::integral_constant<int, 2>{}, q0 + 2);
-        }
-        STAMP(kind == 1 ? 2 : kind == 3 ? 5 : kind == 0 ? 1 : 3);
-        // ---- after the sweep
-        if (kind == 0) {
-            rp = rows_init();
-            double lmu = 0.0;
-            for (int r = lane; r < m; r += 64) lmu += s.t[r] * s.lam[r];
-            mu = wsum(lmu) / m;
-        } else if (kind == 4) {
-            rows_update(sigmu);
-            ++it;
-        }
-        __syncthreads();
+        // last trip: refill with the next sweep's first positions; tail positions compute nothing
+        position(Kc, IC<KN>{}, IC<0>{}, q0, 0, q0 < N1);
+        position(Kc, IC<KN>{}, IC<1>{}, q0 + 1, 1, q0 + 1 < N1);
+        position(Kc, IC<KN>{}, IC<2>{}, q0 + 2, 2, q0 + 2 < N1);
+    };
+
+    issue(IC<0>{}, ring[0], 0);
+    issue(IC<0>{}, ring[1], 1);
+    issue(IC<0>{}, ring[2], 2);
+    sweep(IC<0>{});
+    STAMP(1);
+    rp = rows_init();
+    {
+        double lmu = 0.0;
+        for (int r = lane; r < m; r += 64) lmu += s.t[r] * s.lam[r];
+        mu = wsum(lmu) / m;
+    }
+    wave_sync();
+    int it = 0;
+    while (!(mu < A.tol && rp < A.tol) && it < A.max_iter) {
+        terms(0, 0.0);
         STAMP(6);
-        kind = kind == 4 ? 1 : kind + 1;
+        sweep(IC<1>{});
+        STAMP(2);
+        if (lane < NX) s.dxc[lane] = s.dx[lane];
+        wave_sync();
+        sweep(IC<2>{});
+        STAMP(3);
+        const double sigmu = rows_pred();
+        terms(1, sigmu);
+        STAMP(4);
+        sweep(IC<3>{});
+        STAMP(5);
+        if (lane < NX) s.dxc[lane] = s.dx[lane];
+        wave_sync();
+        sweep(IC<4>{});
+        STAMP(3);
+        rows_update(sigmu);
+        wave_sync();
+        STAMP(6);
+        ++it;
     }
     STAMP_OUT
     // ------------------------------------------------------------ outputs
