@@ -42,7 +42,7 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
            + 2 * qp_even(N1 * 3)            // cxa, cxc
            + QP_SLOT * 64                   // committed stream window
            + QP_RING * 154                  // [A~|b~ K|k_ff] of nodes 0..RING-1 (written late in a backward sweep)
-           + 16 + 4                         // corrector p; zero / junk doubles
+           + 16 + 48 + 2                    // corrector p; zero rows; junk
            + qp_even((size_t)N * 4) + qp_even(N1 * 3) + qp_even(N1)  // u, h, s_k
            + 2 * qp_even(N1 * 3)            // soft-row folds (w, gamma)
            + 2 * qp_even((size_t)N * 4)     // box terms (diag, v)

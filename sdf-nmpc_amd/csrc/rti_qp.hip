@@ -63,11 +63,11 @@ constexpr int SLOT = QP_SLOT, PD = QP_RING;
 // Window of one stream position per sweep kind: n_loads(K) loads of 64 consecutive doubles (lanes
 // clamped to the record), load j landing at window offset 64 j:
 //   0 initial forward     R[0, 256)                    AB, c, C^T in place
-//   1 backward factor     R[0, 320)                    the stage record in place (R_Z reads 0)
+//   1 backward factor     R[0, 384)                    the stage record in place; [R_Z, 384) reads 0
 //   2, 4 forward          F[0, 192) | R[164, 228)      factor rows at 0, C^T at WF_CT
 //   3 backward corrector  F[0, 256) | R[100, 228)      factor record at 0, R[i] at WB_R + i (i >= 100)
 constexpr int WF_CT = 192, WB_R = 256 - 100;
-__host__ __device__ constexpr int n_loads(int K) { return K == 1 ? 5 : K == 3 ? 6 : 4; }
+__host__ __device__ constexpr int n_loads(int K) { return (K == 1 || K == 3) ? 6 : 4; }
 __host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K == 4) ? j < 3 : K == 3 ? j < 4 : false; }
 __host__ __device__ constexpr int load_at(int K, int j) {
     return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 4 ? 64 * j : 100 + 64 * (j - 4));
@@ -126,6 +126,13 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// a copy of v the compiler cannot see through (blocks hoisting of what is derived from it)
+__device__ __forceinline__ int opaque(int v) {
+    int r;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+    return r;
+}
+
 struct Smem {
     ldsd *t, *lam;                 // [m] inequality slacks / duals
     ldsd *dx, *dxc;                // iterate dx; sweep solution (x of predictor, then corrector)
@@ -134,7 +141,7 @@ struct Smem {
     ldsd* win;                     // committed stream window
     ldsd* fsave;                   // [A~|b~ K|k_ff] of nodes < PD
     ldsd* p;                       // corrector Riccati vector p (the factor sweep keeps p in registers)
-    ldsd *zero, *junk;             // two doubles that stay 0; two that absorb stores of inactive lanes
+    ldsd *zero, *junk;             // 48 doubles that stay 0 (zero rows for strided reads); a store sink
     ldsd *uu, *hv, *skv;           // u (box constants), h, cost scaling per node
     ldsd *fw, *fg, *bd, *bv;       // soft folds [N+1][3] (w, gamma), box terms [N][4] (diag, v)
     ldsd* cst;                     // lbu 4 | ubu 4 | lh 3 | uh 3 | zl 3 | Zl 3 (lane-indexed kernel arguments
@@ -150,7 +157,7 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubl
     s.du = take(N * NU); s.dua = take(N * NU); s.duc = take(N * NU);
     s.cxa = take(N1 * NS); s.cxc = take(N1 * NS);
     s.win = take(SLOT * 64); s.fsave = take(PD * F_FW);
-    s.p = take(16); s.zero = take(4); s.junk = s.zero + 2;
+    s.p = take(16); s.zero = take(48); s.junk = take(2);
     s.uu = take(N * NU); s.hv = take(N1 * NS); s.skv = take(N1);
     s.fw = take(N1 * NS); s.fg = take(N1 * NS); s.bd = take(N * NU); s.bv = take(N * NU);
     s.cst = take(20);
@@ -240,7 +247,7 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
 __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     extern __shared__ __align__(16) double lds_q[];
     STAMP_DECL
-    const int b = blockIdx.x, lane = threadIdx.x, g = lane >> 4, c = lane & 15;
+    const int b = blockIdx.x, lane = threadIdx.x;
     const int N = A.N, N1 = N + 1, m = 8 * N + 12 * N1;
     const Smem s = carve((ldsd*)lds_q, N);
     ldsd* const win = s.win;
@@ -271,7 +278,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     }
     for (int e = lane; e < N1; e += 64) s.skv[e] = (A.cost_scaling && e < N) ? A.dt[e] : 1.0;
     if (lane < NX) s.dx[lane] = A.x0[(size_t)b * 10 + lane] - A.x[(size_t)b * N1 * 10 + lane];
-    if (lane < 4) s.zero[lane] = 0.0;
+    if (lane < 48) s.zero[lane] = 0.0;
     __syncthreads();
     STAMP(0);
 
@@ -312,9 +319,9 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // lane r < 10: row r of A~ x + b~ (x_{k+1}); r = 10..13: row of K x + k_ff (u_k); r = 14..16:
     // (C x)_{r-14}; kind 0 (initial iterate, u = 0): rows r < 10 of A x + c from the stage record.
     // Factor rows of nodes < PD come from fsave (written late in the backward sweeps).
-    const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 17;
-    const int fcj = fc ? lane - 14 : 0;
-    auto fw_stage = [&](auto Kc, int k) {
+    auto fw_stage = [&](auto Kc, int k, const int lane) {
+        const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 17;
+        const int fcj = fc ? lane - 14 : 0;
         constexpr int K = decltype(Kc)::value;
         ldsd* const dxo = K == 0 ? s.dx : s.dxc;
         ldsd* const duo = K == 4 ? s.duc : s.dua;
@@ -351,83 +358,84 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // Lane maps (fixed for the solve): accumulator rows a_r = g + 4 r of column c; operand k-step st
     // covers k = 4 st + g.  Every lane-dependent read is a precomputed window index (R_Z: a zero) and
     // every store of an inactive lane goes to a junk slot.
-    int og_i[3], h_i[4], t_i[4], ab_i[3], bb_i[3][4], ct_i[4][3], cc_i[3];
-    bool pa_ok[3], p14[4];
-#pragma unroll
-    for (int st = 0; st < 3; ++st) {
-        const int kk = 4 * st + g;
-        og_i[st] = (kk < NX && c < 15) ? c * 10 + kk : R_Z;  // G = [A B c]: column 14 is c (R_C + kk)
-        pa_ok[st] = c < NX && kk < NX;
-    }
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
-        h_i[r] = (a < 14 && c < 14) ? R_H + tri14(lo, hi) : (a < 14 && c == 14) ? R_G + a : R_Z;
-        t_i[r] = (a < NX && c < NX) ? R_H + tri10(lo, hi) : (a < NX && c == 14) ? R_G + a : R_Z;
-        p14[r] = c == 14 && a < NX;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) ct_i[r][j] = a < NX ? R_CT + j * 10 + a : R_Z;
-        if (r < 3) {
-            ab_i[r] = (a < NX && (c < NX || c == 14)) ? (c < NX ? c : 14) * 10 + a : R_Z;
-#pragma unroll
-            for (int i = 0; i < NU; ++i) bb_i[r][i] = a < NX ? (NX + i) * 10 + a : R_Z;
-        }
-    }
-#pragma unroll
-    for (int j = 0; j < NS; ++j) cc_i[j] = c < NX ? R_CT + j * 10 + c : R_Z;
-    const bool ga = c < 14;                        // G_ab columns (the A operand of G_ab^T W)
-    const double m14 = c == 14 ? 1.0 : 0.0;
-    // box terms: rows 10..13 of M' live in r = 2 (groups 2, 3) and r = 3 (groups 0, 1)
-    int bi[2];
-    double bxm[2], bvm[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const int a = g + 4 * (2 + h);
-        const bool in = a >= NX && a < 14;
-        bi[h] = in ? a - NX : 0;
-        bxm[h] = (in && c == a) ? 1.0 : 0.0;
-        bvm[h] = (in && c == 14) ? 1.0 : 0.0;
-    }
-    double mg[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) mg[i] = g == i ? 1.0 : 0.0;
-    // factor-record store offsets (F_J: junk)
-    const bool xcol = c < NX || c == 14;           // columns of [P | p], [A | c], [K | k_ff]
-    const int xo = c < NX ? c : 10;                // their column in the 11-wide factor-record rows
-    int spc[3], sab[3];
-#pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        const int a = g + 4 * r;
-        spc[r] = (c == 14 && a < NX) ? F_PC + a : F_J;
-        sab[r] = (xcol && a < NX) ? F_AB + a * 11 + xo : F_J;
-    }
-    const int sk_ = xcol ? F_K + g * 11 + xo : F_J;
-    const int sy_ = c < NX ? F_Y + g * 10 + c : F_J;
-    const int sl_ = lane < 10 ? F_L + lane : F_J;
     auto fs_at = [&](int k, int e) -> ldsd* { return e < F_FW ? s.fsave + k * F_FW + e : s.junk; };
 
     d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
-    auto bf_stage = [&](int q) {
+    auto bf_stage = [&](int q, const int lane) {
+        const int g = lane >> 4, c = lane & 15;
+        // Index bases with immediate offsets: a base is R_Z for an inactive lane, and the window is 0 from
+        // R_Z up to 384 in the factor sweep, so base + offset stays 0 there.
+        // og: G[4 st + g][c] (G = [A B c]; column 14 is c at R_C + k) at og01 + 4 st (st = 0, 1), og2
+        const int og01 = c < 15 ? c * 10 + g : R_Z, og2 = (c < 15 && g < 2) ? c * 10 + g + 8 : R_Z;
+        const bool pa2 = c < NX && g < 2, pa01 = c < NX;
+        int h_i[4];
+        bool p14[4];
+    #pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
+            h_i[r] = (a < 14 && c < 14) ? R_H + tri14(lo, hi) : (a < 14 && c == 14) ? R_G + a : R_Z;
+            p14[r] = c == 14 && a < NX;
+        }
+        // fold rows C^T[j][a]: rows a = g + 4 r at ct01 + 4 r + 10 j (r = 0, 1), ct2 + 10 j; column c at cc + 10 j
+        const int ct01 = R_CT + g, ct2 = g < 2 ? R_CT + g + 8 : R_Z, cc = c < NX ? R_CT + c : R_Z;
+        // closed loop: [A | c][a][c] at ab01 + 4 r, ab2; B[a][i] at bb01 + 4 r + 10 i, bb2 + 10 i
+        const bool xcol = c < NX || c == 14;           // columns of [P | p], [A | c], [K | k_ff]
+        const int xo = c < NX ? c : 10;                // their column in the 11-wide factor-record rows
+        const int ab01 = xcol ? (c < NX ? c : 14) * 10 + g : R_Z, ab2 = (xcol && g < 2) ? (c < NX ? c : 14) * 10 + g + 8 : R_Z;
+        const int bb01 = 100 + g, bb2 = g < 2 ? 108 + g : R_Z;
+        const bool ga = c < 14;                        // G_ab columns (the A operand of G_ab^T W)
+        const double m14 = c == 14 ? 1.0 : 0.0;
+        // box terms: rows 10..13 of M' live in r = 2 (groups 2, 3) and r = 3 (groups 0, 1)
+        int bi[2];
+        double bxm[2], bvm[2];
+    #pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int a = g + 4 * (2 + h);
+            const bool in = a >= NX && a < 14;
+            bi[h] = in ? a - NX : 0;
+            bxm[h] = (in && c == a) ? 1.0 : 0.0;
+            bvm[h] = (in && c == 14) ? 1.0 : 0.0;
+        }
+        double mg[4];
+    #pragma unroll
+        for (int i = 0; i < 4; ++i) mg[i] = g == i ? 1.0 : 0.0;
+        // factor-record store offsets (F_J: junk)
+        unsigned spc[3], sab[3];
+    #pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            const int a = g + 4 * r;
+            spc[r] = (c == 14 && a < NX) ? F_PC + a : F_J;
+            sab[r] = (xcol && a < NX) ? F_AB + a * 11 + xo : F_J;
+        }
+        const unsigned sk_ = xcol ? F_K + g * 11 + xo : F_J;
+        const unsigned sy_ = c < NX ? F_Y + g * 10 + c : F_J;
         const int k = N - q;
         // fold (rank 3, VALU): fold[r] = sum_j C[a][j] (w_j C[c][j] | gamma_j)
         double fb[NS];
 #pragma unroll
-        for (int j = 0; j < NS; ++j) fb[j] = fma(s.fw[k * NS + j], win[cc_i[j]], m14 * s.fg[k * NS + j]);
+        for (int j = 0; j < NS; ++j) fb[j] = fma(s.fw[k * NS + j], win[cc + 10 * j], m14 * s.fg[k * NS + j]);
         d4 fold;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) fold[r] = win[ct_i[r][0]] * fb[0] + win[ct_i[r][1]] * fb[1] + win[ct_i[r][2]] * fb[2];
+        for (int r = 0; r < 2; ++r)
+            fold[r] = win[ct01 + 4 * r] * fb[0] + win[ct01 + 4 * r + 10] * fb[1] + win[ct01 + 4 * r + 20] * fb[2];
+        fold[2] = win[ct2] * fb[0] + win[ct2 + 10] * fb[1] + win[ct2 + 20] * fb[2];
+        fold[3] = 0.0;
         if (q == 0) {  // [P_N | p_N] = [H_N | g_N] + fold
 #pragma unroll
-            for (int r = 0; r < 4; ++r) Pa[r] = win[t_i[r]] + fold[r];
+            for (int r = 0; r < 4; ++r) {
+                const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
+                const int t = (a < NX && c < NX) ? R_H + tri10(lo, hi) : (a < NX && c == 14) ? R_G + a : R_Z;
+                Pa[r] = win[t] + fold[r];
+            }
             return;
         }
         double* Fk = F + (size_t)k * FREC;
         // ---- W = P G (K = 10: k-steps 0..2); column 14 -> P c, then + p
-        const double og0 = win[og_i[0]], og1 = win[og_i[1]], og2 = win[og_i[2]];
+        const double og0 = win[og01], og1 = win[og01 + 4], og2v = win[og2];
         d4 W = {0.0, 0.0, 0.0, 0.0};
-        W = mfma(pa_ok[0] ? Pa[0] : 0.0, og0, W);
-        W = mfma(pa_ok[1] ? Pa[1] : 0.0, og1, W);
-        W = mfma(pa_ok[2] ? Pa[2] : 0.0, og2, W);
+        W = mfma(pa01 ? Pa[0] : 0.0, og0, W);
+        W = mfma(pa01 ? Pa[1] : 0.0, og1, W);
+        W = mfma(pa2 ? Pa[2] : 0.0, og2v, W);
         // ---- M' = G_ab^T W + [H | g] + fold + box terms (VALU part first, off the MFMA chain)
         d4 M;
 #pragma unroll
@@ -435,13 +443,24 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
         for (int h = 0; h < 2; ++h)
             M[2 + h] += bxm[h] * s.bd[k * NU + bi[h]] + bvm[h] * s.bv[k * NU + bi[h]];
+        // closed-loop operands (read now, used after the Cholesky)
+        double Ai[3], Bi[3][NU];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            Ai[r] = win[ab01 + 4 * r];
+#pragma unroll
+            for (int i = 0; i < NU; ++i) Bi[r][i] = win[bb01 + 4 * r + 10 * i];
+        }
+        Ai[2] = win[ab2];
+#pragma unroll
+        for (int i = 0; i < NU; ++i) Bi[2][i] = win[bb2 + 10 * i];
 #pragma unroll
         for (int r = 0; r < 3; ++r) Fk[spc[r]] = W[r];
 #pragma unroll
         for (int r = 0; r < 4; ++r) W[r] += p14[r] ? Pa[r] : 0.0;
         M = mfma(ga ? og0 : 0.0, W[0], M);
         M = mfma(ga ? og1 : 0.0, W[1], M);
-        M = mfma(ga ? og2 : 0.0, W[2], M);
+        M = mfma(ga ? og2v : 0.0, W[2], M);
         // ---- L = chol(R^): R^[i][j] = M'[10+i][10+j], read straight from the accumulator lanes
         const double r00 = rdlane(M[2], 42), r10 = rdlane(M[2], 58), r20 = rdlane(M[3], 10), r30 = rdlane(M[3], 26);
         const double r11 = rdlane(M[2], 59), r21 = rdlane(M[3], 11), r31 = rdlane(M[3], 27);
@@ -471,16 +490,16 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double kg = mg[0] * k0 + mg[1] * k1 + mg[2] * k2 + mg[3] * k3;
         double Ab[3];
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
-            Ab[r] = win[ab_i[r]] + win[bb_i[r][0]] * k0 + win[bb_i[r][1]] * k1 + win[bb_i[r][2]] * k2 + win[bb_i[r][3]] * k3;
-        const double lv = lane == 0 ? i0 : lane == 1 ? l10 : lane == 2 ? i1 : lane == 3 ? l20 : lane == 4 ? l21
-                        : lane == 5 ? i2 : lane == 6 ? l30 : lane == 7 ? l31 : lane == 8 ? l32 : i3;
+        for (int r = 0; r < 3; ++r) Ab[r] = Ai[r] + Bi[r][0] * k0 + Bi[r][1] * k1 + Bi[r][2] * k2 + Bi[r][3] * k3;
         // ---- factor record (and its LDS copy for the first forward stages)
 #pragma unroll
         for (int r = 0; r < 3; ++r) Fk[sab[r]] = Ab[r];
         Fk[sk_] = kg;
         Fk[sy_] = yg;
-        Fk[sl_] = lv;
+        {  // the (uniform) Cholesky factor: every lane stores the same 16 bytes, no lane selection
+            d2* Lp = (d2*)(Fk + F_L);
+            Lp[0] = d2{i0, l10}; Lp[1] = d2{i1, l20}; Lp[2] = d2{l21, i2}; Lp[3] = d2{l30, l31}; Lp[4] = d2{l32, i3};
+        }
         if (k < PD) {
 #pragma unroll
             for (int r = 0; r < 3; ++r) *fs_at(k, sab[r]) = Ab[r];
@@ -492,36 +511,34 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // v = P c + p_{k+1};  lane r < 10: p_k[r] = g~_x[r] + (K^T g~_u)[r] + (A~^T v)[r]   (the chain)
     //                     lane 10 + i: z_u[i] = g~_u[i] + (B^T v)[i]
     // then w = L^-1 z_u, k_ff = -L^-T w, b~ = c + B k_ff (off the chain).  g~ = g + fold | box.
-    const ldsd* bc_row = fx ? win + F_AB + lane : fu ? win + WB_R + lane * 10 : win;
-    const int bc_str = fx ? 11 : 1;
-    const ldsd* bc_ct[NS];
-    const ldsd* bc_k[NU];
-    double mu_[NU];
-#pragma unroll
-    for (int j = 0; j < NS; ++j) bc_ct[j] = fx ? win + WB_R + R_CT + j * 10 + lane : s.zero;
-#pragma unroll
-    for (int i = 0; i < NU; ++i) {
-        bc_k[i] = fx ? win + F_K + i * 11 + lane : s.zero;
-        mu_[i] = lane == NX + i ? 1.0 : 0.0;
-    }
-    const ldsd* bc_g = lane < 14 ? win + WB_R + R_G + lane : s.zero;
-    const int bc_st = lane < 14 ? lane * 11 + 10 : F_J;  // b~ rows (lanes < 10), k_ff rows (lanes 10..13)
-    ldsd* const bc_p = fx ? s.p + lane : s.junk;
-    auto bc_stage = [&](int q) {
+    auto bc_stage = [&](int q, const int lane) {
+        const bool fx = lane < NX, fu = lane >= NX && lane < 14;
+        const ldsd* bc_row = fx ? win + F_AB + lane : fu ? win + WB_R + lane * 10 : win;
+        const int bc_str = fx ? 11 : 1;
+        const ldsd* bc_ct = fx ? win + WB_R + R_CT + lane : s.zero;  // C^T[j][r] at + 10 j
+        const ldsd* bc_k = fx ? win + F_K + lane : s.zero;           // K[i][r] at + 11 i
+        const ldsd* bc_g = lane < 14 ? win + WB_R + R_G + lane : s.zero;
+        const double mfx = fx ? 1.0 : 0.0;
+        double mu_[NU];
+    #pragma unroll
+        for (int i = 0; i < NU; ++i) mu_[i] = lane == NX + i ? 1.0 : 0.0;
+        const int bx = fx ? lane : 0;
+        const unsigned bc_st = lane < 14 ? lane * 11 + 10 : F_J;  // b~ rows (lanes < 10), k_ff rows (lanes 10..13)
+        ldsd* const bc_p = fx ? s.p + lane : s.junk;
         const int k = N - q;
         double off = *bc_g;
 #pragma unroll
-        for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * *bc_ct[j];
+        for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * bc_ct[10 * j];
         if (q == 0) {  // p_N = g_N + sum_j gamma_j C_j^T
             *bc_p = off;
             return;
         }
         // g~_u (uniform) and the per-lane offset of the chain
-        double gu[NU];
 #pragma unroll
-        for (int i = 0; i < NU; ++i) gu[i] = win[WB_R + R_G + NX + i] + s.bv[k * NU + i];
-#pragma unroll
-        for (int i = 0; i < NU; ++i) off += fx ? *bc_k[i] * gu[i] : mu_[i] * s.bv[k * NU + i];
+        for (int i = 0; i < NU; ++i) {
+            const double bv = s.bv[k * NU + i];
+            off += bc_k[11 * i] * (win[WB_R + R_G + NX + i] + bv) + mu_[i] * bv;
+        }
         double row[NX];
 #pragma unroll
         for (int l = 0; l < NX; ++l) row[l] = bc_row[l * bc_str];
@@ -543,6 +560,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double z = a0 + a1;
         *bc_p = z;
         // off the chain: k_ff, b~
+        const double cb = win[WB_R + R_C + bx], B0 = win[WB_R + 100 + bx], B1 = win[WB_R + 110 + bx];
+        const double B2 = win[WB_R + 120 + bx], B3 = win[WB_R + 130 + bx];
         const double z0 = rdlane(z, 10), z1 = rdlane(z, 11), z2 = rdlane(z, 12), z3 = rdlane(z, 13);
         const double i0 = win[F_L + 0], l10 = win[F_L + 1], i1 = win[F_L + 2], l20 = win[F_L + 3], l21 = win[F_L + 4];
         const double i2 = win[F_L + 5], l30 = win[F_L + 6], l31 = win[F_L + 7], l32 = win[F_L + 8], i3 = win[F_L + 9];
@@ -554,10 +573,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double k2 = (-w2 - l32 * k3) * i2;
         const double k1 = (-w1 - l21 * k2 - l31 * k3) * i1;
         const double k0 = (-w0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
-        const int bx = fx ? lane : 0;
-        const double bb = win[WB_R + R_C + bx] + win[WB_R + (NX + 0) * 10 + bx] * k0 + win[WB_R + (NX + 1) * 10 + bx] * k1 +
-                          win[WB_R + (NX + 2) * 10 + bx] * k2 + win[WB_R + (NX + 3) * 10 + bx] * k3;
-        const double fv = fx ? bb : mu_[0] * k0 + mu_[1] * k1 + mu_[2] * k2 + mu_[3] * k3;
+        const double bb = cb + B0 * k0 + B1 * k1 + B2 * k2 + B3 * k3;
+        const double fv = mfx * bb + mu_[0] * k0 + mu_[1] * k1 + mu_[2] * k2 + mu_[3] * k3;
         F[(size_t)k * FREC + bc_st] = fv;
         if (k < PD) *fs_at(k, bc_st) = fv;
     };
@@ -778,34 +795,37 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     };
 
     // ------------------------------------------------------------ IPM: sweeps over the record stream
-    auto stage = [&](auto Kc, int q) {
+    auto stage = [&](auto Kc, int q, int ln) {
         constexpr int K = decltype(Kc)::value;
-        if constexpr (K == 1) bf_stage(q);
-        else if constexpr (K == 3) bc_stage(q);
-        else fw_stage(Kc, q);
+        if constexpr (K == 1) bf_stage(q, ln);
+        else if constexpr (K == 3) bc_stage(q, ln);
+        else fw_stage(Kc, q, ln);
     };
     // one stream position: commit ring slot S (position q of this sweep), refill it with position qi
     // of a sweep of kind KI, run the stage
-    auto position = [&](auto Kc, auto KIc, auto Sc, int q, int qi, bool live) {
+    auto position = [&](auto Kc, auto KIc, auto Sc, int q, int qi, bool live, int ln) {
         constexpr int S = decltype(Sc)::value;
         commit(Kc, ring[S]);
         issue(KIc, ring[S], qi);
         wave_sync();
-        if (live) stage(Kc, q);
+        if (live) stage(Kc, q, ln);
         wave_sync();
     };
     auto sweep = [&](auto Kc) {
         constexpr int K = decltype(Kc)::value, KN = K == 4 ? 1 : K + 1;
+        // the stages' lane constants derive from an opaque copy of the lane id, so they are hoisted
+        // to this sweep's preheader and live only during the sweep (not across the whole solve)
+        const int ln = opaque(lane);
         int q0 = 0;
         for (; q0 < NP - PD; q0 += PD) {  // every position of these trips is a node
-            position(Kc, Kc, IC<0>{}, q0, q0 + PD, true);
-            position(Kc, Kc, IC<1>{}, q0 + 1, q0 + 1 + PD, true);
-            position(Kc, Kc, IC<2>{}, q0 + 2, q0 + 2 + PD, true);
+            position(Kc, Kc, IC<0>{}, q0, q0 + PD, true, ln);
+            position(Kc, Kc, IC<1>{}, q0 + 1, q0 + 1 + PD, true, ln);
+            position(Kc, Kc, IC<2>{}, q0 + 2, q0 + 2 + PD, true, ln);
         }
         // last trip: refill with the next sweep's first positions; tail positions compute nothing
-        position(Kc, IC<KN>{}, IC<0>{}, q0, 0, q0 < N1);
-        position(Kc, IC<KN>{}, IC<1>{}, q0 + 1, 1, q0 + 1 < N1);
-        position(Kc, IC<KN>{}, IC<2>{}, q0 + 2, 2, q0 + 2 < N1);
+        position(Kc, IC<KN>{}, IC<0>{}, q0, 0, q0 < N1, ln);
+        position(Kc, IC<KN>{}, IC<1>{}, q0 + 1, 1, q0 + 1 < N1, ln);
+        position(Kc, IC<KN>{}, IC<2>{}, q0 + 2, 2, q0 + 2 < N1, ln);
     };
 
     issue(IC<0>{}, ring[0], 0);
