@@ -126,6 +126,12 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+typedef unsigned u2 __attribute__((ext_vector_type(2)));
+// raw buffer store of one double: SGPR resource + 32-bit lane byte offset + uniform byte offset
+__device__ __forceinline__ void bst(double v, __amdgpu_buffer_rsrc_t r, unsigned vo, unsigned so) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, v), r, vo, so, 0);
+}
+
 // a copy of v the compiler cannot see through (blocks hoisting of what is derived from it)
 __device__ __forceinline__ int opaque(int v) {
     int r;
@@ -253,6 +259,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     ldsd* const win = s.win;
     const double* R = A.work + (size_t)b * qp_work_doubles(N);  // [N+1][REC] stage records
     double* F = A.work + (size_t)b * qp_work_doubles(N) + (size_t)N1 * REC;  // [N+1][FREC]
+    const __amdgpu_buffer_rsrc_t rsF = __builtin_amdgcn_make_buffer_rsrc(F, (short)0, N1 * FREC * 8, 0x00020000);
 
     // ------------------------------------------------------------ per-node constants into LDS
     for (int e = lane; e < N * NU; e += 64) {
@@ -361,34 +368,33 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     auto fs_at = [&](int k, int e) -> ldsd* { return e < F_FW ? s.fsave + k * F_FW + e : s.junk; };
 
     d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
-    auto bf_stage = [&](int q, const int lane) {
+    auto bf_stage = [&](auto Fc, int q, const int lane) {
+        constexpr bool FIRST = decltype(Fc)::value;  // q == 0: the terminal node
         const int g = lane >> 4, c = lane & 15;
         // Index bases with immediate offsets: a base is R_Z for an inactive lane, and the window is 0 from
-        // R_Z up to 384 in the factor sweep, so base + offset stays 0 there.
-        // og: G[4 st + g][c] (G = [A B c]; column 14 is c at R_C + k) at og01 + 4 st (st = 0, 1), og2
+        // R_Z up to 384 in the factor sweep, so base + offset stays 0 there.  Accumulator entries outside
+        // the 10 x 10 (+ column 14) blocks are finite garbage that only ever meets zero operands, so no
+        // operand is masked.
+        // G = [A B c] (column 14 is c at R_C + k): G[4 st + g][c] at og01 + 4 st (st = 0, 1), og2
         const int og01 = c < 15 ? c * 10 + g : R_Z, og2 = (c < 15 && g < 2) ? c * 10 + g + 8 : R_Z;
-        const bool pa2 = c < NX && g < 2, pa01 = c < NX;
         int h_i[4];
-        bool p14[4];
-    #pragma unroll
+#pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
             h_i[r] = (a < 14 && c < 14) ? R_H + tri14(lo, hi) : (a < 14 && c == 14) ? R_G + a : R_Z;
-            p14[r] = c == 14 && a < NX;
         }
-        // fold rows C^T[j][a]: rows a = g + 4 r at ct01 + 4 r + 10 j (r = 0, 1), ct2 + 10 j; column c at cc + 10 j
-        const int ct01 = R_CT + g, ct2 = g < 2 ? R_CT + g + 8 : R_Z, cc = c < NX ? R_CT + c : R_Z;
-        // closed loop: [A | c][a][c] at ab01 + 4 r, ab2; B[a][i] at bb01 + 4 r + 10 i, bb2 + 10 i
+        // fold operands: A = C[c][g] (g < 3), B = w_g C[c][g] (c < 10) | gamma_g (c = 14)
+        const int cgi = (c < NX && g < NS) ? R_CT + g * 10 + c : R_Z, gj = g < NS ? g : 0;
+        const double m14 = c == 14 ? 1.0 : 0.0, mg3 = g < NS ? 1.0 : 0.0;
+        // closed loop: [A | c][a][c] at ab01 + 4 r (r = 0, 1), ab2; A operand B[a = c][g] at bmi
         const bool xcol = c < NX || c == 14;           // columns of [P | p], [A | c], [K | k_ff]
         const int xo = c < NX ? c : 10;                // their column in the 11-wide factor-record rows
         const int ab01 = xcol ? (c < NX ? c : 14) * 10 + g : R_Z, ab2 = (xcol && g < 2) ? (c < NX ? c : 14) * 10 + g + 8 : R_Z;
-        const int bb01 = 100 + g, bb2 = g < 2 ? 108 + g : R_Z;
-        const bool ga = c < 14;                        // G_ab columns (the A operand of G_ab^T W)
-        const double m14 = c == 14 ? 1.0 : 0.0;
+        const int bmi = c < NX ? (NX + g) * 10 + c : R_Z;
         // box terms: rows 10..13 of M' live in r = 2 (groups 2, 3) and r = 3 (groups 0, 1)
         int bi[2];
         double bxm[2], bvm[2];
-    #pragma unroll
+#pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int a = g + 4 * (2 + h);
             const bool in = a >= NX && a < 14;
@@ -397,70 +403,61 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             bvm[h] = (in && c == 14) ? 1.0 : 0.0;
         }
         double mg[4];
-    #pragma unroll
+#pragma unroll
         for (int i = 0; i < 4; ++i) mg[i] = g == i ? 1.0 : 0.0;
-        // factor-record store offsets (F_J: junk)
+        // factor-record store offsets in bytes (F_J: junk)
         unsigned spc[3], sab[3];
-    #pragma unroll
+#pragma unroll
         for (int r = 0; r < 3; ++r) {
             const int a = g + 4 * r;
-            spc[r] = (c == 14 && a < NX) ? F_PC + a : F_J;
-            sab[r] = (xcol && a < NX) ? F_AB + a * 11 + xo : F_J;
+            spc[r] = 8u * ((c == 14 && a < NX) ? F_PC + a : F_J);
+            sab[r] = 8u * ((xcol && a < NX) ? F_AB + a * 11 + xo : F_J);
         }
-        const unsigned sk_ = xcol ? F_K + g * 11 + xo : F_J;
-        const unsigned sy_ = c < NX ? F_Y + g * 10 + c : F_J;
+        const unsigned sk_ = 8u * (xcol ? F_K + g * 11 + xo : F_J);
+        const unsigned sy_ = 8u * (c < NX ? F_Y + g * 10 + c : F_J);
+
         const int k = N - q;
-        // fold (rank 3, VALU): fold[r] = sum_j C[a][j] (w_j C[c][j] | gamma_j)
-        double fb[NS];
-#pragma unroll
-        for (int j = 0; j < NS; ++j) fb[j] = fma(s.fw[k * NS + j], win[cc + 10 * j], m14 * s.fg[k * NS + j]);
-        d4 fold;
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-            fold[r] = win[ct01 + 4 * r] * fb[0] + win[ct01 + 4 * r + 10] * fb[1] + win[ct01 + 4 * r + 20] * fb[2];
-        fold[2] = win[ct2] * fb[0] + win[ct2 + 10] * fb[1] + win[ct2 + 20] * fb[2];
-        fold[3] = 0.0;
-        if (q == 0) {  // [P_N | p_N] = [H_N | g_N] + fold
+        const double cg = win[cgi];
+        const double fb = mg3 * fma(s.fw[k * NS + gj], cg, m14 * s.fg[k * NS + gj]);
+        if constexpr (FIRST) {  // [P_N | p_N] = [H_N | g_N] + fold
+            d4 T;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
-                const int t = (a < NX && c < NX) ? R_H + tri10(lo, hi) : (a < NX && c == 14) ? R_G + a : R_Z;
-                Pa[r] = win[t] + fold[r];
+                T[r] = win[(a < NX && c < NX) ? R_H + tri10(lo, hi) : (a < NX && c == 14) ? R_G + a : R_Z];
             }
+            Pa = mfma(cg, fb, T);
             return;
         }
-        double* Fk = F + (size_t)k * FREC;
+        const unsigned sko = (unsigned)k * (FREC * 8u);
         // ---- W = P G (K = 10: k-steps 0..2); column 14 -> P c, then + p
         const double og0 = win[og01], og1 = win[og01 + 4], og2v = win[og2];
         d4 W = {0.0, 0.0, 0.0, 0.0};
-        W = mfma(pa01 ? Pa[0] : 0.0, og0, W);
-        W = mfma(pa01 ? Pa[1] : 0.0, og1, W);
-        W = mfma(pa2 ? Pa[2] : 0.0, og2v, W);
-        // ---- M' = G_ab^T W + [H | g] + fold + box terms (VALU part first, off the MFMA chain)
+        W = mfma(Pa[0], og0, W);
+        W = mfma(Pa[1], og1, W);
+        W = mfma(Pa[2], og2v, W);
+        __builtin_amdgcn_sched_barrier(0);  // the W chain goes first; the rest fills its latency
+        // ---- M' = G_ab^T W + [H | g] + C^T diag(w) [C | gamma] + box terms
         d4 M;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) M[r] = win[h_i[r]] + fold[r];
+        for (int r = 0; r < 4; ++r) M[r] = win[h_i[r]];
 #pragma unroll
         for (int h = 0; h < 2; ++h)
             M[2 + h] += bxm[h] * s.bd[k * NU + bi[h]] + bvm[h] * s.bv[k * NU + bi[h]];
-        // closed-loop operands (read now, used after the Cholesky)
-        double Ai[3], Bi[3][NU];
+        d4 Ab;  // closed-loop init [A | c] (rows 12..15: don't care)
+        Ab[0] = win[ab01];
+        Ab[1] = win[ab01 + 4];
+        Ab[2] = win[ab2];
+        Ab[3] = 0.0;
+        const double bm = win[bmi];
+        M = mfma(cg, fb, M);
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            Ai[r] = win[ab01 + 4 * r];
+        for (int r = 0; r < 3; ++r) bst(W[r], rsF, spc[r], sko);
 #pragma unroll
-            for (int i = 0; i < NU; ++i) Bi[r][i] = win[bb01 + 4 * r + 10 * i];
-        }
-        Ai[2] = win[ab2];
-#pragma unroll
-        for (int i = 0; i < NU; ++i) Bi[2][i] = win[bb2 + 10 * i];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) Fk[spc[r]] = W[r];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) W[r] += p14[r] ? Pa[r] : 0.0;
-        M = mfma(ga ? og0 : 0.0, W[0], M);
-        M = mfma(ga ? og1 : 0.0, W[1], M);
-        M = mfma(ga ? og2v : 0.0, W[2], M);
+        for (int r = 0; r < 4; ++r) W[r] = fma(m14, Pa[r], W[r]);
+        M = mfma(og0, W[0], M);
+        M = mfma(og1, W[1], M);
+        M = mfma(og2v, W[2], M);
         // ---- L = chol(R^): R^[i][j] = M'[10+i][10+j], read straight from the accumulator lanes
         const double r00 = rdlane(M[2], 42), r10 = rdlane(M[2], 58), r20 = rdlane(M[3], 10), r30 = rdlane(M[3], 26);
         const double r11 = rdlane(M[2], 59), r21 = rdlane(M[3], 11), r31 = rdlane(M[3], 27);
@@ -482,28 +479,27 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double y3 = (s3 - l30 * y0 - l31 * y1 - l32 * y2) * i3;
         const double yg = mg[0] * y0 + mg[1] * y1 + mg[2] * y2 + mg[3] * y3;
         Pa = mfma(-yg, yg, M);
+        __builtin_amdgcn_sched_barrier(0);  // hand P to the next stage before the off-chain work
         // ---- off the chain: [K | k_ff] = -L^-T [Y | w], [A~ | b~] = [A | c] + B [K | k_ff]
         const double k3 = -y3 * i3;
         const double k2 = (-y2 - l32 * k3) * i2;
         const double k1 = (-y1 - l21 * k2 - l31 * k3) * i1;
         const double k0 = (-y0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
         const double kg = mg[0] * k0 + mg[1] * k1 + mg[2] * k2 + mg[3] * k3;
-        double Ab[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) Ab[r] = Ai[r] + Bi[r][0] * k0 + Bi[r][1] * k1 + Bi[r][2] * k2 + Bi[r][3] * k3;
+        Ab = mfma(bm, kg, Ab);
         // ---- factor record (and its LDS copy for the first forward stages)
-#pragma unroll
-        for (int r = 0; r < 3; ++r) Fk[sab[r]] = Ab[r];
-        Fk[sk_] = kg;
-        Fk[sy_] = yg;
+        bst(kg, rsF, sk_, sko);
+        bst(yg, rsF, sy_, sko);
         {  // the (uniform) Cholesky factor: every lane stores the same 16 bytes, no lane selection
-            d2* Lp = (d2*)(Fk + F_L);
+            d2* Lp = (d2*)(F + (size_t)k * FREC + F_L);
             Lp[0] = d2{i0, l10}; Lp[1] = d2{i1, l20}; Lp[2] = d2{l21, i2}; Lp[3] = d2{l30, l31}; Lp[4] = d2{l32, i3};
         }
+#pragma unroll
+        for (int r = 0; r < 3; ++r) bst(Ab[r], rsF, sab[r], sko);
         if (k < PD) {
 #pragma unroll
-            for (int r = 0; r < 3; ++r) *fs_at(k, sab[r]) = Ab[r];
-            *fs_at(k, sk_) = kg;
+            for (int r = 0; r < 3; ++r) *fs_at(k, sab[r] / 8) = Ab[r];
+            *fs_at(k, sk_ / 8) = kg;
         }
     };
 
@@ -511,7 +507,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // v = P c + p_{k+1};  lane r < 10: p_k[r] = g~_x[r] + (K^T g~_u)[r] + (A~^T v)[r]   (the chain)
     //                     lane 10 + i: z_u[i] = g~_u[i] + (B^T v)[i]
     // then w = L^-1 z_u, k_ff = -L^-T w, b~ = c + B k_ff (off the chain).  g~ = g + fold | box.
-    auto bc_stage = [&](int q, const int lane) {
+    auto bc_stage = [&](auto Fc, int q, const int lane) {
+        constexpr bool FIRST = decltype(Fc)::value;
         const bool fx = lane < NX, fu = lane >= NX && lane < 14;
         const ldsd* bc_row = fx ? win + F_AB + lane : fu ? win + WB_R + lane * 10 : win;
         const int bc_str = fx ? 11 : 1;
@@ -529,7 +526,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         double off = *bc_g;
 #pragma unroll
         for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * bc_ct[10 * j];
-        if (q == 0) {  // p_N = g_N + sum_j gamma_j C_j^T
+        if constexpr (FIRST) {  // p_N = g_N + sum_j gamma_j C_j^T
             *bc_p = off;
             return;
         }
@@ -795,20 +792,20 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     };
 
     // ------------------------------------------------------------ IPM: sweeps over the record stream
-    auto stage = [&](auto Kc, int q, int ln) {
+    auto stage = [&](auto Kc, auto Fc, int q, const auto& ln) {
         constexpr int K = decltype(Kc)::value;
-        if constexpr (K == 1) bf_stage(q, ln);
-        else if constexpr (K == 3) bc_stage(q, ln);
+        if constexpr (K == 1) bf_stage(Fc, q, ln);
+        else if constexpr (K == 3) bc_stage(Fc, q, ln);
         else fw_stage(Kc, q, ln);
     };
     // one stream position: commit ring slot S (position q of this sweep), refill it with position qi
     // of a sweep of kind KI, run the stage
-    auto position = [&](auto Kc, auto KIc, auto Sc, int q, int qi, bool live, int ln) {
+    auto position = [&](auto Kc, auto KIc, auto Sc, auto Fc, int q, int qi, bool live, const auto& ln) {
         constexpr int S = decltype(Sc)::value;
         commit(Kc, ring[S]);
         issue(KIc, ring[S], qi);
         wave_sync();
-        if (live) stage(Kc, q, ln);
+        if (live) stage(Kc, Fc, q, ln);
         wave_sync();
     };
     auto sweep = [&](auto Kc) {
@@ -816,16 +813,28 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         // the stages' lane constants derive from an opaque copy of the lane id, so they are hoisted
         // to this sweep's preheader and live only during the sweep (not across the whole solve)
         const int ln = opaque(lane);
-        int q0 = 0;
-        for (; q0 < NP - PD; q0 += PD) {  // every position of these trips is a node
-            position(Kc, Kc, IC<0>{}, q0, q0 + PD, true, ln);
-            position(Kc, Kc, IC<1>{}, q0 + 1, q0 + 1 + PD, true, ln);
-            position(Kc, Kc, IC<2>{}, q0 + 2, q0 + 2 + PD, true, ln);
+        using T_ = IC<1>;
+        using F_ = IC<0>;
+        if (NP > PD) {
+            // first trip: position 0 is the sweep's first node (terminal node of a backward sweep)
+            position(Kc, Kc, IC<0>{}, T_{}, 0, PD, true, ln);
+            position(Kc, Kc, IC<1>{}, F_{}, 1, 1 + PD, true, ln);
+            position(Kc, Kc, IC<2>{}, F_{}, 2, 2 + PD, true, ln);
+            int q0 = PD;
+            for (; q0 < NP - PD; q0 += PD) {  // every position of these trips is a node
+                position(Kc, Kc, IC<0>{}, F_{}, q0, q0 + PD, true, ln);
+                position(Kc, Kc, IC<1>{}, F_{}, q0 + 1, q0 + 1 + PD, true, ln);
+                position(Kc, Kc, IC<2>{}, F_{}, q0 + 2, q0 + 2 + PD, true, ln);
+            }
+            // last trip: refill with the next sweep's first positions; tail positions compute nothing
+            position(Kc, IC<KN>{}, IC<0>{}, F_{}, q0, 0, q0 < N1, ln);
+            position(Kc, IC<KN>{}, IC<1>{}, F_{}, q0 + 1, 1, q0 + 1 < N1, ln);
+            position(Kc, IC<KN>{}, IC<2>{}, F_{}, q0 + 2, 2, q0 + 2 < N1, ln);
+        } else {  // N + 1 <= PD: a single trip
+            position(Kc, IC<KN>{}, IC<0>{}, T_{}, 0, 0, true, ln);
+            position(Kc, IC<KN>{}, IC<1>{}, F_{}, 1, 1, 1 < N1, ln);
+            position(Kc, IC<KN>{}, IC<2>{}, F_{}, 2, 2, 2 < N1, ln);
         }
-        // last trip: refill with the next sweep's first positions; tail positions compute nothing
-        position(Kc, IC<KN>{}, IC<0>{}, q0, 0, q0 < N1, ln);
-        position(Kc, IC<KN>{}, IC<1>{}, q0 + 1, 1, q0 + 1 < N1, ln);
-        position(Kc, IC<KN>{}, IC<2>{}, q0 + 2, 2, q0 + 2 < N1, ln);
     };
 
     issue(IC<0>{}, ring[0], 0);
