@@ -5,15 +5,15 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A "step" is one pass of the hot path over one batch: for every one of the B instances on this GPU,
-the SQP-RTI preparation phase over all N+1 shooting nodes (SDF forward + position-Jacobian,
-ERK4 + forward sensitivities, NONLINEAR_LS residual/Jacobian, h = [hfov, vfov, sdf] and its
-Jacobian) -- SURVEY.md §8(d)'s unit of work.  Inputs are resident in HBM before the timed region.
-value = instances x steps / time over ALL ranks (weak scaling: B instances per GPU).  The full RTI
-iteration (preparation + batched QP feedback phase + iterate update, i.e. one acados SQP_RTI
-solve) is timed in its own loop with the same barrier / max-over-ranks protocol and reported in
-"full_rti".  One process per GPU; instances never interact, so there is no data-path collective;
-RCCL broadcasts the packed weights once at init.
+A "step" is one SQP-RTI solve (acados SQP_RTI, sdf_nmpc/ocp.py:110) for every one of the B instances
+on this GPU: the preparation phase over all N+1 shooting nodes (SDF forward + position-Jacobian, ERK4 +
+forward sensitivities, NONLINEAR_LS residual/Jacobian, h = [hfov, vfov, sdf] and its Jacobian --
+SURVEY.md §8(d)'s unit of work), the feedback phase (the batched QP, rti_qp.hip) and the iterate
+update with u_0.  Every step starts from the same initial iterate (a device copy inside the timed
+region), so each one is a fresh solve of the same synthetic batch.  Inputs are resident in HBM before
+the timed region.  value = instances x steps / time over ALL ranks (weak scaling: B instances per GPU).
+The preparation phase alone is timed in its own loop ("prep").  One process per GPU; instances never
+interact, so there is no data-path collective; RCCL broadcasts the packed weights once at init.
 """
 import argparse
 import json
@@ -29,6 +29,11 @@ sys.path.insert(0, ROOT)
 SDF_FLOP_PER_ROW = 553_984      # fwd 138,456 MAC + d/dpos 138,536 MAC, x2
 SDF_FLOP_PER_INST = 98_304      # hoisted latent GEMVs per instance
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: Peak FP32 (matrix)
+FP64_PEAK_TFLOPS = 78.6         # AMD MI355X spec: FP64 vector = FP64 matrix (not in the guide's table)
+# QP algorithmic FLOP per node per IPM iteration (rti_qp.hip): factor stage
+# W = P G 1500 + M' = G_ab^T W 2100 + fold 330 + chol/solves 240 + Y^T Y 484 + A~ = A + B K 440 FMA,
+# two forward matvecs 2 x 170, corrector 270 FMA (5,704 FMA), ~200 FLOP of row updates
+QP_FLOP_PER_NODE_ITER = 11_608
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md: HBM3E peak (spec)
 
 
@@ -52,7 +57,8 @@ def main():
     ap.add_argument("--cpu-sample", type=int, default=64, help="instances in the CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--quiet", action="store_true")
-    ap.add_argument("--rti-steps", type=int, default=10, help="timed full-RTI steps (0: skip)")
+    ap.add_argument("--prep-steps", type=int, default=50, help="timed preparation-only steps (0: skip)")
+    ap.add_argument("--no-b1", action="store_true", help="skip the B=1 latency probe (profiling runs)")
     args = ap.parse_args()
 
     import torch
@@ -113,10 +119,14 @@ def main():
     u0 = torch.empty((B, 4), dtype=torch.float64, device=dev)
     qopts = _lib.qp_opts(quad)
 
-    def step():
+    x_init, u_init = bufs["x"].clone(), bufs["u"].clone()
+
+    def prep():  # preparation phase only
         _lib.linearize(ctx, net, model, B, N, np_, bufs)
 
-    def rti_step():  # one SQP-RTI solve: preparation, feedback (QP), iterate update + u_0
+    def step():  # one SQP-RTI solve from the initial iterate: preparation, feedback (QP), update + u_0
+        bufs["x"].copy_(x_init)
+        bufs["u"].copy_(u_init)
         _lib.linearize(ctx, net, model, B, N, np_, bufs)
         _lib.qp_solve(ctx, qopts, B, N, bufs)
         _lib.rti_apply(ctx, B, N, bufs["x"], bufs["u"], bufs["dx"], bufs["du"], u0)
@@ -143,8 +153,10 @@ def main():
     ms_per_step = elapsed / args.steps * 1e3
     total = args.global_batch if args.global_batch > 0 else world * B
     value = total * args.steps / elapsed
+    it = bufs["iters"].cpu().numpy()
+    st = bufs["status"].cpu().numpy()
 
-    # per-step latency distribution (each step synchronised on its own) and B=1 latency (config C2)
+    # control-step latency: each step synchronised on its own
     lat = []
     for _ in range(min(args.steps, 50)):
         s0 = time.perf_counter()
@@ -156,37 +168,53 @@ def main():
     # kernel durations by HIP events on the context stream (separate, untimed pass)
     ctx.enable_timing(True)
     ctx.reset_stats()
-    reps = max(10, min(args.steps, 50))
+    reps = max(5, min(args.steps, 20))
     for _ in range(reps):
         step()
-    kst = {k: ctx.kernel_stats(k) for k in ("sdf_hoist", "sdf_mlp", "linearize")}
+    names = ("sdf_hoist", "sdf_mlp", "linearize", "rti_qp_pack", "rti_qp", "rti_apply")
+    kst = {k: ctx.kernel_stats(k) for k in names}
     ctx.enable_timing(False)
     kms = {k: (v[0] / v[1] if v[1] else None) for k, v in kst.items()}
     rows = B * (N + 1)
     sdf_flop = rows * SDF_FLOP_PER_ROW
-    achieved = sdf_flop / (kms["sdf_mlp"] * 1e-3) / 1e12
+    sdf_tf = sdf_flop / (kms["sdf_mlp"] * 1e-3) / 1e12
     lin_b = B * lin_bytes_per_instance(N)
     lin_gbs = lin_b / (kms["linearize"] * 1e-3) / 1e9
+    qp_flop = float(it.sum()) * (N + 1) * QP_FLOP_PER_NODE_ITER
+    qp_tf = qp_flop / (kms["rti_qp"] * 1e-3) / 1e12
 
-    # full SQP-RTI iteration (preparation + QP + update); the iterate evolves step to step
-    full = None
-    if args.rti_steps > 0:
-        for _ in range(2):
-            rti_step()
-        rel = timed(rti_step, args.rti_steps)
-        ctx.enable_timing(True)
-        ctx.reset_stats()
-        rti_step()
-        qst = ctx.kernel_stats("rti_qp")
-        ctx.enable_timing(False)
-        it = bufs["iters"].cpu().numpy()
-        st = bufs["status"].cpu().numpy()
-        full = {"value": total * args.rti_steps / rel, "unit": "instance-RTI-solves/s (prep + QP + update)",
-                "ms_per_step": rel / args.rti_steps * 1e3, "steps": args.rti_steps,
-                "qp_kernel_ms": qst[0] / qst[1] if qst[1] else None,
-                "qp_iters_mean": float(it.mean()), "qp_iters_max": int(it.max()),
-                "qp_converged_frac": float((st == 0).mean()),
-                "qp": "batched Riccati IPM, one wavefront per instance (rti_qp.hip); tol 1e-8, max_iter 100"}
+    # preparation phase alone (acados rti_phase=1), same protocol
+    prep_out = None
+    if args.prep_steps > 0:
+        for _ in range(3):
+            prep()
+        pel = timed(prep, args.prep_steps)
+        prep_out = {"value": total * args.prep_steps / pel, "unit": "instance-RTI-preparations/s",
+                    "ms_per_step": pel / args.prep_steps * 1e3, "steps": args.prep_steps}
+
+    # B = 1, N = horizon: the single-instance control-step latency (BASELINE.json config C2)
+    lat1 = None
+    if rank == 0 and not args.no_b1:
+        b1 = {k: (v[:1].clone() if v.dim() > 0 and v.shape[0] == B else v) for k, v in bufs.items()}
+        b1["dt"] = bufs["dt"]
+        x1, u1_, u01 = b1["x"].clone(), b1["u"].clone(), torch.empty((1, 4), dtype=torch.float64, device=dev)
+
+        def step1():
+            b1["x"].copy_(x1)
+            b1["u"].copy_(u1_)
+            _lib.linearize(ctx, net, model, 1, N, np_, b1)
+            _lib.qp_solve(ctx, qopts, 1, N, b1)
+            _lib.rti_apply(ctx, 1, N, b1["x"], b1["u"], b1["dx"], b1["du"], u01)
+        for _ in range(5):
+            step1()
+        l1 = []
+        for _ in range(30):
+            torch.cuda.synchronize(dev)
+            s0 = time.perf_counter()
+            step1()
+            torch.cuda.synchronize(dev)
+            l1.append((time.perf_counter() - s0) * 1e3)
+        lat1 = float(np.median(l1))
 
     # traffic from the committed PMC profile of this same command (profiles/)
     traffic = None
@@ -196,7 +224,7 @@ def main():
             with open(pmc_path) as f:
                 pmc = json.load(f)
             if pmc.get("B") == B and pmc.get("N") == N and pmc.get("tile_rows") == args.tile_rows:
-                traffic = pmc["kernels"]["sdf_mlp"]["hbm_bytes_per_launch"]
+                traffic = {k: pmc["kernels"][k]["hbm_bytes_per_launch"] for k in ("rti_qp", "sdf_mlp")}
         except Exception:
             traffic = None
 
@@ -209,26 +237,31 @@ def main():
         S = min(args.cpu_sample, B)
         onet = O.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed=0))
         om = O.quad_model(cfg)
-        sub = {k: np.ascontiguousarray(prob[k][:S]) for k in ("x", "u", "p")}
-        O.linearize_batch(om, onet, sub["x"][:2], sub["u"][:2], sub["p"][:2], dt, nthreads=threads)  # warm
+        sub = {k: np.ascontiguousarray(prob[k][:S]) for k in ("x", "u", "p", "yref", "W", "yN", "WN")}
+        sub["dt"] = prob["dt"]
+
+        def cpu_rti(n, nth):  # one SQP-RTI solve of n instances on the host: preparation + QP
+            sl = {k: (v if k == "dt" else v[:n]) for k, v in sub.items()}
+            lin = O.linearize_batch(om, onet, sl["x"], sl["u"], sl["p"], dt, nthreads=nth)
+            return O.qp_ipm_batch(lin, sl, x0[:n], quad, nthreads=nth)
+        cpu_rti(2, threads)  # warm
         c0 = time.perf_counter()
-        O.linearize_batch(om, onet, sub["x"], sub["u"], sub["p"], dt, nthreads=threads)
+        cpu_rti(S, threads)
         cpu_s = time.perf_counter() - c0
         S1 = max(2, S // 16)
         c0 = time.perf_counter()
-        O.linearize_batch(om, onet, sub["x"][:S1], sub["u"][:S1], sub["p"][:S1], dt, nthreads=1)
+        cpu_rti(S1, 1)
         cpu1_s = time.perf_counter() - c0
-        cpu = {"value": S / cpu_s, "unit": "instance-RTI-steps/s (preparation phase)", "cores": threads,
-               "kind": "port",
-               "sample": f"{S} of the {B} instances x {N + 1} nodes, C oracle (oracle/oracle.c, fp32 MLP + fp64 "
-                         f"linearisation, OpenMP over rows); 1-thread rate on {S1} instances = "
-                         f"{S1 / cpu1_s:.1f}/s",
+        cpu = {"value": S / cpu_s, "unit": "instance-RTI-solves/s (prep + QP)", "cores": threads, "kind": "port",
+               "sample": f"{S} of the {B} instances x {N + 1} nodes: C oracle preparation (oracle/oracle.c, fp32 "
+                         f"MLP + fp64 linearisation) + structured Riccati IPM QP (oracle/qp_ipm.c), OpenMP over "
+                         f"instances; 1-thread rate on {S1} instances = {S1 / cpu1_s:.1f}/s",
                "value_1thread": S1 / cpu1_s}
 
     out = {
         "metric": "NMPC solves/sec at batch×N=1024×40 on 1/2/4/8 GPUs; p50 control-step latency",
         "value": value,
-        "unit": "instance-RTI-steps/s",
+        "unit": "instance-RTI-solves/s",
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -236,22 +269,28 @@ def main():
         "higher_is_better": True,
         "scaling": "strong" if args.global_batch > 0 else "weak",
         "vs_baseline": None,
-        "dtype": "f32 (SDF MLP, MFMA) + f64 (linearisation)",
+        "dtype": "f64 (QP, linearisation) + f32 (SDF MLP on MFMA)",
         "data": "synthetic (seeded x0/latent/waypoints, SIREN-init weights seed 0; real weights are LFS pointers)",
-        "config": {"workload": f"C3/C4: batch={B} instances per GPU x N={N}, RTI preparation phase "
-                               "(SDF fwd+d/dpos, ERK4+sens, NLS, h+J_h), 'att' model, default flags",
-                   "phase": "preparation (acados rti_phase=1 semantics); full RTI with the QP in full_rti",
+        "config": {"workload": f"C3/C4: batch={B} instances per GPU x N={N}, one SQP-RTI solve per step "
+                               "(preparation: SDF fwd+d/dpos, ERK4+sens, NLS, h+J_h; feedback: batched Riccati IPM "
+                               "QP to tol 1e-8; iterate update), 'att' model, default flags",
                    "global_batch": total, "horizon": N, "parallelism": f"instances sharded over {world} GPU(s)",
                    "tile_rows": args.tile_rows},
         "p50_step_ms": p50,
+        "p50_step_ms_b1": lat1,
+        "qp_iters_mean": float(it.mean()), "qp_iters_max": int(it.max()), "qp_converged_frac": float((st == 0).mean()),
         "kernel_ms": kms,
-        "roofline": {"bound": "mfma", "kernel": "sdf_mlp", "achieved": achieved, "peak": FP32_MFMA_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / FP32_MFMA_PEAK_TFLOPS, "traffic": traffic,
-                     "flop_per_launch": sdf_flop},
+        "roofline": {"bound": "mfma", "kernel": "rti_qp", "achieved": qp_tf, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": qp_tf / FP64_PEAK_TFLOPS,
+                     "traffic": traffic["rti_qp"] if traffic else None, "flop_per_launch": qp_flop,
+                     "note": "latency-bound serial Riccati recursion (one wavefront per instance); f64 peak"},
+        "roofline_sdf": {"bound": "mfma", "kernel": "sdf_mlp", "achieved": sdf_tf, "peak": FP32_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": sdf_tf / FP32_MFMA_PEAK_TFLOPS,
+                         "traffic": traffic["sdf_mlp"] if traffic else None, "flop_per_launch": sdf_flop},
         "roofline_linearize": {"bound": "hbm", "achieved": lin_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": lin_gbs / HBM_PEAK_GBS, "bytes_per_launch": lin_b},
         "cpu_baseline": cpu,
-        "full_rti": full,
+        "prep": prep_out,
     }
     if rank == 0:
         print(json.dumps(out))

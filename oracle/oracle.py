@@ -27,7 +27,7 @@ class Quad(C.Structure):
 
 def build(force=False):
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
-            os.path.getmtime(os.path.join(HERE, f)) for f in ("oracle.c", "sdf_net.inc", "Makefile")):
+            os.path.getmtime(os.path.join(HERE, f)) for f in ("oracle.c", "sdf_net.inc", "qp_ipm.c", "Makefile")):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB
 
@@ -54,6 +54,8 @@ def lib():
                                              P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d),
                                              P(d), P(d), P(f), C.c_int]
         _lib.orc_max_threads.restype = C.c_int
+        _lib.orc_qp_ipm_batch.argtypes = [C.c_int, C.c_int] + [P(d)] * 17 + [C.c_int, C.c_int, P(d), P(d), P(d),
+                                                                             P(C.c_int), P(C.c_int), P(d), C.c_int]
     return _lib
 
 
@@ -156,4 +158,28 @@ def linearize_batch(m, net, x, u, p, dt, nthreads=1):
                               _p(net.flat, C.c_float), B, N, p.shape[-1], _p(x, C.c_double), _p(u, C.c_double),
                               _p(p, C.c_double), _p(dt, C.c_double), *(_p(out[k], C.c_double) for k in
                               ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh")), _p(out["sdf"], C.c_float), nthreads)
+    return out
+
+
+QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", "W", "yNref", "WN")
+
+
+def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_scaling=True, nthreads=1):
+    """Structured Riccati IPM (qp_ipm.c) over a batch: the CPU restatement of the feedback-phase QP.
+
+    lin: linearisation outputs (xn, AB, y, Jy, yN, JyN, h, Jh) with a leading batch dimension;
+    prob: x, u, yref, W, yN (reference), WN, dt.  Returns dict(dx, du, slack, iters, status, res).
+    """
+    B, N = lin["xn"].shape[0], lin["xn"].shape[1]
+    arrs = dict(lin)
+    arrs.update(x=prob["x"], u=prob["u"], x0=x0, yref=prob["yref"], W=prob["W"], yNref=prob["yN"], WN=prob["WN"])
+    arrs = {k: np.ascontiguousarray(arrs[k], dtype=np.float64) for k in QP_IN}
+    dt = np.ascontiguousarray(prob["dt"], dtype=np.float64)
+    opts = np.concatenate([model.lbu, model.ubu, model.lh, model.uh, model.zl, model.Zl, [lm, tol]]).astype(np.float64)
+    out = dict(dx=np.zeros((B, N + 1, 10)), du=np.zeros((B, N, 4)), slack=np.zeros((B, N + 1, 3, 2)),
+               iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32), res=np.zeros((B, 2)))
+    d = C.c_double
+    lib().orc_qp_ipm_batch(B, N, *[_p(arrs[k], d) for k in QP_IN], _p(dt, d), _p(opts, d), max_iter,
+                           int(bool(cost_scaling)), _p(out["dx"], d), _p(out["du"], d), _p(out["slack"], d),
+                           _p(out["iters"], C.c_int), _p(out["status"], C.c_int), _p(out["res"], d), nthreads)
     return out

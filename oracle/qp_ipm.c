@@ -1,0 +1,420 @@
+/* Structured interior-point solver for the SQP-RTI feedback-phase QP -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of what acados' SQP_RTI hands to HPIPM (sdf_nmpc/ocp.py:110-120: NONLINEAR_LS +
+ * GAUSS_NEWTON cost with levenberg_marquardt, input boxes, soft h rows with L1/L2 slack penalties
+ * ocp.py:80-92, x_0 fixed) on the stage structure: a Mehrotra predictor-corrector whose Newton systems
+ * are LQRs solved by a backward Riccati recursion -- HPIPM's OCP-QP IPM family (HPIPM itself is an
+ * absent third-party dependency).  It is
+ *   - a second, independent checker of csrc/rti_qp.hip (same QP as oracle/qp_oracle.py's dense KKT
+ *     solver, different linear algebra), and
+ *   - the QP half of bench.py's cpu_baseline for the full-RTI metric (one C solve per instance, as
+ *     the reference runs one acados solver per process).
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg call it.
+ *
+ * QP of one instance (w_k = [dx_k; du_k]; s_k = dt_k for k < N with cost scaling, else 1; s_N = 1):
+ *   min  sum_{k<N} s_k 1/2 |J_y,k w_k + r_k|^2_{W_k} + lm/2 |w_k|^2 + s_N 1/2 |J_yN dx_N + r_N|^2_{W_N}
+ *        + lm/2 |dx_N|^2 + sum_{k<=N} s_k (zl.sl_k + Zl/2 sl_k^2 + zl.su_k + Zl/2 su_k^2)
+ *   s.t. dx_0 = x0 - xbar_0,  dx_{k+1} = A_k dx_k + B_k du_k + (xn_k - xbar_{k+1})
+ *        u_k + du_k in [lbu, ubu];  lh - sl_k <= h_k + C_k dx_k <= uh + su_k;  sl, su >= 0
+ * Inputs use the sdfnmpc_linearize layouts (include/sdfnmpc.h): AB [N][14][10] with AB[j][i] =
+ * d xn_i / d (x,u)_j, Jy [N][14][11] (Jy[j][a] = d y_a / d w_j), JyN [10][4], Jh [N+1][10][3].
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+enum { NX = 10, NU = 4, NS = 3, NW = 14 };
+
+typedef struct {
+    double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3], lm, tol;
+    int max_iter, cost_scaling;
+} qp_opts_c;
+
+typedef struct {                  /* stage k < N, or the terminal node k = N (x part only) */
+    double A[NX][NX], Bm[NX][NU], c[NX];
+    double H[NW][NW], g[NW];
+    double C[NS][NX], hl[NS], hu[NS];   /* soft rows: C dx + sl + hl >= 0, -C dx + su + hu >= 0 */
+    double dlo[NU], dup[NU];            /* box rows: du + dlo >= 0, -du + dup >= 0 */
+    double s;                           /* cost scaling s_k */
+} stage_t;
+
+/* in-place lower Cholesky of an n x n SPD matrix; 0 on success */
+static int chol(int n, double* a) {
+    for (int j = 0; j < n; ++j) {
+        double d = a[j * n + j];
+        for (int k = 0; k < j; ++k) d -= a[j * n + k] * a[j * n + k];
+        if (!(d > 0.0)) return 1;
+        d = sqrt(d);
+        a[j * n + j] = d;
+        for (int i = j + 1; i < n; ++i) {
+            double v = a[i * n + j];
+            for (int k = 0; k < j; ++k) v -= a[i * n + k] * a[j * n + k];
+            a[i * n + j] = v / d;
+        }
+    }
+    return 0;
+}
+/* x <- (L L^T)^-1 x */
+static void chol_solve(int n, const double* L, double* x) {
+    for (int i = 0; i < n; ++i) {
+        double v = x[i];
+        for (int k = 0; k < i; ++k) v -= L[i * n + k] * x[k];
+        x[i] = v / L[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+        double v = x[i];
+        for (int k = i + 1; k < n; ++k) v -= L[k * n + i] * x[k];
+        x[i] = v / L[i * n + i];
+    }
+}
+
+/* Rows (m = 8 N + 12 (N+1)), the order of rti_qp.hip: box rows 8 k + 4 up + i; soft rows
+ * 8 N + 12 k + 4 j + q with q = 0 (h lower), 1 (h upper), 2 (sl >= 0), 3 (su >= 0). */
+typedef struct {
+    int N, m;
+    const qp_opts_c* o;
+    stage_t* st;
+    double x0[NX];                /* dx_0 */
+    double *P, *p, *K, *kf;       /* Riccati workspace: (N+1) x NX x NX, (N+1) x NX, N x NU x NX, N x NU */
+} ipm_t;
+
+static void rows_at(const ipm_t* Q, const double* dx, const double* du, const double* sl, const double* su, double* v) {
+    const int N = Q->N;
+    for (int k = 0; k < N; ++k)
+        for (int i = 0; i < NU; ++i) {
+            v[8 * k + i] = du[k * NU + i] + Q->st[k].dlo[i];
+            v[8 * k + 4 + i] = -du[k * NU + i] + Q->st[k].dup[i];
+        }
+    for (int k = 0; k <= N; ++k)
+        for (int j = 0; j < NS; ++j) {
+            double cx = 0.0;
+            for (int l = 0; l < NX; ++l) cx += Q->st[k].C[j][l] * dx[k * NX + l];
+            const int r = 8 * N + 12 * k + 4 * j;
+            v[r] = cx + Q->st[k].hl[j] + sl[k * NS + j];
+            v[r + 1] = -cx + Q->st[k].hu[j] + su[k * NS + j];
+            v[r + 2] = sl[k * NS + j];
+            v[r + 3] = su[k * NS + j];
+        }
+}
+
+/* The Newton system as an LQR in the new iterate: Hessian H + D^T diag(sig) D, gradient g - D^T v.
+ * Soft slacks are eliminated per row pair (a rank-3 fold on the node's state block), box terms land
+ * on the input block.  Writes the solution (dx, du, sl, su); returns nonzero on a failed factorisation. */
+static int lqr(ipm_t* Q, const double* sig, const double* v, double* dx, double* du, double* sl, double* su) {
+    const int N = Q->N;
+    const qp_opts_c* o = Q->o;
+    for (int k = N; k >= 0; --k) {
+        const stage_t* S = &Q->st[k];
+        double Qx[NX * NX], qx[NX];
+        for (int a = 0; a < NX; ++a) {
+            for (int b = 0; b < NX; ++b) Qx[a * NX + b] = S->H[a][b];
+            qx[a] = S->g[a];
+        }
+        for (int j = 0; j < NS; ++j) {  /* eliminated slack pair */
+            const int r0 = 8 * N + 12 * k + 4 * j;
+            const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
+            const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
+            const double gl = zs - v[r0] - v[r0 + 2], gu = zs - v[r0 + 1] - v[r0 + 3];
+            const double fw = sig[r0] * (Hl - sig[r0]) / Hl + sig[r0 + 1] * (Hu - sig[r0 + 1]) / Hu;
+            const double fg = -(v[r0] + sig[r0] * gl / Hl) + (v[r0 + 1] + sig[r0 + 1] * gu / Hu);
+            for (int a = 0; a < NX; ++a) {
+                for (int b = 0; b < NX; ++b) Qx[a * NX + b] += fw * S->C[j][a] * S->C[j][b];
+                qx[a] += fg * S->C[j][a];
+            }
+        }
+        double* Pk = Q->P + (size_t)k * NX * NX;
+        double* pk = Q->p + (size_t)k * NX;
+        if (k == N) {
+            memcpy(Pk, Qx, sizeof Qx);
+            memcpy(pk, qx, sizeof qx);
+            continue;
+        }
+        const double* P1 = Q->P + (size_t)(k + 1) * NX * NX;
+        const double* p1 = Q->p + (size_t)(k + 1) * NX;
+        /* PA = P A, PB = P B, Pc = P c + p */
+        double PA[NX * NX], PB[NX * NU], Pc[NX];
+        for (int a = 0; a < NX; ++a) {
+            for (int b = 0; b < NX; ++b) {
+                double s = 0.0;
+                for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->A[l][b];
+                PA[a * NX + b] = s;
+            }
+            for (int b = 0; b < NU; ++b) {
+                double s = 0.0;
+                for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->Bm[l][b];
+                PB[a * NU + b] = s;
+            }
+            double s = p1[a];
+            for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->c[l];
+            Pc[a] = s;
+        }
+        double Rm[NU * NU], Sm[NU * NX], r[NU];
+        for (int i = 0; i < NU; ++i) {
+            for (int j = 0; j < NU; ++j) {
+                double s = S->H[NX + i][NX + j];
+                for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * PB[l * NU + j];
+                Rm[i * NU + j] = s;
+            }
+            Rm[i * NU + i] += sig[8 * k + i] + sig[8 * k + 4 + i];
+            for (int b = 0; b < NX; ++b) {
+                double s = S->H[NX + i][b];
+                for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * PA[l * NX + b];
+                Sm[i * NX + b] = s;
+            }
+            double s = S->g[NX + i] - v[8 * k + i] + v[8 * k + 4 + i];
+            for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * Pc[l];
+            r[i] = s;
+        }
+        if (chol(NU, Rm)) return 1;
+        double* Kk = Q->K + (size_t)k * NU * NX;
+        double* kf = Q->kf + (size_t)k * NU;
+        for (int b = 0; b < NX; ++b) {  /* K = -R^-1 S, column by column */
+            double col[NU];
+            for (int i = 0; i < NU; ++i) col[i] = Sm[i * NX + b];
+            chol_solve(NU, Rm, col);
+            for (int i = 0; i < NU; ++i) Kk[i * NX + b] = -col[i];
+        }
+        for (int i = 0; i < NU; ++i) kf[i] = r[i];
+        chol_solve(NU, Rm, kf);
+        for (int i = 0; i < NU; ++i) kf[i] = -kf[i];
+        /* P = Q + A^T P A + S^T K,  p = q + A^T (P c + p) + S^T k_ff */
+        for (int a = 0; a < NX; ++a) {
+            for (int b = 0; b < NX; ++b) {
+                double s = Qx[a * NX + b];
+                for (int l = 0; l < NX; ++l) s += S->A[l][a] * PA[l * NX + b];
+                for (int i = 0; i < NU; ++i) s += Sm[i * NX + a] * Kk[i * NX + b];
+                Pk[a * NX + b] = s;
+            }
+            double s = qx[a];
+            for (int l = 0; l < NX; ++l) s += S->A[l][a] * Pc[l];
+            for (int i = 0; i < NU; ++i) s += Sm[i * NX + a] * kf[i];
+            pk[a] = s;
+        }
+    }
+    /* forward: dx_0 fixed, du = K dx + k_ff, dx+ = A dx + B du + c; slacks from the eliminated rows */
+    memcpy(dx, Q->x0, sizeof(double) * NX);
+    for (int k = 0; k <= N; ++k) {
+        const stage_t* S = &Q->st[k];
+        const double* xk = dx + (size_t)k * NX;
+        for (int j = 0; j < NS; ++j) {
+            const int r0 = 8 * N + 12 * k + 4 * j;
+            const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
+            const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
+            const double gl = zs - v[r0] - v[r0 + 2], gu = zs - v[r0 + 1] - v[r0 + 3];
+            double cx = 0.0;
+            for (int l = 0; l < NX; ++l) cx += S->C[j][l] * xk[l];
+            sl[k * NS + j] = -(gl + sig[r0] * cx) / Hl;
+            su[k * NS + j] = -(gu - sig[r0 + 1] * cx) / Hu;
+        }
+        if (k == N) break;
+        const double* Kk = Q->K + (size_t)k * NU * NX;
+        const double* kf = Q->kf + (size_t)k * NU;
+        double* uk = du + (size_t)k * NU;
+        for (int i = 0; i < NU; ++i) {
+            double s = kf[i];
+            for (int l = 0; l < NX; ++l) s += Kk[i * NX + l] * xk[l];
+            uk[i] = s;
+        }
+        double* xn = dx + (size_t)(k + 1) * NX;
+        for (int a = 0; a < NX; ++a) {
+            double s = S->c[a];
+            for (int l = 0; l < NX; ++l) s += S->A[a][l] * xk[l];
+            for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * uk[i];
+            xn[a] = s;
+        }
+    }
+    return 0;
+}
+
+static double step_max(int m, const double* t, const double* l, const double* dt, const double* dl) {
+    double a = 1.0;
+    for (int r = 0; r < m; ++r) {
+        if (dt[r] < 0.0 && -t[r] / dt[r] < a) a = -t[r] / dt[r];
+        if (dl[r] < 0.0 && -l[r] / dl[r] < a) a = -l[r] / dl[r];
+    }
+    return a;
+}
+
+/* One instance.  Returns IPM iterations (status via *conv: 1 converged). */
+static int solve_one(int N, const double* xn, const double* AB, const double* y, const double* Jy, const double* yN,
+                     const double* JyN, const double* h, const double* Jh, const double* x, const double* u,
+                     const double* x0, const double* yref, const double* W, const double* yNref, const double* WN,
+                     const double* dtv, const qp_opts_c* o, double* dx, double* du, double* slack, int* conv,
+                     double* res) {
+    const int N1 = N + 1, m = 8 * N + 12 * N1;
+    ipm_t Q;
+    Q.N = N; Q.m = m; Q.o = o;
+    Q.st = (stage_t*)calloc((size_t)N1, sizeof(stage_t));
+    Q.P = (double*)malloc(sizeof(double) * (size_t)N1 * NX * NX);
+    Q.p = (double*)malloc(sizeof(double) * (size_t)N1 * NX);
+    Q.K = (double*)malloc(sizeof(double) * (size_t)N * NU * NX);
+    Q.kf = (double*)malloc(sizeof(double) * (size_t)N * NU);
+    double* buf = (double*)calloc((size_t)(12 * m + 4 * (N1 * NX + N * NU + 2 * N1 * NS)), sizeof(double));
+    double *t = buf, *lam = t + m, *sig = lam + m, *v = sig + m, *rv = v + m, *dta = rv + m, *dla = dta + m;
+    double *dtc = dla + m, *dlc = dtc + m, *rw = dlc + m;  /* rw: spare */
+    (void)rw;
+    double* zs = buf + 12 * m;
+    const int nz = N1 * NX + N * NU + 2 * N1 * NS;
+    double *zdx = zs, *zdu = zdx + N1 * NX, *zsl = zdu + N * NU, *zsu = zsl + N1 * NS;          /* iterate */
+    double *adx = zs + nz, *adu = adx + N1 * NX, *asl = adu + N * NU, *asu = asl + N1 * NS;     /* affine */
+    double *cdx = zs + 2 * nz, *cdu = cdx + N1 * NX, *csl = cdu + N * NU, *csu = csl + N1 * NS; /* corrector */
+
+    /* ---- stage data (the pack step of rti_qp.hip) */
+    for (int k = 0; k <= N; ++k) {
+        stage_t* S = &Q.st[k];
+        S->s = (o->cost_scaling && k < N) ? dtv[k] : 1.0;
+        for (int j = 0; j < NS; ++j) {
+            for (int l = 0; l < NX; ++l) S->C[j][l] = Jh[((size_t)k * NX + l) * NS + j];
+            S->hl[j] = h[(size_t)k * NS + j] - o->lh[j];
+            S->hu[j] = o->uh[j] - h[(size_t)k * NS + j];
+        }
+        if (k < N) {
+            const double* ab = AB + (size_t)k * NW * NX;
+            for (int i = 0; i < NX; ++i) {
+                for (int j = 0; j < NX; ++j) S->A[i][j] = ab[j * NX + i];
+                for (int j = 0; j < NU; ++j) S->Bm[i][j] = ab[(NX + j) * NX + i];
+                S->c[i] = xn[(size_t)k * NX + i] - x[(size_t)(k + 1) * NX + i];
+            }
+            const double* J = Jy + (size_t)k * NW * 11;
+            double Ws[11], r[11];
+            for (int a = 0; a < 11; ++a) {
+                Ws[a] = S->s * W[(size_t)k * 11 + a];
+                r[a] = y[(size_t)k * 11 + a] - yref[(size_t)k * 11 + a];
+            }
+            for (int i = 0; i < NW; ++i) {
+                double gs = 0.0;
+                for (int a = 0; a < 11; ++a) gs += J[i * 11 + a] * Ws[a] * r[a];
+                S->g[i] = gs;
+                for (int j = 0; j < NW; ++j) {
+                    double hs = 0.0;
+                    for (int a = 0; a < 11; ++a) hs += J[i * 11 + a] * Ws[a] * J[j * 11 + a];
+                    S->H[i][j] = hs + (i == j ? o->lm : 0.0);
+                }
+            }
+            for (int i = 0; i < NU; ++i) {
+                S->dlo[i] = u[(size_t)k * NU + i] - o->lbu[i];
+                S->dup[i] = o->ubu[i] - u[(size_t)k * NU + i];
+            }
+        } else {
+            for (int i = 0; i < NX; ++i) {
+                double gs = 0.0;
+                for (int a = 0; a < 4; ++a) gs += JyN[i * 4 + a] * WN[a] * (yN[a] - yNref[a]);
+                S->g[i] = gs;
+                for (int j = 0; j < NX; ++j) {
+                    double hs = 0.0;
+                    for (int a = 0; a < 4; ++a) hs += JyN[i * 4 + a] * WN[a] * JyN[j * 4 + a];
+                    S->H[i][j] = hs + (i == j ? o->lm : 0.0);
+                }
+            }
+        }
+    }
+    for (int i = 0; i < NX; ++i) Q.x0[i] = x0[i] - x[i];
+
+    /* ---- starting point: dynamics-feasible with du = sl = su = 0; t = max(row, 1), lambda = 3 */
+    memcpy(zdx, Q.x0, sizeof(double) * NX);
+    for (int k = 0; k < N; ++k)
+        for (int a = 0; a < NX; ++a) {
+            double s = Q.st[k].c[a];
+            for (int l = 0; l < NX; ++l) s += Q.st[k].A[a][l] * zdx[k * NX + l];
+            zdx[(k + 1) * NX + a] = s;
+        }
+    rows_at(&Q, zdx, zdu, zsl, zsu, rv);
+    double rp = 0.0, mu = 0.0;
+    for (int r = 0; r < m; ++r) {
+        t[r] = rv[r] > 1.0 ? rv[r] : 1.0;
+        lam[r] = 3.0;
+        if (fabs(rv[r] - t[r]) > rp) rp = fabs(rv[r] - t[r]);
+        mu += t[r] * lam[r];
+    }
+    mu /= m;
+    /* row constants d (rows at z = 0) for v = sig (t - d) */
+    double* d0 = (double*)calloc((size_t)m, sizeof(double));
+    {
+        double* zero = (double*)calloc((size_t)nz, sizeof(double));
+        rows_at(&Q, zero, zero + N1 * NX, zero + N1 * NX + N * NU, zero + N1 * NX + N * NU + N1 * NS, d0);
+        free(zero);
+    }
+    int it = 0, fail = 0;
+    while (!(mu < o->tol && rp < o->tol) && it < o->max_iter) {
+        /* predictor */
+        for (int r = 0; r < m; ++r) {
+            sig[r] = lam[r] / t[r];
+            v[r] = sig[r] * (t[r] - d0[r]);
+        }
+        if (lqr(&Q, sig, v, adx, adu, asl, asu)) { fail = 1; break; }
+        rows_at(&Q, adx, adu, asl, asu, rv);
+        for (int r = 0; r < m; ++r) {
+            dta[r] = rv[r] - t[r];
+            dla[r] = -sig[r] * dta[r] - lam[r];
+        }
+        const double aa = step_max(m, t, lam, dta, dla);
+        double mua = 0.0;
+        for (int r = 0; r < m; ++r) mua += (t[r] + aa * dta[r]) * (lam[r] + aa * dla[r]);
+        mua /= m;
+        const double sigmu = (mua / mu) * (mua / mu) * (mua / mu) * mu;
+        /* corrector */
+        for (int r = 0; r < m; ++r) v[r] = sig[r] * (t[r] - d0[r]) - (dta[r] * dla[r] - sigmu) / t[r];
+        if (lqr(&Q, sig, v, cdx, cdu, csl, csu)) { fail = 1; break; }
+        rows_at(&Q, cdx, cdu, csl, csu, rv);
+        for (int r = 0; r < m; ++r) {
+            dtc[r] = rv[r] - t[r];
+            dlc[r] = -sig[r] * dtc[r] - lam[r] - (dta[r] * dla[r] - sigmu) / t[r];
+        }
+        double al = 0.995 * step_max(m, t, lam, dtc, dlc);
+        if (al > 1.0) al = 1.0;
+        mu = 0.0;
+        for (int r = 0; r < m; ++r) {
+            t[r] += al * dtc[r];
+            lam[r] += al * dlc[r];
+            mu += t[r] * lam[r];
+        }
+        mu /= m;
+        for (int e = 0; e < nz; ++e) zs[e] += al * (zs[2 * nz + e] - zs[e]);
+        rp *= (1.0 - al);
+        ++it;
+    }
+    memcpy(dx, zdx, sizeof(double) * N1 * NX);
+    memcpy(du, zdu, sizeof(double) * N * NU);
+    if (slack)
+        for (int e = 0; e < N1 * NS; ++e) {
+            slack[2 * e] = zsl[e];
+            slack[2 * e + 1] = zsu[e];
+        }
+    *conv = !fail && mu < o->tol && rp < o->tol;
+    if (res) { res[0] = mu; res[1] = rp; }
+    free(d0); free(buf); free(Q.st); free(Q.P); free(Q.p); free(Q.K); free(Q.kf);
+    return it;
+}
+
+/* Batched entry point (OpenMP over instances).  opts: lbu 4, ubu 4, lh 3, uh 3, zl 3, Zl 3, lm, tol.
+ * status: 0 converged, 1 max_iter / failure (rti_qp.hip's convention). */
+void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const double* y, const double* Jy,
+                      const double* yN, const double* JyN, const double* h, const double* Jh, const double* x,
+                      const double* u, const double* x0, const double* yref, const double* W, const double* yNref,
+                      const double* WN, const double* dt, const double* opts, int max_iter, int cost_scaling,
+                      double* dx, double* du, double* slack, int* iters, int* status, double* res, int nthreads) {
+    qp_opts_c o;
+    memcpy(o.lbu, opts, 4 * sizeof(double));
+    memcpy(o.ubu, opts + 4, 4 * sizeof(double));
+    memcpy(o.lh, opts + 8, 3 * sizeof(double));
+    memcpy(o.uh, opts + 11, 3 * sizeof(double));
+    memcpy(o.zl, opts + 14, 3 * sizeof(double));
+    memcpy(o.Zl, opts + 17, 3 * sizeof(double));
+    o.lm = opts[20];
+    o.tol = opts[21];
+    o.max_iter = max_iter;
+    o.cost_scaling = cost_scaling;
+    const int N1 = N + 1;
+#pragma omp parallel for schedule(dynamic) num_threads(nthreads > 0 ? nthreads : 1)
+    for (int b = 0; b < B; ++b) {
+        int conv = 0;
+        iters[b] = solve_one(N, xn + (size_t)b * N * NX, AB + (size_t)b * N * NW * NX, y + (size_t)b * N * 11,
+                             Jy + (size_t)b * N * NW * 11, yN + (size_t)b * 4, JyN + (size_t)b * 40,
+                             h + (size_t)b * N1 * NS, Jh + (size_t)b * N1 * NX * NS, x + (size_t)b * N1 * NX,
+                             u + (size_t)b * N * NU, x0 + (size_t)b * NX, yref + (size_t)b * N * 11,
+                             W + (size_t)b * N * 11, yNref + (size_t)b * 4, WN + (size_t)b * 4, dt, &o,
+                             dx + (size_t)b * N1 * NX, du + (size_t)b * N * NU,
+                             slack ? slack + (size_t)b * N1 * NS * 2 : NULL, &conv, res ? res + 2 * b : NULL);
+        status[b] = conv ? 0 : 1;
+    }
+}

@@ -697,6 +697,7 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
     for (int i = 0; i < 4; ++i) { q.lbu[i] = o->lbu[i]; q.ubu[i] = o->ubu[i]; }
     for (int i = 0; i < 3; ++i) { q.lh[i] = o->lh[i]; q.uh[i] = o->uh[i]; q.zl[i] = o->zl[i]; q.Zl[i] = o->Zl[i]; }
     q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling;
+    HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(q, ctx->stream); }));
     HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
     return SDFNMPC_OK;
 }

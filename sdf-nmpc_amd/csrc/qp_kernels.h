@@ -50,7 +50,8 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
 }
 __host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N) * sizeof(double); }
 
-hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);
+hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s);  // stage records into the workspace
+hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);       // the IPM (after launch_rti_qp_pack)
 hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx, const double* du, double* u0,
                             hipStream_t s);
 

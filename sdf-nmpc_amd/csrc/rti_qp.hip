@@ -912,13 +912,16 @@ hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx
     return hipGetLastError();
 }
 
-hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s) {
+hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     hipLaunchKernelGGL(rti_qp_pack_kernel, dim3((unsigned)(a.B * (a.N + 1))), dim3(256), 0, s, a);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
+    return hipGetLastError();
+}
+
+hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
     const size_t lds = qp_lds_bytes(a.N);
-    e = hipFuncSetAttribute((const void*)rti_qp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute((const void*)rti_qp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(rti_qp_kernel, dim3(a.B), dim3(64), lds, s, a);
     return hipGetLastError();

@@ -92,3 +92,17 @@ def test_rti_apply(gpu_ctx):
     _lib.rti_apply(gpu_ctx, B, N, xd, ud, dxd, dud, u0)
     gpu_ctx.synchronize()
     assert torch.equal(xd.cpu(), x + dx) and torch.equal(ud.cpu(), u + du) and torch.equal(u0.cpu(), (u + du)[:, 0])
+
+
+@pytest.mark.parametrize("B,N,seed,noise", [(64, 40, 3, 0.05), (32, 20, 9, 0.5)])
+def test_qp_matches_riccati_oracle_batch(gpu_ctx, oracle_lib, cfg, B, N, seed, noise):
+    """A wider batch against the structured C IPM (oracle/qp_ipm.c), itself pinned to the dense IPM."""
+    prob, x0, t = setup(gpu_ctx, cfg, B, N, seed, x0_noise=noise)
+    model = solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL)
+    assert (t["status"].cpu().numpy() == 0).all()
+    lin = {k: t[k].cpu().numpy() for k in ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh")}
+    ref = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, nthreads=8)
+    assert (ref["status"] == 0).all()
+    np.testing.assert_allclose(t["du"].cpu().numpy(), ref["du"], rtol=0, atol=SOL_ATOL)
+    np.testing.assert_allclose(t["dx"].cpu().numpy(), ref["dx"], rtol=0, atol=SOL_ATOL)
+    np.testing.assert_allclose(t["slack"].cpu().numpy(), ref["slack"], rtol=0, atol=SOL_ATOL)

@@ -3,7 +3,7 @@
 FETCH_SIZE / WRITE_SIZE are kilobytes per dispatch (rocprofv3 derived metrics, TCC_EA0 requests).
 gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE counts half of the bytes of 16-B-per-lane
 streaming reads -> doubled; WRITE_SIZE is exact for 16-B stores, uncalibrated for narrower ones.
-Usage: python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> B N tile_rows
+Usage: python tools/pmc_summary.py <fetch_counter_collection.csv> <write_counter_collection.csv> B N tile_rows [csv_out_dir]
 """
 import collections
 import csv
@@ -36,6 +36,17 @@ def main():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     with open(os.path.join(root, "profiles", "pmc_summary.json"), "w") as f:
         json.dump(out, f, indent=1)
+    if len(sys.argv) > 6:  # per-kernel csv summaries (mean KB per dispatch) into this directory
+        for path, counter, tag in ((fetch, "FETCH_SIZE", "fetch"), (write, "WRITE_SIZE", "write")):
+            acc = collections.defaultdict(list)
+            with open(path) as f:
+                for row in csv.DictReader(f):
+                    if row["Counter_Name"] == counter:
+                        acc[row["Kernel_Name"].split("(")[0].replace("void ", "")].append(float(row["Counter_Value"]))
+            with open(os.path.join(sys.argv[6], f"pmc_{tag}_per_kernel.csv"), "w") as f:
+                f.write("kernel,counter,dispatches,mean_KB_per_dispatch\n")
+                for k, v in sorted(acc.items()):
+                    f.write(f'"{k}",{counter},{len(v)},{sum(v) / len(v):.3f}\n')
     for k, v in out["kernels"].items():
         print(f"{k:28s} fetch {v['fetch_bytes_per_launch'] / 1e6:10.3f} MB  write {v['write_bytes_per_launch'] / 1e6:10.3f} MB")
 

@@ -17,8 +17,8 @@ int main(int argc, char** argv) {
   q.lm=opt[20]; q.tol=opt[21]; q.max_iter=100; q.cost_scaling=1;
   hipMalloc(&q.dx,8*B*(N+1)*10); hipMalloc(&q.du,8*B*N*4); hipMalloc(&q.status,4*B); hipMalloc(&q.iters,4*B); hipMalloc(&q.res,16*B);
   hipMalloc(&q.work,8*B*qp_work_doubles(N)); hipMalloc(&q.stamps,8*B*16);
-  for (int r=0;r<3;++r) launch_rti_qp(q,0);
-  hipEvent_t a,b; hipEventCreate(&a); hipEventCreate(&b); hipEventRecord(a); launch_rti_qp(q,0); hipEventRecord(b); hipEventSynchronize(b);
+  for (int r=0;r<3;++r) { launch_rti_qp_pack(q,0); launch_rti_qp(q,0); }
+  hipEvent_t a,b; hipEventCreate(&a); hipEventCreate(&b); launch_rti_qp_pack(q,0); hipEventRecord(a); launch_rti_qp(q,0); hipEventRecord(b); hipEventSynchronize(b);
   float ms; hipEventElapsedTime(&ms,a,b);
   std::vector<double> st(B*16); hipMemcpy(st.data(),q.stamps,8*B*16,hipMemcpyDeviceToHost);
   std::vector<int> it(B); hipMemcpy(it.data(),q.iters,4*B,hipMemcpyDeviceToHost);
