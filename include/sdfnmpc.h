@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define SDFNMPC_ABI_VERSION 1
+#define SDFNMPC_ABI_VERSION 2
 
 enum {
     SDFNMPC_OK = 0,
@@ -96,6 +96,9 @@ typedef struct {
     int cost_scaling;      /* 1: stage cost and slack penalties x dt_k, terminal x 1 (acados default) */
     int max_iter;          /* qp_solver_iter_max (ocp.py:115) */
     double tol;            /* IPM stop: mean complementarity and max primal residual below tol */
+    int ny;                /* stage residuals: 11, or 12 with flags.sdf_cost (gen_model.py:65-66): the 12th,
+                              (1 - s/2)^4 of the flagged SDF value s = h[2], and its Jacobian
+                              -2 (1 - s/2)^3 J_h[2] are formed from h / J_h by the QP (yref, W: [B][N][ny]) */
 } sdfnmpc_qp_opts;
 
 /* Batched QP of the RTI feedback phase, built from sdfnmpc_linearize outputs. */
@@ -105,8 +108,8 @@ typedef struct {
     const double* x;     /* [B][N+1][10] iterate the QP was built at */
     const double* u;     /* [B][N][4] */
     const double* x0;    /* [B][10] measured state (Ocp.solve x0) */
-    const double* yref;  /* [B][N][11] stage references (Ocp.solve y[k]) */
-    const double* W;     /* [B][N][11] diagonal weights (Ocp.solve W[k], set as np.diag) */
+    const double* yref;  /* [B][N][ny] stage references (Ocp.solve y[k]) */
+    const double* W;     /* [B][N][ny] diagonal weights (Ocp.solve W[k], set as np.diag) */
     const double* yNref; /* [B][4] */
     const double* WN;    /* [B][4] */
     const double* dt;    /* [N] */

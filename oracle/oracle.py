@@ -54,8 +54,9 @@ def lib():
                                              P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d),
                                              P(d), P(d), P(f), C.c_int]
         _lib.orc_max_threads.restype = C.c_int
-        _lib.orc_qp_ipm_batch.argtypes = [C.c_int, C.c_int] + [P(d)] * 17 + [C.c_int, C.c_int, P(d), P(d), P(d),
-                                                                             P(C.c_int), P(C.c_int), P(d), C.c_int]
+        _lib.orc_qp_ipm_batch.argtypes = [C.c_int, C.c_int] + [P(d)] * 17 + [C.c_int, C.c_int, C.c_int, P(d), P(d),
+                                                                             P(d), P(C.c_int), P(C.c_int), P(d),
+                                                                             C.c_int]
     return _lib
 
 
@@ -179,7 +180,8 @@ def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_sca
     out = dict(dx=np.zeros((B, N + 1, 10)), du=np.zeros((B, N, 4)), slack=np.zeros((B, N + 1, 3, 2)),
                iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32), res=np.zeros((B, 2)))
     d = C.c_double
+    ny = arrs["W"].shape[-1]
     lib().orc_qp_ipm_batch(B, N, *[_p(arrs[k], d) for k in QP_IN], _p(dt, d), _p(opts, d), max_iter,
-                           int(bool(cost_scaling)), _p(out["dx"], d), _p(out["du"], d), _p(out["slack"], d),
+                           int(bool(cost_scaling)), ny, _p(out["dx"], d), _p(out["du"], d), _p(out["slack"], d),
                            _p(out["iters"], C.c_int), _p(out["status"], C.c_int), _p(out["res"], d), nthreads)
     return out

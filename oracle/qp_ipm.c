@@ -239,7 +239,7 @@ static double step_max(int m, const double* t, const double* l, const double* dt
 static int solve_one(int N, const double* xn, const double* AB, const double* y, const double* Jy, const double* yN,
                      const double* JyN, const double* h, const double* Jh, const double* x, const double* u,
                      const double* x0, const double* yref, const double* W, const double* yNref, const double* WN,
-                     const double* dtv, const qp_opts_c* o, double* dx, double* du, double* slack, int* conv,
+                     const double* dtv, const qp_opts_c* o, int ny, double* dx, double* du, double* slack, int* conv,
                      double* res) {
     const int N1 = N + 1, m = 8 * N + 12 * N1;
     ipm_t Q;
@@ -275,19 +275,25 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
                 for (int j = 0; j < NU; ++j) S->Bm[i][j] = ab[(NX + j) * NX + i];
                 S->c[i] = xn[(size_t)k * NX + i] - x[(size_t)(k + 1) * NX + i];
             }
-            const double* J = Jy + (size_t)k * NW * 11;
-            double Ws[11], r[11];
-            for (int a = 0; a < 11; ++a) {
-                Ws[a] = S->s * W[(size_t)k * 11 + a];
-                r[a] = y[(size_t)k * 11 + a] - yref[(size_t)k * 11 + a];
+            double J[NW][12], Ws[12], r[12];  /* J_y as [w][residual]; with ny = 12 the sdf cost row */
+            for (int i = 0; i < NW; ++i)
+                for (int a = 0; a < 11; ++a) J[i][a] = Jy[((size_t)k * NW + i) * 11 + a];
+            for (int a = 0; a < ny; ++a) {
+                Ws[a] = S->s * W[(size_t)k * ny + a];
+                r[a] = (a < 11 ? y[(size_t)k * 11 + a] : 0.0) - yref[(size_t)k * ny + a];
+            }
+            if (ny == 12) {  /* flags.sdf_cost (gen_model.py:65-66): (1 - s/2)^4 of s = h[2] */
+                const double tq = 1.0 - 0.5 * h[(size_t)k * NS + 2];
+                r[11] += tq * tq * tq * tq;
+                for (int i = 0; i < NW; ++i) J[i][11] = i < NX ? -2.0 * tq * tq * tq * Jh[((size_t)k * NX + i) * NS + 2] : 0.0;
             }
             for (int i = 0; i < NW; ++i) {
                 double gs = 0.0;
-                for (int a = 0; a < 11; ++a) gs += J[i * 11 + a] * Ws[a] * r[a];
+                for (int a = 0; a < ny; ++a) gs += J[i][a] * Ws[a] * r[a];
                 S->g[i] = gs;
                 for (int j = 0; j < NW; ++j) {
                     double hs = 0.0;
-                    for (int a = 0; a < 11; ++a) hs += J[i * 11 + a] * Ws[a] * J[j * 11 + a];
+                    for (int a = 0; a < ny; ++a) hs += J[i][a] * Ws[a] * J[j][a];
                     S->H[i][j] = hs + (i == j ? o->lm : 0.0);
                 }
             }
@@ -391,7 +397,7 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
 void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const double* y, const double* Jy,
                       const double* yN, const double* JyN, const double* h, const double* Jh, const double* x,
                       const double* u, const double* x0, const double* yref, const double* W, const double* yNref,
-                      const double* WN, const double* dt, const double* opts, int max_iter, int cost_scaling,
+                      const double* WN, const double* dt, const double* opts, int max_iter, int cost_scaling, int ny,
                       double* dx, double* du, double* slack, int* iters, int* status, double* res, int nthreads) {
     qp_opts_c o;
     memcpy(o.lbu, opts, 4 * sizeof(double));
@@ -411,8 +417,8 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
         iters[b] = solve_one(N, xn + (size_t)b * N * NX, AB + (size_t)b * N * NW * NX, y + (size_t)b * N * 11,
                              Jy + (size_t)b * N * NW * 11, yN + (size_t)b * 4, JyN + (size_t)b * 40,
                              h + (size_t)b * N1 * NS, Jh + (size_t)b * N1 * NX * NS, x + (size_t)b * N1 * NX,
-                             u + (size_t)b * N * NU, x0 + (size_t)b * NX, yref + (size_t)b * N * 11,
-                             W + (size_t)b * N * 11, yNref + (size_t)b * 4, WN + (size_t)b * 4, dt, &o,
+                             u + (size_t)b * N * NU, x0 + (size_t)b * NX, yref + (size_t)b * N * ny,
+                             W + (size_t)b * N * ny, yNref + (size_t)b * 4, WN + (size_t)b * 4, dt, &o, ny,
                              dx + (size_t)b * N1 * NX, du + (size_t)b * N * NU,
                              slack ? slack + (size_t)b * N1 * NS * 2 : NULL, &conv, res ? res + 2 * b : NULL);
         status[b] = conv ? 0 : 1;

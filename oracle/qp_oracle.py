@@ -33,7 +33,13 @@ def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=Non
     q["B"] = np.transpose(lin["AB"][:, 10:, :], (0, 2, 1))    # [N,10,4]
     q["c"] = lin["xn"] - xbar[1:]
     Jy = np.transpose(lin["Jy"], (0, 2, 1))                   # [N,11,14]
-    r = lin["y"] - yref
+    r = lin["y"] - yref[:, :11]
+    if W.shape[-1] == 12:  # flags.sdf_cost (gen_model.py:65-66): residual (1 - s/2)^4 of s = h[2]
+        t = 1.0 - 0.5 * lin["h"][:N, 2]
+        j = np.zeros((N, 1, 14))
+        j[:, 0, :10] = (-2.0 * t ** 3)[:, None] * lin["Jh"][:N, :, 2]
+        Jy = np.concatenate([Jy, j], axis=1)
+        r = np.concatenate([r, (t ** 4 - yref[:, 11])[:, None]], axis=1)
     q["H"] = np.einsum("kai,ka,kaj->kij", Jy, W, Jy) * s[:N, None, None] + lm * np.eye(14)
     q["g"] = np.einsum("kai,ka,ka->ki", Jy, W, r) * s[:N, None]
     JyN = lin["JyN"].T                                         # [4,10]

@@ -53,7 +53,7 @@ class LinArgsC(C.Structure):
 class QpOptsC(C.Structure):
     _fields_ = [("lbu", C.c_double * 4), ("ubu", C.c_double * 4), ("lh", C.c_double * 3), ("uh", C.c_double * 3),
                 ("zl", C.c_double * 3), ("Zl", C.c_double * 3), ("lm", C.c_double), ("cost_scaling", C.c_int),
-                ("max_iter", C.c_int), ("tol", C.c_double)]
+                ("max_iter", C.c_int), ("tol", C.c_double), ("ny", C.c_int)]
 
 
 QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", "W", "yNref", "WN", "dt")
@@ -107,7 +107,7 @@ def load():
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    if lib.sdfnmpc_abi_version() != 1:
+    if lib.sdfnmpc_abi_version() != 2:
         raise SdfnmpcError("libsdfnmpc.so ABI version mismatch")
     _lib = lib
     return lib
@@ -261,7 +261,7 @@ def qp_opts(model, lm=10.0, cost_scaling=True, max_iter=100, tol=1e-8) -> QpOpts
     """QP data of the 'att' model (model.Quad) + solver options (ocp.py:113-120 defaults)."""
     v = lambda a, n: (C.c_double * n)(*[float(x) for x in a])
     return QpOptsC(v(model.lbu, 4), v(model.ubu, 4), v(model.lh, 3), v(model.uh, 3), v(model.zl, 3),
-                   v(model.Zl, 3), float(lm), int(bool(cost_scaling)), int(max_iter), float(tol))
+                   v(model.Zl, 3), float(lm), int(bool(cost_scaling)), int(max_iter), float(tol), int(model.ny))
 
 
 def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):

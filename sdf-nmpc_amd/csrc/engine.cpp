@@ -679,6 +679,7 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
         return fail(SDFNMPC_E_ARG, "NULL array in sdfnmpc_qp_args");
     if (o->lm <= 0.0 || o->max_iter < 1 || !(o->tol > 0.0))
         return fail(SDFNMPC_E_ARG, "qp opts: lm > 0 (strict convexity), max_iter >= 1, tol > 0 required");
+    if (o->ny != 11 && o->ny != 12) return fail(SDFNMPC_E_ARG, "qp opts: ny must be 11 or 12 (sdf_cost)");
     if (qp_lds_bytes(a->N) > 160 * 1024) return fail(SDFNMPC_E_UNSUPPORTED, "horizon too long for the LDS-resident QP");
     ScopedDevice sd(ctx->device);
     HIPCHK(ctx->qpw.ensure((size_t)a->B * qp_work_doubles(a->N) * sizeof(double)));
@@ -696,7 +697,7 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
     q.work = (double*)ctx->qpw.p;
     for (int i = 0; i < 4; ++i) { q.lbu[i] = o->lbu[i]; q.ubu[i] = o->ubu[i]; }
     for (int i = 0; i < 3; ++i) { q.lh[i] = o->lh[i]; q.uh[i] = o->uh[i]; q.zl[i] = o->zl[i]; q.Zl[i] = o->Zl[i]; }
-    q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling;
+    q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling; q.ny = o->ny;
     HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(q, ctx->stream); }));
     HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
     return SDFNMPC_OK;

@@ -22,6 +22,7 @@ struct QpArgs {
     double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3];
     double lm, tol;
     int max_iter, cost_scaling;
+    int ny;  // 11, or 12 with the sdf cost residual (formed in the pack kernel from h[2], J_h[2])
 };
 
 constexpr int QP_REC = 300;   // stage record: [A B | c | g | C^T | H upper | 0]            (rti_qp.hip)

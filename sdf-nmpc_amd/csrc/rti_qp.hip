@@ -181,14 +181,28 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
     const int b = blockIdx.x / N1, k = blockIdx.x - b * N1;
     double* Rk = A.work + (size_t)b * qp_work_doubles(N) + (size_t)k * REC;
     const double* Jh = A.Jh + ((size_t)b * N1 + k) * 30;
-    __shared__ double Js[154], Ws[11], rs[11];
+    __shared__ double Js[14 * 12], Ws[12], rs[12];  // J_y as [14][ny], weights x s_k, residuals
+    const int ny = A.ny;
     if (k < N) {
         const size_t bk = (size_t)b * N + k;
         const double sk = A.cost_scaling ? A.dt[k] : 1.0;
-        for (int e = threadIdx.x; e < 154; e += 256) Js[e] = A.Jy[bk * 154 + e];
-        if (threadIdx.x < 11) {
-            Ws[threadIdx.x] = sk * A.W[bk * 11 + threadIdx.x];
-            rs[threadIdx.x] = A.y[bk * 11 + threadIdx.x] - A.yref[bk * 11 + threadIdx.x];
+        for (int e = threadIdx.x; e < 154; e += 256) Js[(e / 11) * ny + e % 11] = A.Jy[bk * 154 + e];
+        if (threadIdx.x < ny) {
+            const int i = threadIdx.x;
+            Ws[i] = sk * A.W[bk * ny + i];
+            double y;
+            if (i < 11) {
+                y = A.y[bk * 11 + i];
+            } else {  // sdf cost residual (gen_model.py:65-66): (1 - s/2)^4 of the flagged SDF value s = h[2]
+                const double t = 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2];
+                y = t * t * t * t;
+            }
+            rs[i] = y - A.yref[bk * ny + i];
+        }
+        if (ny == 12 && threadIdx.x < 14) {  // d/dw of the sdf cost: -2 (1 - s/2)^3 J_h[2] on the state part
+            const int a = threadIdx.x;
+            const double t = 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2];
+            Js[a * 12 + 11] = a < 10 ? -2.0 * t * t * t * Jh[a * 3 + 2] : 0.0;
         }
         __syncthreads();
         const double* AB = A.AB + bk * 140;
@@ -202,7 +216,7 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
                 v = xn[e - R_C] - xb1[e - R_C];
             } else if (e < R_CT) {
                 const int a = e - R_G;
-                for (int i = 0; i < 11; ++i) v += Js[a * 11 + i] * Ws[i] * rs[i];
+                for (int i = 0; i < ny; ++i) v += Js[a * ny + i] * Ws[i] * rs[i];
             } else if (e < R_H) {  // C^T: row j = d h_j / d x
                 const int q = e - R_CT, j = q / 10;
                 v = Jh[(q - 10 * j) * 3 + j];
@@ -210,7 +224,7 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
                 int q = e - R_H, a = 0;
                 while (q >= 14 - a) { q -= 14 - a; ++a; }
                 const int c = a + q;
-                for (int i = 0; i < 11; ++i) v += Js[a * 11 + i] * Ws[i] * Js[c * 11 + i];
+                for (int i = 0; i < ny; ++i) v += Js[a * ny + i] * Ws[i] * Js[c * ny + i];
                 v += (a == c ? A.lm : 0.0);
             }
             Rk[e] = v;

@@ -48,9 +48,11 @@ class Quad:
         fl = cfg.flags
         if cfg.mpc.model != "att":
             raise UnsupportedConfig(f"mpc.model '{cfg.mpc.model}': only 'att' is built (SURVEY.md §8: default model)")
-        if fl.get("recursive_feasibility") or fl.get("stability") or fl.get("sdf_cost"):
-            raise UnsupportedConfig("flags recursive_feasibility / stability / sdf_cost are not built "
-                                    "(SURVEY.md §8(f) rank 4)")
+        if fl.get("recursive_feasibility") or fl.get("stability"):
+            # the reference itself cannot build these: gen_model.py:74 asserts on a non-existent
+            # cfg.control_mode (AttributeError) -- SURVEY.md Appendix A
+            raise UnsupportedConfig("flags recursive_feasibility / stability are broken in the reference "
+                                    "(gen_model.py:74 reads cfg.control_mode, which Config does not define)")
         if not (fl.get("enable_sdf") and fl.get("sdf_constraint") and fl.get("vfov_constraint")):
             raise UnsupportedConfig("this build evaluates h = [hfov, vfov, sdf]: enable_sdf, sdf_constraint and "
                                     "vfov_constraint must be True")
@@ -75,7 +77,11 @@ class Quad:
         sf, sd = cfg.mpc.weights.slack_fov, cfg.mpc.weights.slack_df
         self.zl = np.array([sf[0], sf[0], sd[0]], dtype=float)
         self.Zl = np.array([sf[1], sf[1], sd[1]], dtype=float)
-        self.extra_W = np.array([])
+        # flags.sdf_cost: stage residual (1 - s/2)^4 of the flagged SDF value, weight 20
+        # (gen_model.py:65-66, base_model.py:add_cost_stage); the QP forms it from h[2], J_h[2]
+        self.sdf_cost = bool(fl.get("sdf_cost"))
+        self.extra_W = np.array([20.0]) if self.sdf_cost else np.array([])
+        self.ny = 11 + len(self.extra_W)
 
     # ---- input -> command maps (quad_rollpitchyawrate.py:37-45): batched over leading dims of x, u
     def _att(self, u):

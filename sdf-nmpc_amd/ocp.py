@@ -126,7 +126,7 @@ class Ocp:
         self.qp_opts = _lib.qp_opts(model, lm=float(cfg.mpc.lm_reg if lm is None else lm), max_iter=qp_iter_max,
                                     tol=qp_tol)
         f64 = dict(dtype=torch.float64, device=self.device)
-        sh = dict(x=(B, N + 1, 10), u=(B, N, 4), p=(B, N + 1, model.np), x0=(B, 10), yref=(B, N, 11), W=(B, N, 11),
+        sh = dict(x=(B, N + 1, 10), u=(B, N, 4), p=(B, N + 1, model.np), x0=(B, 10), yref=(B, N, model.ny), W=(B, N, model.ny),
                   yNref=(B, 4), WN=(B, 4), xn=(B, N, 10), AB=(B, N, 14, 10), y=(B, N, 11), Jy=(B, N, 14, 11),
                   yN=(B, 4), JyN=(B, 10, 4), h=(B, N + 1, 3), Jh=(B, N + 1, 10, 3), dx=(B, N + 1, 10), du=(B, N, 4),
                   slack=(B, N + 1, 3, 2), res=(B, 2), u0=(B, 4))

@@ -53,7 +53,7 @@ def rk4(x, u, dt, lim):
     return x + dt / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
 
 
-def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None):
+def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None, sdf_cost: bool = False):
     rng = np.random.default_rng(seed)
     lim = cfg.robot.limits
     L = int(cfg.nn.size_latent)
@@ -95,4 +95,7 @@ def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None):
     W = np.broadcast_to(Wrow, (B, N, 11)).copy()
     yN = yref[:, -1, :4].copy()
     WN = W[:, -1, :4].copy()
+    if sdf_cost:  # flags.sdf_cost: 12th residual (1 - s/2)^4 with reference 0 and weight 20 (model.Quad.extra_W)
+        yref = np.concatenate([yref, np.zeros((B, N, 1))], axis=-1)
+        W = np.concatenate([W, np.full((B, N, 1), 20.0)], axis=-1)
     return dict(x=x, u=u, p=p, dt=np.asarray(dt, float), yref=yref, W=W, yN=yN, WN=WN, x0=x0, latent=latent)

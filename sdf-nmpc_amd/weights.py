@@ -213,3 +213,13 @@ def from_torchscript(path: str) -> Tuple[NetSpec, Dict[str, np.ndarray]]:
     if not np.array_equal(sd["embed.dirs"], embedding_dirs(embed)):
         raise ValueError("unexpected embedding directions")
     return spec, {k: sd[k] for k, _ in spec.param_shapes()}
+
+
+if __name__ == "__main__":  # offline converter: python -m sdf_nmpc_amd.weights model.pt model.sdfw
+    import sys
+
+    if len(sys.argv) != 3:
+        raise SystemExit("usage: python -m sdf_nmpc_amd.weights <neural_df TorchScript .pt> <out .sdfw>")
+    _spec, _params = from_torchscript(sys.argv[1])
+    save(sys.argv[2], _spec, _params)
+    print(f"{sys.argv[2]}: {_spec} ({_spec.n_params()} parameters)")

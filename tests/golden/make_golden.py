@@ -21,6 +21,10 @@ What is pinned to what:
                           finite differences of it (derivatives).  CasADi/acados are not installed,
                           so this is the strongest pin available here.
   * grid_golden.npz    -- ocp.py:21-27 shooting grid (numpy linspace/hstack/diff, bit-exact target).
+  * ts_golden.npz      -- the state_dict layout (names, shapes, embedding buffers) and the w0 / max_df
+                          attributes of ``torch.jit.script(NeuralDF(...))`` -- what df_train.py saves and
+                          gen_model.py:32 loads -- pinning weights.from_torchscript (data only: no
+                          TorchScript archive, which would carry the reference's code, is committed).
   * params_golden.npz  -- the reference's own ``Nmpc.set_latent`` / ``Nmpc.set_ref`` /
                           ``Quad.formate_ref`` (controller.py:50-54,133-142, quad_rollpitchyawrate.py:
                           62-65) called unbound on small stand-in objects; ``Config`` from the
@@ -369,8 +373,23 @@ def params_golden():
     print("params_golden.npz", len(out))
 
 
+def ts_golden():
+    spec = W.DEFAULT_SPEC
+    net = ref_net(spec, W.siren_weights(spec, 0), torch.float32)
+    sm = torch.jit.script(net)
+    sd = sm.state_dict()
+    out = {"keys": np.array(list(sd.keys())), "w0": np.float64(sm.w0), "max_df": np.float64(sm.max_df)}
+    for k, v in sd.items():
+        out[f"shape/{k}"] = np.array(v.shape, dtype=np.int64)
+        if "embed" in k:  # the embedding buffers are data the loader checks
+            out[f"buf/{k}"] = v.detach().numpy()
+    np.savez_compressed(os.path.join(HERE, "ts_golden.npz"), **out)
+    print("ts_golden.npz", len(out))
+
+
 if __name__ == "__main__":
-    sdf_golden()
-    lin_golden()
-    grid_golden()
-    params_golden()
+    only = sys.argv[1:]
+    for name, fn in (("sdf", sdf_golden), ("lin", lin_golden), ("grid", grid_golden), ("params", params_golden),
+                     ("ts", ts_golden)):
+        if not only or name in only:
+            fn()

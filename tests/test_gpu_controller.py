@@ -12,6 +12,10 @@ from sdf_nmpc_amd.reference import Ref, yaw2quat
 pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("ignore:no SDF weights")]
 
 U0_ATOL = 2e-5   # fp32 SDF rows differ from the oracle's by ~1e-7 rel; the QP solutions agree to ~1e-6
+# flags.sdf_cost puts the fp32 SDF gradient (parity bar 1e-5 rel) into the Hessian
+# with weight 20 through J = -2 (1 - s/2)^3 ds/dx; the GPU-vs-oracle QP parity on IDENTICAL
+# linearisations stays at 1e-5 (tests/test_gpu_qp.py::test_qp_sdf_cost_matches_riccati_oracle)
+U0_ATOL_SDF_COST = 1e-4
 
 
 def scenario(n, rng):
@@ -56,15 +60,16 @@ def oracle_u0(n, x0, oracle_lib):
     return np.array(u0)
 
 
-@pytest.mark.parametrize("B", [1, 3])
-def test_nmpc_rti_step_matches_oracle(oracle_lib, B):
-    n = Nmpc(Config(), batch=B)
+@pytest.mark.parametrize("B,sdf_cost", [(1, False), (3, False), (3, True)])
+def test_nmpc_rti_step_matches_oracle(oracle_lib, B, sdf_cost):
+    n = Nmpc(Config(flags__sdf_cost=sdf_cost), batch=B)
+    assert n.model.ny == (12 if sdf_cost else 11) and n.W.shape[-1] == n.model.ny
     x0 = scenario(n, np.random.default_rng(10 + B))
     n.set_x0(x0)
     assert n.solve() == 0
     assert (n.ocp.status == 0).all()
     u = np.atleast_2d(n.get_u())
-    np.testing.assert_allclose(u, oracle_u0(n, x0, oracle_lib), rtol=0, atol=U0_ATOL)
+    np.testing.assert_allclose(u, oracle_u0(n, x0, oracle_lib), rtol=0, atol=U0_ATOL_SDF_COST if sdf_cost else U0_ATOL)
     assert (u >= n.model.lbu - 1e-9).all() and (u <= n.model.ubu + 1e-9).all()
     x, uu = n.get_matrices()
     np.testing.assert_array_equal(np.atleast_2d(u), np.atleast_2d(uu[..., 0, :]))

@@ -11,10 +11,10 @@ QP_TOL = 1e-10          # IPM stop tolerance used for the parity runs
 SOL_ATOL = 1e-5         # |du - du_ref|, |dx - dx_ref| (IPM solutions agree to ~sqrt(mu) level)
 
 
-def setup(gpu_ctx, cfg, B, N, seed, x0_noise=0.05):
+def setup(gpu_ctx, cfg, B, N, seed, x0_noise=0.05, sdf_cost=False):
     import torch
     dev = torch.device("cuda", gpu_ctx.device)
-    prob = synth.make_problem(cfg, B, N, seed=seed)
+    prob = synth.make_problem(cfg, B, N, seed=seed, sdf_cost=sdf_cost)
     rng = np.random.default_rng(seed)
     x0 = prob["x"][:, 0] + rng.normal(0, x0_noise, (B, 10))
     t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
@@ -33,8 +33,11 @@ def setup(gpu_ctx, cfg, B, N, seed, x0_noise=0.05):
     return prob, x0, t
 
 
-def solve(gpu_ctx, cfg, t, B, N, **kw):
-    model = Quad(cfg)
+def solve(gpu_ctx, cfg, t, B, N, sdf_cost=False, **kw):
+    import copy
+    c = copy.deepcopy(cfg)
+    c.flags["sdf_cost"] = sdf_cost
+    model = Quad(c)
     _lib.qp_solve(gpu_ctx, _lib.qp_opts(model, **kw), B, N, t)
     gpu_ctx.synchronize()
     return model
@@ -106,3 +109,20 @@ def test_qp_matches_riccati_oracle_batch(gpu_ctx, oracle_lib, cfg, B, N, seed, n
     np.testing.assert_allclose(t["du"].cpu().numpy(), ref["du"], rtol=0, atol=SOL_ATOL)
     np.testing.assert_allclose(t["dx"].cpu().numpy(), ref["dx"], rtol=0, atol=SOL_ATOL)
     np.testing.assert_allclose(t["slack"].cpu().numpy(), ref["slack"], rtol=0, atol=SOL_ATOL)
+
+
+def test_qp_sdf_cost_matches_riccati_oracle(gpu_ctx, oracle_lib, cfg):
+    """flags.sdf_cost: the 12th residual (1 - s/2)^4 formed by the pack kernel from h[2], J_h[2]."""
+    B, N = 16, 40
+    prob, x0, t = setup(gpu_ctx, cfg, B, N, 21, x0_noise=0.2, sdf_cost=True)
+    model = solve(gpu_ctx, cfg, t, B, N, sdf_cost=True, tol=QP_TOL)
+    assert model.ny == 12 and (t["status"].cpu().numpy() == 0).all()
+    lin = {k: t[k].cpu().numpy() for k in ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh")}
+    ref = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, nthreads=8)
+    assert (ref["status"] == 0).all()
+    np.testing.assert_allclose(t["du"].cpu().numpy(), ref["du"], rtol=0, atol=SOL_ATOL)
+    np.testing.assert_allclose(t["dx"].cpu().numpy(), ref["dx"], rtol=0, atol=SOL_ATOL)
+    # and the residual changes the solution (the term is live)
+    _, _, t2 = setup(gpu_ctx, cfg, B, N, 21, x0_noise=0.2)
+    solve(gpu_ctx, cfg, t2, B, N, tol=QP_TOL)
+    assert np.abs(t2["du"].cpu().numpy() - ref["du"]).max() > 1e-6

@@ -15,19 +15,29 @@ from sdf_nmpc_amd.model import Quad
 SOL_ATOL = 1e-6   # both IPMs stopped at tol 1e-10: solutions agree to ~sqrt(mu)
 
 
-def _instance_set(oracle_lib, cfg, B, N, seed, noise):
-    prob = synth.make_problem(cfg, B, N, seed=seed)
+def _with_flags(cfg, **flags):
+    import copy
+    c = copy.deepcopy(cfg)
+    for k, v in flags.items():
+        c.flags[k] = v
+    return c
+
+
+def _instance_set(oracle_lib, cfg, B, N, seed, noise, sdf_cost=False):
+    prob = synth.make_problem(cfg, B, N, seed=seed, sdf_cost=sdf_cost)
     x0 = prob["x"][:, 0] + np.random.default_rng(seed).normal(0, noise, (B, 10))
     net = oracle_lib.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
     lin = oracle_lib.linearize_batch(oracle_lib.quad_model(cfg), net, prob["x"], prob["u"], prob["p"], prob["dt"])
     return prob, x0, lin
 
 
-@pytest.mark.parametrize("B,N,seed,noise", [(3, 20, 1, 0.05), (2, 40, 2, 0.05), (2, 12, 7, 0.5)])
-def test_riccati_ipm_matches_dense_ipm(oracle_lib, cfg, B, N, seed, noise):
+@pytest.mark.parametrize("B,N,seed,noise,sdf_cost", [(3, 20, 1, 0.05, False), (2, 40, 2, 0.05, False),
+                                                     (2, 12, 7, 0.5, False), (2, 20, 4, 0.2, True)])
+def test_riccati_ipm_matches_dense_ipm(oracle_lib, cfg, B, N, seed, noise, sdf_cost):
     import qp_oracle
-    model = Quad(cfg)
-    prob, x0, lin = _instance_set(oracle_lib, cfg, B, N, seed, noise)
+    model = Quad(_with_flags(cfg, sdf_cost=sdf_cost))
+    assert model.ny == (12 if sdf_cost else 11)
+    prob, x0, lin = _instance_set(oracle_lib, cfg, B, N, seed, noise, sdf_cost)
     r = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=1e-10)
     assert (r["status"] == 0).all()
     for b in range(B):
