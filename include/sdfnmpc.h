@@ -121,6 +121,43 @@ typedef struct {
     double* res;         /* [B][2] optional: (mean complementarity, max primal residual) */
 } sdfnmpc_qp_args;
 
+/* Batched reference / parameter packing: RefGen (ref_gen.py:17-130) ->
+ * formate_ref (quad_rollpitchyawrate.py:62-65) -> Nmpc.set_ref / set_latent / set_sdf_flag
+ * (controller.py:45-54,133-142) for B instances x (N+1) nodes on the device. */
+typedef struct {
+    int mode;              /* 0 gen_ref_list_wps, 1 gen_ref_joystick, 2 from_x0, -1 latent / flag only */
+    int yaw_mode;          /* path samples: 0 identity, 1 'ref', 2 'align', 3 x0 quaternion ('curent', sic) */
+    int st_enable;         /* ref.stop_and_turn.enable */
+    int st_mode;           /* stop-and-turn yaw: 0 current, 1 'topic', 2 'align' */
+    double st_dang;        /* ref.stop_and_turn.dang_min */
+    double align_off;      /* ref.align_yaw_offset */
+    double dmin;           /* ref.yaw_align_dmin */
+    double vref, wzref;    /* ref.vref, ref.wzref */
+    double T;              /* mpc.T */
+    double B_p_C[3], B_R_C[9]; /* sensor extrinsics (config.py) */
+} sdfnmpc_ref_opts;
+
+typedef struct {
+    int B, N, np, ny;      /* np = 17 + latent size; ny = 11 or 12 (sdf_cost) */
+    int n_wp;              /* waypoints per instance (mode 0), <= 32 */
+    int L;                 /* latent size (when latent != NULL) */
+    const double* x0;      /* [B][x0_stride] current state */
+    int x0_stride;
+    const double* wp_p;    /* [B][n_wp][3] (mode 0) */
+    const double* wp_q;    /* [B][n_wp][4] (mode 0) */
+    const double* vw;      /* [B][4] (vx, vy, vz, wz) in [-1, 1] (mode 1) */
+    const double* wrow;    /* [ny] the W row formate_ref builds from the caller's weight set */
+    const double* latent;  /* [B][L] or NULL (then W_p_Bo / W_R_Bo are ignored) */
+    const double* W_p_Bo;  /* [B][3] body position at image time */
+    const double* W_R_Bo;  /* [B][9] body attitude at image time, row-major */
+    const double* flag;    /* [B] sdf flag or NULL */
+    double* p;             /* [B][N+1][np] OCP parameters */
+    double* yref;          /* [B][N][ny] */
+    double* W;             /* [B][N][ny] */
+    double* yNref;         /* [B][4] */
+    double* WN;            /* [B][4] */
+} sdfnmpc_ref_args;
+
 int sdfnmpc_abi_version(void);
 const char* sdfnmpc_last_error(void);
 
@@ -128,6 +165,8 @@ const char* sdfnmpc_last_error(void);
 int sdfnmpc_ctx_create(int device, void* hip_stream /* NULL: create a non-blocking stream */, sdfnmpc_ctx** out);
 void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx);
 int sdfnmpc_ctx_set_stream(sdfnmpc_ctx* ctx, void* hip_stream);
+/* launch on the legacy null stream (handle 0, e.g. PyTorch's default stream) */
+int sdfnmpc_ctx_use_null_stream(sdfnmpc_ctx* ctx);
 void* sdfnmpc_ctx_stream(sdfnmpc_ctx* ctx);
 int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx);
 /* rows per SDF workgroup: 32 (2 workgroups / CU) or 64 (1 workgroup / CU); default 32 */
@@ -169,6 +208,9 @@ int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* opts, const sdfnmp
 /* x[B][N+1][10] += dx, u[B][N][4] += du, u0[B][4] = u[:, 0] (u0 may be NULL) */
 int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, const double* dx, const double* du,
                       double* u0);
+
+/* ---- batched reference / parameter packing into the OCP device buffers (sdfnmpc_ref_args) ---- */
+int sdfnmpc_pack_refs(sdfnmpc_ctx* ctx, const sdfnmpc_ref_opts* opts, const sdfnmpc_ref_args* args);
 
 /* ---- shooting grid (host, bit-exact numpy.linspace/diff semantics of ocp.py:21-27) ---- */
 int sdfnmpc_shooting_grid(int N, double T, int uniform, int nb_short_nodes, double dt_short, double* nodes,

@@ -22,11 +22,11 @@ L4C_PATH = os.path.join(LIB_DIR, "libsdf_l4c.so")
 # exported symbols declared in include/sdfnmpc.h (checked by tests/test_abi.py)
 SYMBOLS = [
     "sdfnmpc_abi_version", "sdfnmpc_last_error", "sdfnmpc_ctx_create", "sdfnmpc_ctx_destroy",
-    "sdfnmpc_ctx_set_stream", "sdfnmpc_ctx_stream", "sdfnmpc_ctx_synchronize", "sdfnmpc_ctx_set_tile_rows",
+    "sdfnmpc_ctx_set_stream", "sdfnmpc_ctx_use_null_stream", "sdfnmpc_ctx_stream", "sdfnmpc_ctx_synchronize", "sdfnmpc_ctx_set_tile_rows",
     "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
-    "sdfnmpc_linearize", "sdfnmpc_shooting_grid", "sdfnmpc_qp_solve", "sdfnmpc_rti_apply",
+    "sdfnmpc_linearize", "sdfnmpc_shooting_grid", "sdfnmpc_qp_solve", "sdfnmpc_rti_apply", "sdfnmpc_pack_refs",
 ]
 L4C_SYMBOLS = [
     f"{p}sdf_l4c{s}" for p in ("", "jac_", "adj1_")
@@ -54,6 +54,22 @@ class QpOptsC(C.Structure):
     _fields_ = [("lbu", C.c_double * 4), ("ubu", C.c_double * 4), ("lh", C.c_double * 3), ("uh", C.c_double * 3),
                 ("zl", C.c_double * 3), ("Zl", C.c_double * 3), ("lm", C.c_double), ("cost_scaling", C.c_int),
                 ("max_iter", C.c_int), ("tol", C.c_double), ("ny", C.c_int)]
+
+
+class RefOptsC(C.Structure):
+    _fields_ = [("mode", C.c_int), ("yaw_mode", C.c_int), ("st_enable", C.c_int), ("st_mode", C.c_int),
+                ("st_dang", C.c_double), ("align_off", C.c_double), ("dmin", C.c_double), ("vref", C.c_double),
+                ("wzref", C.c_double), ("T", C.c_double), ("B_p_C", C.c_double * 3), ("B_R_C", C.c_double * 9)]
+
+
+REF_IN = ("wp_p", "wp_q", "vw", "wrow", "latent", "W_p_Bo", "W_R_Bo", "flag")
+REF_OUT = ("p", "yref", "W", "yNref", "WN")
+
+
+class RefArgsC(C.Structure):
+    _fields_ = [("B", C.c_int), ("N", C.c_int), ("np", C.c_int), ("ny", C.c_int), ("n_wp", C.c_int),
+                ("L", C.c_int), ("x0", C.c_void_p), ("x0_stride", C.c_int)] + [
+        (n, C.c_void_p) for n in REF_IN + REF_OUT]
 
 
 QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", "W", "yNref", "WN", "dt")
@@ -84,6 +100,7 @@ def load():
         "sdfnmpc_ctx_create": (i, [i, vp, P(vp)]),
         "sdfnmpc_ctx_destroy": (None, [vp]),
         "sdfnmpc_ctx_set_stream": (i, [vp, vp]),
+        "sdfnmpc_ctx_use_null_stream": (i, [vp]),
         "sdfnmpc_ctx_stream": (vp, [vp]),
         "sdfnmpc_ctx_synchronize": (i, [vp]),
         "sdfnmpc_ctx_set_tile_rows": (i, [vp, i]),
@@ -103,6 +120,7 @@ def load():
         "sdfnmpc_shooting_grid": (i, [i, d, i, i, d, P(d), P(d)]),
         "sdfnmpc_qp_solve": (i, [vp, P(QpOptsC), P(QpArgsC)]),
         "sdfnmpc_rti_apply": (i, [vp, i, i, vp, vp, vp, vp, vp]),
+        "sdfnmpc_pack_refs": (i, [vp, P(RefOptsC), P(RefArgsC)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -137,10 +155,14 @@ class Context:
     """One HIP device + stream (sdfnmpc_ctx)."""
 
     def __init__(self, device: int = 0, stream=None, tile_rows: int = 32):
+        """stream: None -> a private non-blocking stream; a HIP stream handle (int) -> that stream, where
+        0 is the legacy null stream (PyTorch's default stream), so the kernels are ordered with torch's."""
         lib = load()
         h = C.c_void_p()
-        _check(lib.sdfnmpc_ctx_create(device, stream, C.byref(h)))
+        _check(lib.sdfnmpc_ctx_create(device, stream or None, C.byref(h)))
         self.h = h
+        if stream is not None and int(stream) == 0:
+            _check(lib.sdfnmpc_ctx_use_null_stream(h))
         self.device = device
         self.set_tile_rows(tile_rows)
 
@@ -148,7 +170,10 @@ class Context:
         _check(load().sdfnmpc_ctx_set_tile_rows(self.h, rows))
 
     def set_stream(self, stream):
-        _check(load().sdfnmpc_ctx_set_stream(self.h, stream))
+        if stream is not None and int(stream) == 0:
+            _check(load().sdfnmpc_ctx_use_null_stream(self.h))
+        else:
+            _check(load().sdfnmpc_ctx_set_stream(self.h, stream))
 
     def synchronize(self):
         _check(load().sdfnmpc_ctx_synchronize(self.h))
@@ -280,3 +305,24 @@ def shooting_grid(N: int, T: float, uniform=True, nb_short_nodes=2, dt_short=0.0
     _check(load().sdfnmpc_shooting_grid(N, T, int(bool(uniform)), nb_short_nodes, dt_short, nodes.ctypes.data_as(P),
                                         dt.ctypes.data_as(P)))
     return nodes, dt
+
+
+def ref_opts(cfg, mode: int) -> RefOptsC:
+    """RefGen knobs of a config (ref_gen.py) for sdfnmpc_pack_refs; mode 0 waypoints, 1 joystick, 2 from_x0,
+    -1 latent / flag only."""
+    r = cfg.ref
+    ym = str(r.yaw_mode)
+    yaw_mode = {"ref": 1, "align": 2, "curent": 3}.get(ym, 0)  # 'current' / 'zero': identity (ref_gen.py:12, sic)
+    st_mode = {"topic": 1, "align": 2}.get(ym, 0)
+    v = lambda a, n: (C.c_double * n)(*[float(x) for x in np.asarray(a, dtype=float).ravel()])
+    return RefOptsC(int(mode), yaw_mode, int(bool(r.stop_and_turn.enable)), st_mode, float(r.stop_and_turn.dang_min),
+                    float(r.align_yaw_offset), float(r.yaw_align_dmin), float(r.vref), float(r.wzref), float(cfg.mpc.T),
+                    v(cfg.sensor.B_p_C, 3), v(cfg.sensor.B_R_C, 9))
+
+
+def pack_refs(ctx: Context, opts: RefOptsC, B: int, N: int, np_: int, ny: int, bufs: dict, n_wp: int = 0, L: int = 0):
+    """Enqueue sdfnmpc_pack_refs.  bufs: device tensors named as sdfnmpc_ref_args (x0 [B][stride])."""
+    x0 = bufs.get("x0")
+    stride = int(x0.shape[-1]) if x0 is not None else 0
+    a = RefArgsC(B, N, np_, ny, n_wp, L, _ptr(x0), stride, *[_ptr(bufs.get(k)) for k in REF_IN + REF_OUT])
+    _check(load().sdfnmpc_pack_refs(ctx.h, C.byref(opts), C.byref(a)))

@@ -51,6 +51,7 @@ class Nmpc:
     def reset(self):
         """Reset internal matrices to default values (controller.py:35-44)."""
         m = self.model
+        self._dev_params = False
         self.x0 = None
         self.p = np.zeros(self._shape(self.N + 1, m.np))
         self.y = np.zeros(self._shape(self.N, m.ny))
@@ -65,11 +66,13 @@ class Nmpc:
     def set_sdf_flag(self, flag):
         """Enable/disable the sdf constraint (controller.py:47-49); flag: scalar or [B]."""
         f = np.asarray(flag, dtype=float)
+        self._dev_params = False
         self.p[..., self.cfg.mpc.p_idx.flag] = f[..., None] if f.ndim else f
 
     def set_latent(self, latent, W_p_Bo, W_R_Bo):
         """Latent and camera pose at the time of the image (controller.py:52-56), batched over a leading dim."""
         idx = self.cfg.mpc.p_idx
+        self._dev_params = False
         W_R_Bo = np.asarray(W_R_Bo, dtype=float)
         W_p_Co = W_R_Bo @ np.asarray(self.cfg.sensor.B_p_C, dtype=float).ravel() + W_p_Bo
         W_R_Co = (W_R_Bo @ np.asarray(self.cfg.sensor.B_R_C, dtype=float)).reshape(W_R_Bo.shape[:-2] + (9,))
@@ -96,7 +99,10 @@ class Nmpc:
         """One SQP-RTI iteration for every instance (controller.py:74-83)."""
         try:
             self.ocp.shift(self.cfg.mpc.shift)
-            self.ocp.solve(self.x0, self.y, self.yN, self.W, self.WN, self.p)
+            if self._dev_params:  # references / parameters live in the device buffers (gen_refs_device)
+                self.ocp.solve(self.x0, None, None, None, None, None)
+            else:
+                self.ocp.solve(self.x0, self.y, self.yN, self.W, self.WN, self.p)
             self.fail_count = 0
         except Exception as e:  # same contract as the reference: report, count, keep running
             print("solver failed:", e)
@@ -147,10 +153,80 @@ class Nmpc:
         df, _ = self.ocp.net.eval_host(np.concatenate([Co_p_B, pk[:, idx.latent:]], axis=1), want_grad=False)
         return df[:1] if self.B == 1 else df[:, None]
 
+    # ---- device-side parameter packing (csrc/ref_pack.hip)
+    def _dev(self, a, dtype=None):
+        import torch
+        return torch.as_tensor(np.array(a, dtype=np.float64, order="C"), device=self.ocp.device)
+
+    def _to_device(self):
+        """First switch to the device path: upload the host parameters once."""
+        if not self._dev_params:
+            m = self.model
+            for name, v, shape in (("p", self.p, (self.N + 1, m.np)), ("yref", self.y, (self.N, m.ny)),
+                                   ("W", self.W, (self.N, m.ny)), ("yNref", self.yN, (m.nyN,)),
+                                   ("WN", self.WN, (m.nyN,))):
+                self.ocp._put(name, v, shape)
+
+    def gen_refs_device(self, mode="wps", wps=None, vw=None, weights=None):
+        """RefGen + formate_ref + set_ref for every instance and node in one kernel launch, written straight
+        into the OCP's device buffers (p[:, :, q_d], y, W, yN, WN).
+
+        mode 'wps': ``RefGen.gen_ref_list_wps`` (ref_gen.py:25-99) from x0 (``set_x0``) through the
+        waypoints ``wps = (p [B][n][3], q [B][n][4])`` (or a list of ``Waypoint`` for B = 1); 'joystick':
+        ``gen_ref_joystick(vw)`` (ref_gen.py:101-130), vw [B][4]; 'hover': ``from_x0`` (ref_gen.py:17-23).
+        ``weights`` is the weight set formate_ref reads (e.g. ``Ref(cfg).W_on``); the joystick mode zeroes
+        its position weights as gen_ref_joystick does.  Until a host setter is called again, ``solve``
+        uses the device buffers for y, W, yN, WN and p.
+        """
+        from . import _lib
+        from .ref_gen import weight_row
+        from .reference import Ref
+        if self.x0 is None:
+            raise ValueError("set_x0 before gen_refs_device (the references start at the current state)")
+        Bn = max(self.B, 1)
+        ws = weights if weights is not None else Ref(self.cfg).W_on
+        wrow = weight_row(self.model, ws)
+        code = {"wps": 0, "joystick": 1, "hover": 2}[mode]
+        if code == 1:
+            wrow[:3] = 0.0  # ref.Wp = [0, 0, 0] (ref_gen.py:122)
+        bufs = self.ocp.bufs
+        args = {"x0": self._dev(np.reshape(self.x0, (Bn, -1))), "wrow": self._dev(wrow)}
+        n_wp = 0
+        if code == 0:
+            if isinstance(wps, (list, tuple)) and len(wps) and hasattr(wps[0], "p"):
+                wps = (np.array([w.p for w in wps])[None], np.array([w.q for w in wps])[None])
+            wp_p = np.reshape(np.asarray(wps[0], float), (Bn, -1, 3))
+            wp_q = np.reshape(np.asarray(wps[1], float), (Bn, -1, 4))
+            n_wp = wp_p.shape[1]
+            args.update(wp_p=self._dev(wp_p), wp_q=self._dev(wp_q))
+        elif code == 1:
+            args["vw"] = self._dev(np.reshape(np.asarray(vw, float), (Bn, 4)))
+        for k in ("p", "W", "WN"):
+            args[k] = bufs[k]
+        args["yref"], args["yNref"] = bufs["yref"], bufs["yNref"]
+        self._to_device()
+        _lib.pack_refs(self.ocp.ctx, _lib.ref_opts(self.cfg, code), Bn, self.N, self.model.np, self.model.ny, args,
+                       n_wp=n_wp)
+        self._dev_params = True
+
+    def set_latent_device(self, latent, W_p_Bo, W_R_Bo, flag=None):
+        """set_latent (+ set_sdf_flag) on the device buffers for every instance (controller.py:45-54)."""
+        from . import _lib
+        Bn = max(self.B, 1)
+        self._to_device()
+        L = int(self.cfg.nn.size_latent)
+        args = {"latent": self._dev(np.reshape(latent, (Bn, L))), "W_p_Bo": self._dev(np.reshape(W_p_Bo, (Bn, 3))),
+                "W_R_Bo": self._dev(np.reshape(W_R_Bo, (Bn, 9))), "p": self.ocp.bufs["p"]}
+        if flag is not None:
+            args["flag"] = self._dev(np.broadcast_to(np.asarray(flag, float), (Bn,)))
+        _lib.pack_refs(self.ocp.ctx, _lib.ref_opts(self.cfg, -1), Bn, self.N, self.model.np, self.model.ny, args, L=L)
+        self._dev_params = True
+
     def set_ref(self, ref, k, b=None):
         """y, W and q_d of node k from a reference object (controller.py:136-142); b selects one instance
         of a batch (None: all)."""
         sel = () if self.B == 1 else (slice(None),) if b is None else (b,)
+        self._dev_params = False
         self.p[sel + (k, self.cfg.mpc.p_idx.q_d)] = ref.q
         y, W = self.model.formate_ref(ref)
         if k < self.N:

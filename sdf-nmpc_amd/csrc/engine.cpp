@@ -18,6 +18,7 @@
 #include "../../include/sdfnmpc.h"
 #include "lin_kernels.h"
 #include "qp_kernels.h"
+#include "ref_kernels.h"
 #include "sdf_kernels.h"
 
 using namespace sdfn;
@@ -165,6 +166,21 @@ extern "C" void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx) {
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;  // device buffers are freed by their destructors, on ctx->device
+}
+
+// The legacy default (null) stream: PyTorch's default stream has the handle 0, which
+// sdfnmpc_ctx_create / _set_stream read as "create a private stream"; this call makes the context
+// launch on the null stream itself, so its kernels are ordered with the framework's default-stream work.
+extern "C" int sdfnmpc_ctx_use_null_stream(sdfnmpc_ctx* ctx) {
+    if (!ctx) return fail(SDFNMPC_E_ARG, "ctx is NULL");
+    ScopedDevice sd(ctx->device);
+    if (ctx->own_stream) {
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        (void)hipStreamDestroy(ctx->stream);
+        ctx->own_stream = false;
+    }
+    ctx->stream = nullptr;
+    return SDFNMPC_OK;
 }
 
 extern "C" int sdfnmpc_ctx_set_stream(sdfnmpc_ctx* ctx, void* stream) {
@@ -700,6 +716,33 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
     q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling; q.ny = o->ny;
     HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(q, ctx->stream); }));
     HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_pack_refs(sdfnmpc_ctx* ctx, const sdfnmpc_ref_opts* o, const sdfnmpc_ref_args* a) {
+    if (!ctx || !o || !a) return fail(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_pack_refs");
+    if (a->B < 0 || a->N < 1 || a->np < 17 || (a->ny != 11 && a->ny != 12) || !a->p)
+        return fail(SDFNMPC_E_ARG, "pack_refs: bad B / N / np / ny or NULL p");
+    if (o->mode < -1 || o->mode > 2) return fail(SDFNMPC_E_ARG, "pack_refs: mode must be -1..2");
+    if (o->mode >= 0 && (!a->x0 || a->x0_stride < 7 || !a->wrow || !a->yref || !a->W || !a->yNref || !a->WN))
+        return fail(SDFNMPC_E_ARG, "pack_refs: x0 (stride >= 7), wrow and the reference outputs are required");
+    if (o->mode == 0 && (a->n_wp < 1 || a->n_wp > RP_MAX_WP || !a->wp_p || !a->wp_q))
+        return fail(SDFNMPC_E_ARG, "pack_refs: mode 0 needs 1..32 waypoints (wp_p, wp_q)");
+    if (o->mode == 1 && !a->vw) return fail(SDFNMPC_E_ARG, "pack_refs: mode 1 needs vw");
+    if (a->latent && (!a->W_p_Bo || !a->W_R_Bo || a->L < 1 || 17 + a->L > a->np))
+        return fail(SDFNMPC_E_ARG, "pack_refs: latent needs W_p_Bo, W_R_Bo and 17 + L <= np");
+    ScopedDevice sd(ctx->device);
+    RefPackArgs r{};
+    r.B = a->B; r.N = a->N; r.np_ = a->np; r.ny = a->ny; r.n_wp = a->n_wp; r.L = a->L;
+    r.mode = o->mode; r.yaw_mode = o->yaw_mode; r.st_enable = o->st_enable; r.st_mode = o->st_mode;
+    r.st_dang = o->st_dang; r.align_off = o->align_off; r.dmin = o->dmin; r.vref = o->vref; r.wzref = o->wzref;
+    r.T = o->T;
+    for (int i = 0; i < 3; ++i) r.B_p_C[i] = o->B_p_C[i];
+    for (int i = 0; i < 9; ++i) r.B_R_C[i] = o->B_R_C[i];
+    r.x0 = a->x0; r.x0_stride = a->x0_stride; r.wp_p = a->wp_p; r.wp_q = a->wp_q; r.vw = a->vw; r.wrow = a->wrow;
+    r.latent = a->latent; r.W_p_Bo = a->W_p_Bo; r.W_R_Bo = a->W_R_Bo; r.flag = a->flag;
+    r.p = a->p; r.yref = a->yref; r.W = a->W; r.yNref = a->yNref; r.WN = a->WN;
+    HIPCHK(timed(ctx, "ref_pack", [&] { return launch_ref_pack(r, ctx->stream); }));
     return SDFNMPC_OK;
 }
 

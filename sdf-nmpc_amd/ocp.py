@@ -170,14 +170,13 @@ class Ocp:
             u[:, : self.N - k] = u[:, k: self.N].clone()
 
     def solve(self, x0, y, yN, W, WN, p):
-        """ocp.py:163-172: set x0 / references / weights (diagonals) / parameters, one SQP-RTI iteration."""
+        """ocp.py:163-172: set x0 / references / weights (diagonals) / parameters, one SQP-RTI iteration.
+        An argument given as None keeps the device buffer as it is (written by ref_gen.pack_refs)."""
         N, m = self.N, self.model
-        self._put("x0", x0, (m.nx,))
-        self._put("yref", y, (N, m.ny))
-        self._put("W", W, (N, m.ny))
-        self._put("yNref", yN, (m.nyN,))
-        self._put("WN", WN, (m.nyN,))
-        self._put("p", p, (N + 1, m.np))
+        for name, v, shape in (("x0", x0, (m.nx,)), ("yref", y, (N, m.ny)), ("W", W, (N, m.ny)),
+                               ("yNref", yN, (m.nyN,)), ("WN", WN, (m.nyN,)), ("p", p, (N + 1, m.np))):
+            if v is not None:
+                self._put(name, v, shape)
         b = self.bufs
         b["x"][:, 0] = b["x0"]
         t0 = time.perf_counter()

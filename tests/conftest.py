@@ -38,6 +38,6 @@ def gpu_ctx():
     if not torch.cuda.is_available():
         pytest.fail("gpu test on a machine without a HIP device")
     from sdf_nmpc_amd import _lib
-    ctx = _lib.Context(0)
+    ctx = _lib.Context(0, stream=torch.cuda.current_stream().cuda_stream)  # ordered with torch's stream
     yield ctx
     ctx.close()

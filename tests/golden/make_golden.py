@@ -25,6 +25,8 @@ What is pinned to what:
                           attributes of ``torch.jit.script(NeuralDF(...))`` -- what df_train.py saves and
                           gen_model.py:32 loads -- pinning weights.from_torchscript (data only: no
                           TorchScript archive, which would carry the reference's code, is committed).
+  * refgen_golden.npz  -- the reference's own ``RefGen`` (ref_gen.py:7-130): gen_ref_list_wps over random
+                          paths for every yaw mode, stop-and-turn on/off, gen_ref_joystick, from_x0.
   * params_golden.npz  -- the reference's own ``Nmpc.set_latent`` / ``Nmpc.set_ref`` /
                           ``Quad.formate_ref`` (controller.py:50-54,133-142, quad_rollpitchyawrate.py:
                           62-65) called unbound on small stand-in objects; ``Config`` from the
@@ -373,6 +375,89 @@ def params_golden():
     print("params_golden.npz", len(out))
 
 
+def refgen_golden():
+    """ref_gen.py:7-130 on random paths.  Each case stores x0, waypoints, the config knobs and the
+    returned trajectory as rows [p3 q4 v3 wz1] (N or N+1 rows; NaN-padded to N+1)."""
+    import copy as _copy
+    from sdf_nmpc.ref_gen import RefGen
+    from sdf_nmpc.utils.math import euler2quat
+
+    rng = np.random.default_rng(91)
+    out = {}
+    N = int(CFG.mpc.N)
+    case = 0
+    modes = ["align", "ref", "current", "zero", "curent"]
+    for mode in modes:
+        for st_on in (False, True):
+            for rep in range(4):
+                cfg = _copy.deepcopy(CFG)
+                cfg.ref.yaw_mode = mode
+                cfg.ref.stop_and_turn.enable = st_on
+                cfg.ref.stop_and_turn.dang_min = float(rng.uniform(0.3, 1.5))
+                cfg.ref.align_yaw_offset = float(rng.choice([0.0, 0.2]))
+                cfg.ref.vref = float(rng.choice([1.0, 3.0]))
+                g = RefGen(cfg)
+                x0 = np.zeros(13)
+                x0[:3] = rng.uniform(-2, 2, 3)
+                x0[3:7] = euler2quat(np.array([0.1, -0.1, rng.uniform(-np.pi, np.pi)]))
+                x0[7:10] = rng.normal(0, 1, 3)
+                nwp = int(rng.integers(1, 5))
+                kind = rep % 4
+                wps = []
+                for w in range(nwp):
+                    wp = types.SimpleNamespace()
+                    # kind 2: a short path (total < vref * T: padded tail), kind 3: first waypoint on x0 (align dmin)
+                    scale = 0.3 if kind == 2 else 4.0
+                    wp.p = x0[:3] + rng.uniform(-scale, scale, 3) * (w + 1)
+                    if kind == 3 and w == 0:
+                        wp.p = x0[:3] + np.array([0.01, 0.0, 0.5])
+                    wp.q = euler2quat(np.array([0.0, 0.0, rng.uniform(-np.pi, np.pi)]))
+                    wps.append(wp)
+                g.x0 = x0
+                traj = g.gen_ref_list_wps(wps)
+                rows = np.full((N + 1, 11), np.nan)
+                for k, r in enumerate(traj):
+                    rows[k] = np.concatenate([np.asarray(r.p, float), np.asarray(r.q, float), np.asarray(r.v, float),
+                                              [float(r.wz)]])
+                out[f"w{case}/x0"] = x0
+                out[f"w{case}/wp_p"] = np.array([w.p for w in wps])
+                out[f"w{case}/wp_q"] = np.array([w.q for w in wps])
+                out[f"w{case}/knobs"] = np.array([modes.index(mode), float(st_on), cfg.ref.stop_and_turn.dang_min,
+                                                  cfg.ref.align_yaw_offset, cfg.ref.vref, cfg.ref.yaw_align_dmin,
+                                                  cfg.mpc.T, N])
+                out[f"w{case}/traj"] = rows
+                out[f"w{case}/len"] = np.array(len(traj))
+                case += 1
+    out["n_wps_cases"] = np.array(case)
+    jc = 0
+    for mode in ("align", "ref", "curent"):
+        for rep in range(3):
+            cfg = _copy.deepcopy(CFG)
+            cfg.ref.yaw_mode = mode
+            g = RefGen(cfg)
+            x0 = np.zeros(10)
+            x0[:3] = rng.uniform(-2, 2, 3)
+            x0[3:7] = euler2quat(np.array([0.0, 0.0, rng.uniform(-np.pi, np.pi)]))
+            vw = rng.uniform(-1, 1, 4) * (0.0 if rep == 2 else 1.0)
+            g.x0 = x0
+            traj = g.gen_ref_joystick(vw)
+            out[f"j{jc}/x0"] = x0
+            out[f"j{jc}/vw"] = vw
+            out[f"j{jc}/mode"] = np.array(["align", "ref", "curent"].index(mode))
+            out[f"j{jc}/traj"] = np.array([np.concatenate([np.asarray(r.p, float), np.asarray(r.q, float),
+                                                           np.asarray(r.v, float), [float(r.wz)]]) for r in traj])
+            out[f"j{jc}/Wp"] = np.array(traj[0].Wp, float)
+            jc += 1
+    out["n_joy_cases"] = np.array(jc)
+    g = RefGen(CFG)
+    g.x0 = np.array([0.5, -1, 2, *euler2quat(np.array([0, 0, 1.2])), 0, 0, 0])
+    out["from_x0/x0"] = g.x0
+    out["from_x0/traj"] = np.array([np.concatenate([np.asarray(r.p, float), np.asarray(r.q, float),
+                                                    np.asarray(r.v, float), [float(r.wz)]]) for r in g.from_x0()])
+    np.savez_compressed(os.path.join(HERE, "refgen_golden.npz"), **out)
+    print("refgen_golden.npz", len(out))
+
+
 def ts_golden():
     spec = W.DEFAULT_SPEC
     net = ref_net(spec, W.siren_weights(spec, 0), torch.float32)
@@ -390,6 +475,6 @@ def ts_golden():
 if __name__ == "__main__":
     only = sys.argv[1:]
     for name, fn in (("sdf", sdf_golden), ("lin", lin_golden), ("grid", grid_golden), ("params", params_golden),
-                     ("ts", ts_golden)):
+                     ("ts", ts_golden), ("refgen", refgen_golden)):
         if not only or name in only:
             fn()
