@@ -111,6 +111,14 @@ __device__ __forceinline__ double rdlane(double v, int l) {
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+// 1/x: hardware estimate + two Newton steps (the IPM's row updates; replaces IEEE division)
+__device__ __forceinline__ double rcp_nr(double x) {
+    double y = __builtin_amdgcn_rcp(x);
+    double e = fma(-x, y, 1.0);
+    y = fma(y, e, y);
+    e = fma(-x, y, 1.0);
+    return fma(y, e, y);
+}
 // 1/sqrt(v), v > 0: hardware estimate + one Newton step
 __device__ __forceinline__ double rsqrt_nr(double v) {
     double y = __builtin_amdgcn_rsq(v);
@@ -612,9 +620,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     return wmax(rp);
     };
 
-    // soft group (k, j) = rows (hl, hu, sl, su): barrier weights, v's, eliminated slack block
+    // soft group (k, j) = rows (hl, hu, sl, su): barrier weights, v's, eliminated slack block.
+    // Divisions are reciprocal multiplications (rcp_nr: v_rcp_f64 + two Newton steps), one per
+    // denominator.
     struct Grp {
-        double s1, s2, s3, s4, v1, v2, v3, v4, Hl, Hu, gl, gu;
+        double s1, s2, s3, s4, v1, v2, v3, v4, Hl, Hu, iHl, iHu, gl, gu;
     };
     auto group = [&](int k, int j, int phase, double sigmu) -> Grp {
         Grp g;
@@ -622,7 +632,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double sk = s.skv[k];
         const double t1 = s.t[r0], t2 = s.t[r0 + 1], t3 = s.t[r0 + 2], t4 = s.t[r0 + 3];
         const double l1 = s.lam[r0], l2 = s.lam[r0 + 1], l3 = s.lam[r0 + 2], l4 = s.lam[r0 + 3];
-        g.s1 = l1 / t1; g.s3 = l2 / t2; g.s2 = l3 / t3; g.s4 = l4 / t4;
+        const double it1 = rcp_nr(t1), it2 = rcp_nr(t2), it3 = rcp_nr(t3), it4 = rcp_nr(t4);
+        g.s1 = l1 * it1; g.s3 = l2 * it2; g.s2 = l3 * it3; g.s4 = l4 * it4;
         const double h = s.hv[k * 3 + j];
         g.v1 = g.s1 * (t1 - (h - s.cst[8 + j]));
         g.v3 = g.s3 * (t2 - (s.cst[11 + j] - h));
@@ -631,17 +642,19 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double Zs = sk * s.cst[17 + j], zs = sk * s.cst[14 + j];
         g.Hl = Zs + g.s1 + g.s2;
         g.Hu = Zs + g.s3 + g.s4;
+        g.iHl = rcp_nr(g.Hl);
+        g.iHu = rcp_nr(g.Hu);
         if (phase) {  // corrector: affine deltas of the four rows, recomputed from the affine solution
             const double cxa = s.cxa[k * NS + j];
-            const double sla = -((zs - g.v1 - g.v2) + g.s1 * cxa) / g.Hl;
-            const double sua = -((zs - g.v3 - g.v4) - g.s3 * cxa) / g.Hu;
+            const double sla = -((zs - g.v1 - g.v2) + g.s1 * cxa) * g.iHl;
+            const double sua = -((zs - g.v3 - g.v4) - g.s3 * cxa) * g.iHu;
             const double d1 = cxa + (h - s.cst[8 + j]) + sla - t1;
             const double d2 = -cxa + (s.cst[11 + j] - h) + sua - t2;
             const double d3 = sla - t3, d4 = sua - t4;
-            g.v1 -= (d1 * (-g.s1 * d1 - l1) - sigmu) / t1;
-            g.v3 -= (d2 * (-g.s3 * d2 - l2) - sigmu) / t2;
-            g.v2 -= (d3 * (-g.s2 * d3 - l3) - sigmu) / t3;
-            g.v4 -= (d4 * (-g.s4 * d4 - l4) - sigmu) / t4;
+            g.v1 -= (d1 * (-g.s1 * d1 - l1) - sigmu) * it1;
+            g.v3 -= (d2 * (-g.s3 * d2 - l2) - sigmu) * it2;
+            g.v2 -= (d3 * (-g.s2 * d3 - l3) - sigmu) * it3;
+            g.v4 -= (d4 * (-g.s4 * d4 - l4) - sigmu) * it4;
         }
         g.gl = zs - g.v1 - g.v2;
         g.gu = zs - g.v3 - g.v4;
@@ -649,11 +662,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     };
     auto box_v = [&](int k, int i, int up, int phase, double sigmu) -> double {
         const int r = 8 * k + 4 * up + i;
-        const double t = s.t[r], l = s.lam[r], sg = l / t;
+        const double t = s.t[r], l = s.lam[r], it = rcp_nr(t), sg = l * it;
         double v = sg * (t - box_d(k, i, up));
         if (phase) {
             const double da = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
-            v -= (da * (-sg * da - l) - sigmu) / t;
+            v -= (da * (-sg * da - l) - sigmu) * it;
         }
         return v;
     };
@@ -662,13 +675,12 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         for (int e = lane; e < N1 * NS; e += 64) {
             const int k = e / NS, j = e - NS * k;
             const Grp g = group(k, j, phase, sigmu);
-            const double iHl = 1.0 / g.Hl, iHu = 1.0 / g.Hu;
-            if (!phase) s.fw[e] = g.s1 * (g.Hl - g.s1) * iHl + g.s3 * (g.Hu - g.s3) * iHu;
-            s.fg[e] = -(g.v1 + g.s1 * g.gl * iHl) + (g.v3 + g.s3 * g.gu * iHu);
+            if (!phase) s.fw[e] = g.s1 * (g.Hl - g.s1) * g.iHl + g.s3 * (g.Hu - g.s3) * g.iHu;
+            s.fg[e] = -(g.v1 + g.s1 * g.gl * g.iHl) + (g.v3 + g.s3 * g.gu * g.iHu);
         }
         for (int e = lane; e < N * NU; e += 64) {
             const int k = e >> 2, i = e & 3;
-            if (!phase) s.bd[e] = s.lam[8 * k + i] / s.t[8 * k + i] + s.lam[8 * k + 4 + i] / s.t[8 * k + 4 + i];
+            if (!phase) s.bd[e] = s.lam[8 * k + i] * rcp_nr(s.t[8 * k + i]) + s.lam[8 * k + 4 + i] * rcp_nr(s.t[8 * k + 4 + i]);
             s.bv[e] = -box_v(k, i, 0, phase, sigmu) + box_v(k, i, 1, phase, sigmu);
         }
         wave_sync();
@@ -678,7 +690,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // row values of a soft group (k, j) at an LQR solution with C dx = cxs, and its slacks
     auto soft_vals = [&](const Grp& g, int k, int j, double cxs, double* v) {
         const double h = s.hv[k * 3 + j];
-        const double sl = -(g.gl + g.s1 * cxs) / g.Hl, su = -(g.gu - g.s3 * cxs) / g.Hu;
+        const double sl = -(g.gl + g.s1 * cxs) * g.iHl, su = -(g.gu - g.s3 * cxs) * g.iHu;
         v[0] = cxs + (h - s.cst[8 + j]) + sl;
         v[1] = -cxs + (s.cst[11 + j] - h) + su;
         v[2] = sl;
@@ -691,14 +703,14 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     auto rows_pred = [&]() -> double {
         double amax = 1.0;
         auto bound = [&](double t, double l, double dt, double dl) {
-            if (dt < 0.0) amax = fmin(amax, -t / dt);
-            if (dl < 0.0) amax = fmin(amax, -l / dl);
+            if (dt < 0.0) amax = fmin(amax, -t * rcp_nr(dt));
+            if (dl < 0.0) amax = fmin(amax, -l * rcp_nr(dl));
         };
         for (int r = lane; r < 8 * N; r += 64) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
             const double t = s.t[r], l = s.lam[r];
             const double dt = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
-            bound(t, l, dt, -(l / t) * dt - l);
+            bound(t, l, dt, -(l * rcp_nr(t)) * dt - l);
         }
         for (int e = lane; e < N1 * NS; e += 64) {
             const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
@@ -708,7 +720,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q], dt = v[q] - t;
-                bound(t, l, dt, -(l / t) * dt - l);
+                bound(t, l, dt, -(l * rcp_nr(t)) * dt - l);
             }
         }
         const double aa = wmin(amax);
@@ -717,7 +729,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
             const double t = s.t[r], l = s.lam[r];
             const double dt = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
-            lmua += (t + aa * dt) * (l + aa * (-(l / t) * dt - l));
+            lmua += (t + aa * dt) * (l + aa * (-(l * rcp_nr(t)) * dt - l));
         }
         for (int e = lane; e < N1 * NS; e += 64) {
             const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
@@ -727,7 +739,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q], dt = v[q] - t;
-                lmua += (t + aa * dt) * (l + aa * (-(l / t) * dt - l));
+                lmua += (t + aa * dt) * (l + aa * (-(l * rcp_nr(t)) * dt - l));
             }
         }
         const double mua = wsum(lmua) / m;
@@ -738,8 +750,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     auto rows_update = [&](double sigmu) {
         double amax = 1.0;
         auto bound = [&](double t, double l, double dt, double dl) {
-            if (dt < 0.0) amax = fmin(amax, -t / dt);
-            if (dl < 0.0) amax = fmin(amax, -l / dl);
+            if (dt < 0.0) amax = fmin(amax, -t * rcp_nr(dt));
+            if (dl < 0.0) amax = fmin(amax, -l * rcp_nr(dl));
         };
         // direction of row r: dt = val(z_c) - t, dl = -sigma dt - l - (dt_a dl_a - sigma mu) / t
         amax = 1.0;
@@ -748,7 +760,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const double t = s.t[r], l = s.lam[r];
             const double dt = (up ? -s.duc[k * NU + i] : s.duc[k * NU + i]) + box_d(k, i, up) - t;
             const double dta = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
-            bound(t, l, dt, -(l / t) * dt - l - (dta * (-(l / t) * dta - l) - sigmu) / t);
+            const double it = rcp_nr(t), sg = l * it;
+            bound(t, l, dt, -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it);
         }
         for (int e = lane; e < N1 * NS; e += 64) {
             const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
@@ -760,7 +773,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q];
                 const double dta = va[q] - t, dt = vc[q] - t;
-                bound(t, l, dt, -(l / t) * dt - l - (dta * (-(l / t) * dta - l) - sigmu) / t);
+                const double it = rcp_nr(t), sg = l * it;
+            bound(t, l, dt, -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it);
             }
         }
         const double al = fmin(1.0, 0.995 * wmin(amax));
@@ -771,7 +785,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const double t = s.t[r], l = s.lam[r];
             const double dt = (up ? -s.duc[k * NU + i] : s.duc[k * NU + i]) + box_d(k, i, up) - t;
             const double dta = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
-            const double dl = -(l / t) * dt - l - (dta * (-(l / t) * dta - l) - sigmu) / t;
+            const double it = rcp_nr(t), sg = l * it;
+            const double dl = -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it;
             const double tn = t + al * dt, ln = l + al * dl;
             lmu += tn * ln;
             s.t[r] = tn;
@@ -788,7 +803,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q];
                 const double dta = va[q] - t, dt = vc[q] - t;
-                const double dl = -(l / t) * dt - l - (dta * (-(l / t) * dta - l) - sigmu) / t;
+                const double it = rcp_nr(t), sg = l * it;
+            const double dl = -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it;
                 tn[q] = t + al * dt;
                 ln[q] = l + al * dl;
                 lmu += tn[q] * ln[q];
