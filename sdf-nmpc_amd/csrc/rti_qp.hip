@@ -370,12 +370,15 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             for (int l = 0; l < NX; ++l) row[l] = rp[l];
             off = *(lane < 14 ? fk + lane * 11 + 10 : s.zero);
         }
+        d2 xv[NX / 2];  // the chain input x_k, read after everything else
+#pragma unroll
+        for (int l = 0; l < NX / 2; ++l) xv[l] = xp[l];
+        __builtin_amdgcn_sched_barrier(0);
         double a0 = off, a1 = 0.0;
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) {
-            const d2 x = xp[l];
-            a0 = fma(row[2 * l], x.x, a0);
-            a1 = fma(row[2 * l + 1], x.y, a1);
+            a0 = fma(row[2 * l], xv[l].x, a0);
+            a1 = fma(row[2 * l + 1], xv[l].y, a1);
         }
         ldsd* dst = fc ? cxo + k * NS + fcj
                   : (k < N && fx) ? dxo + (k + 1) * NX + lane
@@ -552,38 +555,46 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             *bc_p = off;
             return;
         }
-        // g~_u (uniform) and the per-lane offset of the chain
+        // ---- every LDS read of the stage first (one round trip), the chain input p_{k+1} last
+        double bvv[NU], guw[NU], kk[NU], row[NX];
 #pragma unroll
         for (int i = 0; i < NU; ++i) {
-            const double bv = s.bv[k * NU + i];
-            off += bc_k[11 * i] * (win[WB_R + R_G + NX + i] + bv) + mu_[i] * bv;
+            bvv[i] = s.bv[k * NU + i];
+            guw[i] = win[WB_R + R_G + NX + i];
+            kk[i] = bc_k[11 * i];
         }
-        double row[NX];
 #pragma unroll
         for (int l = 0; l < NX; ++l) row[l] = bc_row[l * bc_str];
         const ldsd2* pc = (const ldsd2*)(win + F_PC);
-        const ldsd2* pp = (const ldsd2*)s.p;
-        double v[NX];
+        const ldsd2* Lq = (const ldsd2*)(win + F_L);
+        d2 pcv[NX / 2], Lv[5];
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) {
-            const d2 a = pc[l], p = pp[l];
-            v[2 * l] = a.x + p.x;
-            v[2 * l + 1] = a.y + p.y;
+            pcv[l] = pc[l];
+            Lv[l] = Lq[l];
         }
+        const double cb = win[WB_R + R_C + bx], B0 = win[WB_R + 100 + bx], B1 = win[WB_R + 110 + bx];
+        const double B2 = win[WB_R + 120 + bx], B3 = win[WB_R + 130 + bx];
+        const ldsd2* pp = (const ldsd2*)s.p;
+        d2 pv[NX / 2];
+#pragma unroll
+        for (int l = 0; l < NX / 2; ++l) pv[l] = pp[l];
+        __builtin_amdgcn_sched_barrier(0);
+        // g~_u (uniform) and the per-lane offset of the chain
+#pragma unroll
+        for (int i = 0; i < NU; ++i) off += kk[i] * (guw[i] + bvv[i]) + mu_[i] * bvv[i];
         double a0 = off, a1 = 0.0;
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) {
-            a0 = fma(row[2 * l], v[2 * l], a0);
-            a1 = fma(row[2 * l + 1], v[2 * l + 1], a1);
+            a0 = fma(row[2 * l], pcv[l].x + pv[l].x, a0);
+            a1 = fma(row[2 * l + 1], pcv[l].y + pv[l].y, a1);
         }
         const double z = a0 + a1;
         *bc_p = z;
         // off the chain: k_ff, b~
-        const double cb = win[WB_R + R_C + bx], B0 = win[WB_R + 100 + bx], B1 = win[WB_R + 110 + bx];
-        const double B2 = win[WB_R + 120 + bx], B3 = win[WB_R + 130 + bx];
         const double z0 = rdlane(z, 10), z1 = rdlane(z, 11), z2 = rdlane(z, 12), z3 = rdlane(z, 13);
-        const double i0 = win[F_L + 0], l10 = win[F_L + 1], i1 = win[F_L + 2], l20 = win[F_L + 3], l21 = win[F_L + 4];
-        const double i2 = win[F_L + 5], l30 = win[F_L + 6], l31 = win[F_L + 7], l32 = win[F_L + 8], i3 = win[F_L + 9];
+        const double i0 = Lv[0].x, l10 = Lv[0].y, i1 = Lv[1].x, l20 = Lv[1].y, l21 = Lv[2].x;
+        const double i2 = Lv[2].y, l30 = Lv[3].x, l31 = Lv[3].y, l32 = Lv[4].x, i3 = Lv[4].y;
         const double w0 = z0 * i0;
         const double w1 = (z1 - l10 * w0) * i1;
         const double w2 = (z2 - l20 * w0 - l21 * w1) * i2;
@@ -594,7 +605,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double k0 = (-w0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
         const double bb = cb + B0 * k0 + B1 * k1 + B2 * k2 + B3 * k3;
         const double fv = mfx * bb + mu_[0] * k0 + mu_[1] * k1 + mu_[2] * k2 + mu_[3] * k3;
-        F[(size_t)k * FREC + bc_st] = fv;
+        bst(fv, rsF, 8u * bc_st, (unsigned)k * (FREC * 8u));
         if (k < PD) *fs_at(k, bc_st) = fv;
     };
 
