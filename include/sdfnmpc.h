@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define SDFNMPC_ABI_VERSION 2
+#define SDFNMPC_ABI_VERSION 3
 
 enum {
     SDFNMPC_OK = 0,
@@ -211,6 +211,33 @@ int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, cons
 
 /* ---- batched reference / parameter packing into the OCP device buffers (sdfnmpc_ref_args) ---- */
 int sdfnmpc_pack_refs(sdfnmpc_ctx* ctx, const sdfnmpc_ref_opts* opts, const sdfnmpc_ref_args* args);
+
+/* ---- in-loop VAE encoder ----
+ * Replaces VaeWrapper.set_img + VaeWrapper.encode (sdf_nmpc/vae.py:29-40): preprocessing
+ * (vae.py:15-24: float32 cast, Reshape's bilinear resize, ClipDistance, Depth2Range) and
+ * Encoder.forward (network/vae.py:39-43, eval mode) for B images in one call on the context stream.
+ * The encoder is the reference architecture (1 channel, conv7x7/2 + ELU + maxpool, ResBlocks
+ * 64/128/256/512, avgpool 2x2, mean Linear); weights come as a `.vaew` blob (sdf-nmpc_amd/vae.py:pack)
+ * with every BatchNorm folded into its convolution. */
+typedef struct sdfnmpc_vae sdfnmpc_vae;
+
+typedef struct {
+    int B;                 /* images */
+    int in_h, in_w;        /* raw image size; resized bilinearly to the encoder's H x W when different */
+    int dtype;             /* 0 float32, 1 uint16 (ToDevice casts to float32) */
+    float clip;            /* ClipDistance.dmax = sensor.dmax / sensor.mm_resolution * 1000 */
+    const float* yz;       /* device [H][W] Depth2Range.yz_sqrt (sdf-nmpc_amd/vae.py:depth2range_table),
+                              NULL when sensor.is_depth is false */
+} sdfnmpc_vae_opts;
+
+int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* vaew_blob, size_t bytes, sdfnmpc_vae** out);
+void sdfnmpc_vae_free(sdfnmpc_vae* vae);
+int sdfnmpc_vae_size_latent(const sdfnmpc_vae* vae);
+/* img: device [B][in_h][in_w]; latent: device [B][L] float32; latent64: optional device [B][L] float64
+ * (the precision Nmpc.set_latent stores into p).  The activation workspace (~5.7 MB per 270x480 image)
+ * is owned by the encoder object and grows with B. */
+int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* vae, const sdfnmpc_vae_opts* opts, const void* img,
+                       float* latent, double* latent64);
 
 /* ---- shooting grid (host, bit-exact numpy.linspace/diff semantics of ocp.py:21-27) ---- */
 int sdfnmpc_shooting_grid(int N, double T, int uniform, int nb_short_nodes, double dt_short, double* nodes,

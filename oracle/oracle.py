@@ -27,7 +27,7 @@ class Quad(C.Structure):
 
 def build(force=False):
     if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < max(
-            os.path.getmtime(os.path.join(HERE, f)) for f in ("oracle.c", "sdf_net.inc", "qp_ipm.c", "Makefile")):
+            os.path.getmtime(os.path.join(HERE, f)) for f in ("oracle.c", "sdf_net.inc", "qp_ipm.c", "vae.c", "Makefile")):
         subprocess.run(["make", "-s", "-C", HERE], check=True)
     return LIB
 
@@ -57,6 +57,9 @@ def lib():
         _lib.orc_qp_ipm_batch.argtypes = [C.c_int, C.c_int] + [P(d)] * 17 + [C.c_int, C.c_int, C.c_int, P(d), P(d),
                                                                              P(d), P(C.c_int), P(C.c_int), P(d),
                                                                              C.c_int]
+        _lib.orc_vae_preprocess.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
+                                            P(f), P(f)]
+        _lib.orc_vae_encode.argtypes = [P(f), C.c_int, C.c_int, C.c_int, P(f), C.c_int, C.c_int, P(d), P(d)]
     return _lib
 
 
@@ -185,3 +188,31 @@ def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_sca
                            int(bool(cost_scaling)), ny, _p(out["dx"], d), _p(out["du"], d), _p(out["slack"], d),
                            _p(out["iters"], C.c_int), _p(out["status"], C.c_int), _p(out["res"], d), nthreads)
     return out
+
+
+def vae_preprocess(img, shape, clip_scale, yz=None):
+    """vae.py:15-24 preprocessing of one raw image [Hi, Wi] (float32 or uint16) -> fp32 [H, W]."""
+    img = np.ascontiguousarray(img)
+    dtype = 1 if img.dtype == np.uint16 else 0
+    if dtype == 0:
+        img = np.ascontiguousarray(img, dtype=np.float32)
+    H, W = shape
+    out = np.empty((H, W), np.float32)
+    yzp = None if yz is None else _p(np.ascontiguousarray(yz, dtype=np.float32), C.c_float)
+    lib().orc_vae_preprocess(img.ctypes.data, dtype, img.shape[0], img.shape[1], H, W, float(clip_scale), yzp,
+                             _p(out, C.c_float))
+    return out
+
+
+def vae_encode(pre, flat_params, L=128, bn=True, stage_sums=False):
+    """Encoder.forward (network/vae.py:39-43) in fp64 on preprocessed images [B, H, W]."""
+    pre = np.ascontiguousarray(pre, dtype=np.float32)
+    if pre.ndim == 2:
+        pre = pre[None]
+    B, H, W = pre.shape
+    lat = np.empty((B, L), np.float64)
+    ss = np.empty(64 + 128 + 256 + 512 + 512, np.float64) if stage_sums else None
+    flat = np.ascontiguousarray(flat_params, dtype=np.float32)
+    lib().orc_vae_encode(_p(pre, C.c_float), B, H, W, _p(flat, C.c_float), L, int(bn), _p(lat, C.c_double),
+                         None if ss is None else _p(ss, C.c_double))
+    return (lat, ss) if stage_sums else lat

@@ -27,6 +27,7 @@ SYMBOLS = [
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
     "sdfnmpc_linearize", "sdfnmpc_shooting_grid", "sdfnmpc_qp_solve", "sdfnmpc_rti_apply", "sdfnmpc_pack_refs",
+    "sdfnmpc_vae_load", "sdfnmpc_vae_free", "sdfnmpc_vae_size_latent", "sdfnmpc_vae_encode",
 ]
 L4C_SYMBOLS = [
     f"{p}sdf_l4c{s}" for p in ("", "jac_", "adj1_")
@@ -76,6 +77,11 @@ QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", 
 QP_OUT = ("dx", "du", "slack", "status", "iters", "res")
 
 
+class VaeOptsC(C.Structure):
+    _fields_ = [("B", C.c_int), ("in_h", C.c_int), ("in_w", C.c_int), ("dtype", C.c_int), ("clip", C.c_float),
+                ("yz", C.c_void_p)]
+
+
 class QpArgsC(C.Structure):
     _fields_ = [("B", C.c_int), ("N", C.c_int)] + [(n, C.c_void_p) for n in QP_IN + QP_OUT]
 
@@ -121,11 +127,15 @@ def load():
         "sdfnmpc_qp_solve": (i, [vp, P(QpOptsC), P(QpArgsC)]),
         "sdfnmpc_rti_apply": (i, [vp, i, i, vp, vp, vp, vp, vp]),
         "sdfnmpc_pack_refs": (i, [vp, P(RefOptsC), P(RefArgsC)]),
+        "sdfnmpc_vae_load": (i, [vp, vp, sz, P(vp)]),
+        "sdfnmpc_vae_free": (None, [vp]),
+        "sdfnmpc_vae_size_latent": (i, [vp]),
+        "sdfnmpc_vae_encode": (i, [vp, vp, P(VaeOptsC), vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    if lib.sdfnmpc_abi_version() != 2:
+    if lib.sdfnmpc_abi_version() != 3:
         raise SdfnmpcError("libsdfnmpc.so ABI version mismatch")
     _lib = lib
     return lib
@@ -326,3 +336,47 @@ def pack_refs(ctx: Context, opts: RefOptsC, B: int, N: int, np_: int, ny: int, b
     stride = int(x0.shape[-1]) if x0 is not None else 0
     a = RefArgsC(B, N, np_, ny, n_wp, L, _ptr(x0), stride, *[_ptr(bufs.get(k)) for k in REF_IN + REF_OUT])
     _check(load().sdfnmpc_pack_refs(ctx.h, C.byref(opts), C.byref(a)))
+
+
+class Vae:
+    """Device-resident VAE encoder (sdfnmpc_vae) from a `.vaew` blob (sdf_nmpc_amd.vae.pack)."""
+
+    def __init__(self, ctx: Context, blob: bytes, batch: int = 1):
+        self.ctx = ctx
+        h = C.c_void_p()
+        buf = C.create_string_buffer(blob, len(blob))
+        _check(load().sdfnmpc_vae_load(ctx.h, buf, len(blob), C.byref(h)))
+        self.h = h
+        self.batch = batch
+
+    @property
+    def size_latent(self) -> int:
+        return int(load().sdfnmpc_vae_size_latent(self.h))
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().sdfnmpc_vae_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def vae_opts(cfg, clip: float) -> VaeOptsC:
+    """Per-call options from the config (sensor.dmax / mm_resolution, is_depth); B / size / dtype / yz per call."""
+    o = VaeOptsC()
+    o.clip = float(clip)
+    o.dtype = 0
+    return o
+
+
+def vae_encode(ctx: Context, vae: Vae, opts: VaeOptsC, img, yz, latent, latent64=None, depth2range=True):
+    """Enqueue sdfnmpc_vae_encode: img device tensor [B][H][W] (float32 or uint16), latent [B][L] fp32."""
+    import torch
+
+    o = VaeOptsC(int(img.shape[0]), int(img.shape[-2]), int(img.shape[-1]), 1 if img.dtype == torch.uint16 else 0,
+                 float(opts.clip), _ptr(yz) if depth2range else None)
+    _check(load().sdfnmpc_vae_encode(ctx.h, vae.h, C.byref(o), _ptr(img), _ptr(latent), _ptr(latent64)))

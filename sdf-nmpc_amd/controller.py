@@ -156,6 +156,8 @@ class Nmpc:
     # ---- device-side parameter packing (csrc/ref_pack.hip)
     def _dev(self, a, dtype=None):
         import torch
+        if torch.is_tensor(a):  # already a tensor (e.g. VaeWrapper's device latents): no host round trip
+            return a.to(device=self.ocp.device, dtype=torch.float64).contiguous()
         return torch.as_tensor(np.array(a, dtype=np.float64, order="C"), device=self.ocp.device)
 
     def _to_device(self):
@@ -215,7 +217,8 @@ class Nmpc:
         Bn = max(self.B, 1)
         self._to_device()
         L = int(self.cfg.nn.size_latent)
-        args = {"latent": self._dev(np.reshape(latent, (Bn, L))), "W_p_Bo": self._dev(np.reshape(W_p_Bo, (Bn, 3))),
+        lat = latent.reshape(Bn, L) if hasattr(latent, "data_ptr") else np.reshape(latent, (Bn, L))
+        args = {"latent": self._dev(lat), "W_p_Bo": self._dev(np.reshape(W_p_Bo, (Bn, 3))),
                 "W_R_Bo": self._dev(np.reshape(W_R_Bo, (Bn, 9))), "p": self.ocp.bufs["p"]}
         if flag is not None:
             args["flag"] = self._dev(np.broadcast_to(np.asarray(flag, float), (Bn,)))

@@ -20,6 +20,7 @@
 #include "qp_kernels.h"
 #include "ref_kernels.h"
 #include "sdf_kernels.h"
+#include "vae_kernels.h"
 
 using namespace sdfn;
 
@@ -780,5 +781,169 @@ extern "C" int sdfnmpc_shooting_grid(int N, double T, int uniform, int n_short, 
         np_linspace(dt_short * n_short, T, N - n_short + 1, nodes + n_short);
     }
     for (int k = 0; k < N; ++k) dt[k] = nodes[k + 1] - nodes[k];
+    return SDFNMPC_OK;
+}
+
+// ------------------------------------------------------------------------------------------------
+// in-loop VAE encoder: .vaew blob -> device weights + activation workspace
+struct VaeLayer {
+    const float* w = nullptr;
+    const float* b = nullptr;
+    int cin = 0, cout = 0, ks = 0, stride = 0;
+};
+
+struct sdfnmpc_vae {
+    int device = 0;
+    int L = 0, H = 0, W = 0;
+    int Hc = 0, Wc = 0, Hp = 0, Wp = 0;
+    int bh[4] = {0}, bw[4] = {0};  // block output maps
+    void* dmem = nullptr;
+    VaeLayer stem, conv[11], head;  // conv: b0a b0s b0b b1a b1s b1b b2a b2s b2b b3a b3b
+    DevBuf ws;
+    int ws_B = 0;
+};
+
+static const int kVaeBlockIn[4] = {64, 128, 256, 512};
+static const int kVaeBlockStride[4] = {2, 2, 2, 1};
+
+extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes, sdfnmpc_vae** out) {
+    if (!ctx || !blob || !out) return fail(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_vae_load");
+    *out = nullptr;
+    struct Hdr {
+        char magic[8];
+        uint32_t version, nb_chan, L, H, W, n_convs, n_floats, reserved;
+    } h;
+    if (bytes < sizeof(Hdr)) return fail(SDFNMPC_E_FORMAT, "vaew: truncated header");
+    memcpy(&h, blob, sizeof(Hdr));
+    if (memcmp(h.magic, "SDFNVAEW", 8) != 0 || h.version != 1) return fail(SDFNMPC_E_FORMAT, "not a version-1 .vaew blob");
+    if (h.nb_chan != 1 || h.n_convs != 13 || h.L < 1 || h.L > 4096 || h.H < 8 || h.W < 8 || h.H > 8192 || h.W > 8192)
+        return fail(SDFNMPC_E_UNSUPPORTED, "vaew: only the 1-channel reference encoder (13 convolutions) is built");
+    if (bytes != sizeof(Hdr) + 4ull * h.n_floats) return fail(SDFNMPC_E_FORMAT, "vaew: size mismatch");
+    const float* src = (const float*)((const char*)blob + sizeof(Hdr));
+    auto* v = new sdfnmpc_vae();
+    v->device = ctx->device;
+    v->L = (int)h.L; v->H = (int)h.H; v->W = (int)h.W;
+    v->Hc = (v->H - 1) / 2 + 1; v->Wc = (v->W - 1) / 2 + 1;
+    v->Hp = (v->Hc - 1) / 2 + 1; v->Wp = (v->Wc - 1) / 2 + 1;
+    // expected layer list (vae.py:device_layers) and host re-layout of stem / head
+    struct Spec { int cin, cout, ks, stride; };
+    std::vector<Spec> specs = {{1, 64, 7, 2}};
+    int hh = v->Hp, ww = v->Wp;
+    for (int k = 0; k < 4; ++k) {
+        const int ci = kVaeBlockIn[k], s = kVaeBlockStride[k], co = ci * s;
+        specs.push_back({ci, co, 3, s});
+        if (s != 1) specs.push_back({ci, co, 1, s});
+        specs.push_back({co, co, 3, 1});
+        hh = (hh - 1) / s + 1;
+        ww = (ww - 1) / s + 1;
+        v->bh[k] = hh;
+        v->bw[k] = ww;
+    }
+    specs.push_back({2048, (int)h.L, 1, 1});
+    size_t need = 0;
+    for (auto& s : specs) need += (size_t)s.cout * s.ks * s.ks * s.cin + s.cout;
+    if (need != h.n_floats) {
+        delete v;
+        return fail(SDFNMPC_E_FORMAT, "vaew: parameter count does not match the reference encoder");
+    }
+    std::vector<float> dev(need);
+    size_t off = 0;
+    for (size_t li = 0; li < specs.size(); ++li) {
+        const Spec& s = specs[li];
+        const size_t nw = (size_t)s.cout * s.ks * s.ks * s.cin;
+        if (li == 0) {  // stem [64][7][7][1] -> tap-major [49][64]
+            for (int c = 0; c < 64; ++c)
+                for (int t = 0; t < 49; ++t) dev[off + t * 64 + c] = src[off + c * 49 + t];
+        } else if (li + 1 == specs.size()) {  // head [L][2048] -> [2048][L]
+            for (int o = 0; o < s.cout; ++o)
+                for (int f = 0; f < 2048; ++f) dev[off + (size_t)f * s.cout + o] = src[off + (size_t)o * 2048 + f];
+        } else {
+            memcpy(&dev[off], src + off, nw * 4);
+        }
+        memcpy(&dev[off + nw], src + off + nw, (size_t)s.cout * 4);
+        off += nw + s.cout;
+    }
+    ScopedDevice sd(ctx->device);
+    if (hipMalloc(&v->dmem, need * 4) != hipSuccess ||
+        hipMemcpy(v->dmem, dev.data(), need * 4, hipMemcpyHostToDevice) != hipSuccess) {
+        if (v->dmem) (void)hipFree(v->dmem);
+        delete v;
+        return fail(SDFNMPC_E_HIP, "vaew: device upload failed");
+    }
+    const float* d = (const float*)v->dmem;
+    off = 0;
+    for (size_t li = 0; li < specs.size(); ++li) {
+        const Spec& s = specs[li];
+        VaeLayer L{d + off, d + off + (size_t)s.cout * s.ks * s.ks * s.cin, s.cin, s.cout, s.ks, s.stride};
+        if (li == 0) v->stem = L;
+        else if (li + 1 == specs.size()) v->head = L;
+        else v->conv[li - 1] = L;
+        off += (size_t)s.cout * s.ks * s.ks * s.cin + s.cout;
+    }
+    *out = v;
+    return SDFNMPC_OK;
+}
+
+extern "C" void sdfnmpc_vae_free(sdfnmpc_vae* v) {
+    if (!v) return;
+    ScopedDevice sd(v->device);
+    if (v->dmem) (void)hipFree(v->dmem);
+    delete v;
+}
+
+extern "C" int sdfnmpc_vae_size_latent(const sdfnmpc_vae* v) { return v ? v->L : -1; }
+
+extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmpc_vae_opts* o, const void* img,
+                                  float* latent, double* latent64) {
+    if (!ctx || !v || !o) return fail(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_vae_encode");
+    if (o->B < 0 || (o->B > 0 && (!img || !latent))) return fail(SDFNMPC_E_ARG, "vae_encode: bad B or NULL image / latent");
+    if (o->dtype != 0 && o->dtype != 1) return fail(SDFNMPC_E_ARG, "vae_encode: dtype must be 0 (float32) or 1 (uint16)");
+    if (o->in_h < 1 || o->in_w < 1 || !(o->clip > 0.f)) return fail(SDFNMPC_E_ARG, "vae_encode: bad image size or clip");
+    if (ctx->device != v->device) return fail(SDFNMPC_E_ARG, "vae_encode: encoder loaded on another device");
+    const int B = o->B;
+    if (B == 0) return SDFNMPC_OK;
+    ScopedDevice sd(ctx->device);
+    // workspace: pre [B][H][W] | X | Y (block in/out ping-pong) | T (conv_a) | S (shortcut)
+    const size_t n_pre = (size_t)v->H * v->W;
+    size_t n_x = (size_t)v->Hp * v->Wp * 64, n_t = 0;
+    for (int k = 0; k < 4; ++k) {
+        const size_t nb = (size_t)v->bh[k] * v->bw[k] * kVaeBlockIn[k] * kVaeBlockStride[k];
+        n_x = std::max(n_x, nb);
+        n_t = std::max(n_t, nb);
+    }
+    const size_t per = n_pre + 2 * n_x + 2 * n_t;
+    HIPCHK(v->ws.ensure(per * B * sizeof(float)));
+    float* P = (float*)v->ws.p;
+    float* X = P + n_pre * B;
+    float* Y = X + n_x * B;
+    float* T = Y + n_x * B;
+    float* S = T + n_t * B;
+    hipStream_t st = ctx->stream;
+    VaePreArgs pa{img, o->dtype, B, o->in_h, o->in_w, v->H, v->W, o->clip, o->yz, P};
+    HIPCHK(timed(ctx, "vae_pre", [&] { return launch_vae_pre(pa, st); }));
+    VaeStemArgs sa{P, v->stem.w, v->stem.b, X, B, v->H, v->W, v->Hc, v->Wc, v->Hp, v->Wp};
+    HIPCHK(timed(ctx, "vae_stem", [&] { return launch_vae_stem(sa, st); }));
+    int h = v->Hp, w = v->Wp, li = 0;
+    for (int k = 0; k < 4; ++k) {
+        const int s = kVaeBlockStride[k], ho = v->bh[k], wo = v->bw[k];
+        const VaeLayer& ca = v->conv[li++];
+        VaeConvArgs a1{X, ca.w, ca.b, nullptr, T, B, h, w, ca.cin, ho, wo, ca.cout, 1};
+        HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a1, 3, s, st); }));
+        const float* resid = X;
+        if (s != 1) {
+            const VaeLayer& cs = v->conv[li++];
+            VaeConvArgs a2{X, cs.w, cs.b, nullptr, S, B, h, w, cs.cin, ho, wo, cs.cout, 0};
+            HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a2, 1, s, st); }));
+            resid = S;
+        }
+        const VaeLayer& cb = v->conv[li++];
+        VaeConvArgs a3{T, cb.w, cb.b, resid, Y, B, ho, wo, cb.cin, ho, wo, cb.cout, 1};
+        HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a3, 3, 1, st); }));
+        std::swap(X, Y);
+        h = ho;
+        w = wo;
+    }
+    VaeHeadArgs ha{X, v->head.w, v->head.b, latent, latent64, B, h, w, v->L};
+    HIPCHK(timed(ctx, "vae_head", [&] { return launch_vae_head(ha, st); }));
     return SDFNMPC_OK;
 }

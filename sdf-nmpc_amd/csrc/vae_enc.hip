@@ -1,0 +1,340 @@
+// In-loop VAE encoder on gfx950: B depth images -> B latent means.
+//
+// Reference: sdf_nmpc/vae.py:15-40 (preprocessing + Encoder.forward), network/vae.py:6-46 (Encoder),
+// network/resnet.py:5-56 (ResBlock), utils/preprocessing.py (Reshape, ClipDistance, Depth2Range).
+// Inference semantics: dropout is the identity and every BatchNorm is folded into its convolution on
+// the host (sdf-nmpc_amd/vae.py:_fold), so the network is a chain of biased convolutions.
+//
+// Kernels (activations NHWC fp32, resident in one workspace):
+//   vae_pre_kernel   raw depth -> range image (resize, clip, depth->range), one thread per pixel
+//   vae_stem_kernel  conv7x7/2 + ELU + maxpool3/2 fused per 7x8 pooled tile: the 15x17 conv tile lives
+//                    in LDS, the tap weights are wave-uniform (scalar loads), one conv pixel per lane
+//   vae_conv_kernel  every ResBlock convolution as an implicit GEMM on f32 MFMA 32x32x2 (exact fp32
+//                    products): 128x128 output tile per workgroup, K staged 16 at a time through
+//                    double-buffered LDS, bias / residual / ReLU fused into the epilogue
+//   vae_head_kernel  AdaptiveAvgPool2d((2,2)) + Flatten + mean Linear, 4 images per workgroup
+#include <hip/hip_runtime.h>
+
+#include <math.h>
+
+#include "vae_kernels.h"
+
+namespace sdfn {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------------------
+// preprocessing: ToDevice (float32), Reshape (bilinear, align_corners=False), ClipDistance,
+// Depth2Range -- fp32 in torch's operation order (oracle/vae.c:orc_vae_preprocess)
+__global__ __launch_bounds__(256) void vae_pre_kernel(VaePreArgs a) {
+#pragma clang fp contract(off)
+    const int b = blockIdx.y;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= a.H * a.W) return;
+    const int y = i / a.W, x = i - y * a.W;
+    const size_t ib = (size_t)b * a.Hi * a.Wi;
+    auto px = [&](int yy, int xx) -> float {
+        const size_t k = ib + (size_t)yy * a.Wi + xx;
+        return a.dtype == 1 ? (float)((const unsigned short*)a.img)[k] : ((const float*)a.img)[k];
+    };
+    float v;
+    if (a.Hi == a.H && a.Wi == a.W) {
+        v = px(y, x);
+    } else {
+        const float sh = (float)a.Hi / (float)a.H, sw = (float)a.Wi / (float)a.W;
+        float fy = sh * ((float)y + 0.5f) - 0.5f, fx = sw * ((float)x + 0.5f) - 0.5f;
+        fy = fy < 0.f ? 0.f : fy;
+        fx = fx < 0.f ? 0.f : fx;
+        const int y0 = (int)fy, x0 = (int)fx;
+        const int y1 = y0 + (y0 < a.Hi - 1), x1 = x0 + (x0 < a.Wi - 1);
+        const float ly1 = fy - (float)y0, ly0 = 1.f - ly1, lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+        v = ly0 * (lx0 * px(y0, x0) + lx1 * px(y0, x1)) + ly1 * (lx0 * px(y1, x0) + lx1 * px(y1, x1));
+    }
+    v = v / a.clip;
+    v = v < 0.f ? 0.f : (v > 1.f ? 1.f : v);
+    if (a.yz) {
+        v = v * a.yz[i];
+        v = v < 0.f ? 0.f : (v > 1.f ? 1.f : v);
+    }
+    a.out[(size_t)b * a.H * a.W + i] = v;
+}
+
+hipError_t launch_vae_pre(const VaePreArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(vae_pre_kernel, dim3((a.H * a.W + 255) / 256, a.B), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// stem: conv7x7/2 pad 3 (1 -> 64) + bias + ELU + maxpool3/2 pad 1 (vae.py:19-21)
+constexpr int ST_PY = 7, ST_PX = 8;                        // pooled tile
+constexpr int ST_CY = 2 * ST_PY + 1, ST_CX = 2 * ST_PX + 1;  // conv tile 15 x 17 = 255 pixels
+constexpr int ST_IY = 2 * ST_CY + 5, ST_IX = 2 * ST_CX + 5;  // input patch 35 x 39
+constexpr int ST_IXP = ST_IX + 1;
+constexpr int ST_CS = 65;                                  // conv tile stride (floats): odd -> no conflicts
+
+__global__ __launch_bounds__(256) void vae_stem_kernel(VaeStemArgs a) {
+    __shared__ float patch[ST_IY * ST_IXP];
+    __shared__ float conv[ST_CY * ST_CX * ST_CS];
+    const int t = threadIdx.x, img = blockIdx.z;
+    const int py0 = blockIdx.y * ST_PY, px0 = blockIdx.x * ST_PX;
+    const int gy0 = 4 * py0 - 5, gx0 = 4 * px0 - 5;
+    const float* in = a.in + (size_t)img * a.H * a.W;
+    for (int e = t; e < ST_IY * ST_IX; e += 256) {
+        const int r = e / ST_IX, c = e - r * ST_IX;
+        const int gy = gy0 + r, gx = gx0 + c;
+        patch[r * ST_IXP + c] = ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W) ? in[(size_t)gy * a.W + gx] : 0.f;
+    }
+    __syncthreads();
+    if (t < ST_CY * ST_CX) {
+        const int cyl = t / ST_CX, cxl = t - cyl * ST_CX;
+        float acc[64];
+#pragma unroll
+        for (int c = 0; c < 64; ++c) acc[c] = a.b[c];
+        const float* pp = patch + (2 * cyl) * ST_IXP + 2 * cxl;
+        for (int ky = 0; ky < 7; ++ky) {
+#pragma unroll
+            for (int kx = 0; kx < 7; ++kx) {
+                const float v = pp[ky * ST_IXP + kx];
+                const float* wr = a.w + (ky * 7 + kx) * 64;  // wave-uniform: scalar loads
+#pragma unroll
+                for (int c = 0; c < 64; ++c) acc[c] = fmaf(wr[c], v, acc[c]);
+            }
+        }
+        const int cy = 2 * py0 - 1 + cyl, cx = 2 * px0 - 1 + cxl;
+        const bool ok = (unsigned)cy < (unsigned)a.Hc && (unsigned)cx < (unsigned)a.Wc;
+#pragma unroll
+        for (int c = 0; c < 64; ++c) {
+            const float v = acc[c] > 0.f ? acc[c] : expm1f(acc[c]);  // ELU(alpha = 1)
+            conv[t * ST_CS + c] = ok ? v : -INFINITY;                // outside the map: never the max
+        }
+    }
+    __syncthreads();
+    const int c = t & 63;
+    for (int q = t >> 6; q < ST_PY * ST_PX; q += 4) {
+        const int pyl = q / ST_PX, pxl = q - pyl * ST_PX;
+        const int py = py0 + pyl, px = px0 + pxl;
+        if (py >= a.Hp || px >= a.Wp) continue;
+        float m = -INFINITY;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) m = fmaxf(m, conv[((2 * pyl + dy) * ST_CX + 2 * pxl + dx) * ST_CS + c]);
+        a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c] = m;
+    }
+}
+
+hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    if (a.Hc != (a.H - 1) / 2 + 1 || a.Wc != (a.W - 1) / 2 + 1 || a.Hp != (a.Hc - 1) / 2 + 1 ||
+        a.Wp != (a.Wc - 1) / 2 + 1)
+        return hipErrorInvalidValue;
+    dim3 grid((a.Wp + ST_PX - 1) / ST_PX, (a.Hp + ST_PY - 1) / ST_PY, a.B);
+    hipLaunchKernelGGL(vae_stem_kernel, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// implicit-GEMM convolution: out[m][n] = sum_k A[m][k] W[n][k], m = (image, oy, ox), n = channel,
+// k = (ky, kx, ci).  Tile 128 x 128 x 16, 4 waves as 2 x 2 of 64 x 64 (four 32x32 MFMA blocks each).
+// LDS rows are 16 k-values padded to 20 floats: the ds_read_b128 lane groups then hit 16 distinct
+// 16-byte slots (conflict-free).  Within a K-tile, MFMA step s feeds lane half h with k = 8h + s
+// (the same permutation for A and B), so each lane reads its 8 k-values with two ds_read_b128.
+constexpr int CV_BM = 128, CV_BN = 128, CV_BK = 16, CV_LD = 20;
+
+// component-wise select (a ?: on the float4 struct goes through a stack slot)
+__device__ __forceinline__ float4 sel4(bool ok, float4 v) {
+    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
+}
+
+template <int KS, int S>
+__global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
+    constexpr int P = KS / 2;
+    __shared__ float As[2][CV_BM * CV_LD];
+    __shared__ float Bs[2][CV_BN * CV_LD];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
+    const int M = a.B * a.Ho * a.Wo, MT = (M + CV_BM - 1) / CV_BM;
+    const int nt = blockIdx.x / MT, mt = blockIdx.x - nt * MT;
+    const int Cin = a.Cin, K = KS * KS * Cin, KT = K / CV_BK;
+    const int kq = tid & 3;
+
+    // loader rows (A) and columns (B) of this thread (scalars, so nothing is indexed dynamically)
+    const int HW = a.Ho * a.Wo;
+    const int m0 = mt * CV_BM + (tid >> 2), m1 = m0 + 64;
+    const bool v0 = m0 < M, v1 = m1 < M;
+    const int q0 = v0 ? m0 : 0, q1 = v1 ? m1 : 0;
+    const int im0 = q0 / HW, r0 = q0 - im0 * HW, oy0 = r0 / a.Wo, ox0 = r0 - oy0 * a.Wo;
+    const int im1 = q1 / HW, r1 = q1 - im1 * HW, oy1 = r1 / a.Wo, ox1 = r1 - oy1 * a.Wo;
+    const int iyA = oy0 * S - P, ixA = ox0 * S - P, iyB = oy1 * S - P, ixB = ox1 * S - P;
+    const float* pa0 = a.in + (size_t)im0 * a.Hi * a.Wi * Cin + 4 * kq;
+    const float* pa1 = a.in + (size_t)im1 * a.Hi * a.Wi * Cin + 4 * kq;
+    const float* pb0 = a.w + (size_t)(nt * CV_BN + (tid >> 2)) * K + 4 * kq;
+    const float* pb1 = pb0 + (size_t)64 * K;
+    const int srow0 = (tid >> 2) * CV_LD + 4 * kq, srow1 = srow0 + 64 * CV_LD;
+
+    float4 ra0, ra1, rb0, rb1;
+    int ky = 0, kx = 0, c0 = 0;  // K-tile position (tap, channel block) being loaded
+#define VAE_LOAD(kt)                                                                                          \
+    do {                                                                                                      \
+        const int iy0_ = iyA + ky, ix0_ = ixA + kx, iy1_ = iyB + ky, ix1_ = ixB + kx;                          \
+        const bool ok0_ = v0 && (unsigned)iy0_ < (unsigned)a.Hi && (unsigned)ix0_ < (unsigned)a.Wi;           \
+        const bool ok1_ = v1 && (unsigned)iy1_ < (unsigned)a.Hi && (unsigned)ix1_ < (unsigned)a.Wi;           \
+        /* always load from a valid address (the image origin when outside), then select */                  \
+        const float4 t0_ = *(const float4*)(pa0 + (ok0_ ? ((size_t)iy0_ * a.Wi + ix0_) * Cin + c0 : 0));         \
+        const float4 t1_ = *(const float4*)(pa1 + (ok1_ ? ((size_t)iy1_ * a.Wi + ix1_) * Cin + c0 : 0));         \
+        ra0 = sel4(ok0_, t0_);                                                                                \
+        ra1 = sel4(ok1_, t1_);                                                                                \
+        rb0 = *(const float4*)(pb0 + (size_t)(kt) * CV_BK);                                                   \
+        rb1 = *(const float4*)(pb1 + (size_t)(kt) * CV_BK);                                                   \
+        c0 += CV_BK;                                                                                          \
+        if (c0 == Cin) {                                                                                      \
+            c0 = 0;                                                                                           \
+            if (++kx == KS) {                                                                                 \
+                kx = 0;                                                                                       \
+                ++ky;                                                                                         \
+            }                                                                                                 \
+        }                                                                                                     \
+    } while (0)
+#define VAE_STASH(buf)                                        \
+    do {                                                      \
+        *(float4*)(&As[buf][srow0]) = ra0;                    \
+        *(float4*)(&As[buf][srow1]) = ra1;                    \
+        *(float4*)(&Bs[buf][srow0]) = rb0;                    \
+        *(float4*)(&Bs[buf][srow1]) = rb1;                    \
+    } while (0)
+
+    floatx16 acc[2][2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+    VAE_LOAD(0);
+    VAE_STASH(0);
+    __syncthreads();
+    for (int kt = 0; kt < KT; ++kt) {
+        const int buf = kt & 1;
+        if (kt + 1 < KT) VAE_LOAD(kt + 1);
+        float av[2][8], bv[2][8];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const float* ap = &As[buf][(wm * 64 + 32 * i + lr) * CV_LD + 8 * lh];
+            const float* bp = &Bs[buf][(wn * 64 + 32 * i + lr) * CV_LD + 8 * lh];
+            const float4 a0 = *(const float4*)ap, a1 = *(const float4*)(ap + 4);
+            const float4 b0 = *(const float4*)bp, b1 = *(const float4*)(bp + 4);
+            av[i][0] = a0.x; av[i][1] = a0.y; av[i][2] = a0.z; av[i][3] = a0.w;
+            av[i][4] = a1.x; av[i][5] = a1.y; av[i][6] = a1.z; av[i][7] = a1.w;
+            bv[i][0] = b0.x; bv[i][1] = b0.y; bv[i][2] = b0.z; bv[i][3] = b0.w;
+            bv[i][4] = b1.x; bv[i][5] = b1.y; bv[i][6] = b1.z; bv[i][7] = b1.w;
+        }
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[j][s], acc[i][j], 0, 0, 0);
+        if (kt + 1 < KT) VAE_STASH(buf ^ 1);
+        __syncthreads();
+    }
+
+    // epilogue: lane (lr, lh), register r holds row 8(r/4) + 4 lh + r%4, column lr of each block
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int n = nt * CV_BN + wn * 64 + 32 * j + lr;
+        const float bias = a.b[n];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int m = mt * CV_BM + wm * 64 + 32 * i + 8 * (r >> 2) + 4 * lh + (r & 3);
+                if (m < M) {
+                    const size_t o = (size_t)m * a.Cout + n;
+                    float v = acc[i][j][r] + bias;
+                    if (a.resid) v += a.resid[o];
+                    if (a.relu) v = fmaxf(v, 0.f);
+                    a.out[o] = v;
+                }
+            }
+    }
+#undef VAE_LOAD
+#undef VAE_STASH
+}
+
+hipError_t launch_vae_conv(const VaeConvArgs& a, int ks, int stride, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    const int p = ks / 2;
+    if (a.Cin % CV_BK || a.Cout % CV_BN || a.Ho != (a.Hi + 2 * p - ks) / stride + 1 ||
+        a.Wo != (a.Wi + 2 * p - ks) / stride + 1)
+        return hipErrorInvalidValue;
+    const long long M = (long long)a.B * a.Ho * a.Wo;
+    const long long grid = ((M + CV_BM - 1) / CV_BM) * (a.Cout / CV_BN);
+    if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
+    if (ks == 3 && stride == 1)
+        hipLaunchKernelGGL((vae_conv_kernel<3, 1>), dim3((unsigned)grid), dim3(256), 0, s, a);
+    else if (ks == 3 && stride == 2)
+        hipLaunchKernelGGL((vae_conv_kernel<3, 2>), dim3((unsigned)grid), dim3(256), 0, s, a);
+    else if (ks == 1 && stride == 2)
+        hipLaunchKernelGGL((vae_conv_kernel<1, 2>), dim3((unsigned)grid), dim3(256), 0, s, a);
+    else
+        return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------------------
+// head: AdaptiveAvgPool2d((2,2)) (bin i spans [floor(i h/2), ceil((i+1) h/2))), Flatten (c*4 + i*2 + j),
+// mean Linear.  4 images per workgroup; features in LDS, the [2048][L] weight read once per workgroup.
+constexpr int HD_IMG = 4;
+
+__global__ __launch_bounds__(256) void vae_head_kernel(VaeHeadArgs a) {
+    __shared__ float feat[HD_IMG][2048];
+    const int t = threadIdx.x, b0 = blockIdx.x * HD_IMG;
+    for (int q = 0; q < HD_IMG; ++q) {
+        const int b = b0 + q;
+        for (int c = t; c < 512; c += 256)
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int j = 0; j < 2; ++j) {
+                    float s = 0.f;
+                    const int y0 = (i * a.h) / 2, y1 = ((i + 1) * a.h + 1) / 2;
+                    const int x0 = (j * a.w) / 2, x1 = ((j + 1) * a.w + 1) / 2;
+                    if (b < a.B)
+                        for (int y = y0; y < y1; ++y)
+                            for (int x = x0; x < x1; ++x) s += a.in[(((size_t)b * a.h + y) * a.w + x) * 512 + c];
+                    feat[q][c * 4 + i * 2 + j] = s / (float)((y1 - y0) * (x1 - x0));
+                }
+    }
+    __syncthreads();
+    const int pair = t >> 7;  // images 2 pair, 2 pair + 1 (wave-uniform)
+    for (int o = t & 127; o < a.L; o += 128) {
+        float s0 = a.b[o], s1 = s0;
+        const float* f0 = feat[2 * pair];
+        const float* f1 = feat[2 * pair + 1];
+        for (int f = 0; f < 2048; ++f) {
+            const float w = a.wt[(size_t)f * a.L + o];
+            s0 = fmaf(w, f0[f], s0);
+            s1 = fmaf(w, f1[f], s1);
+        }
+        const int bA = b0 + 2 * pair, bB = bA + 1;
+        if (bA < a.B) {
+            a.latent[(size_t)bA * a.L + o] = s0;
+            if (a.latent64) a.latent64[(size_t)bA * a.L + o] = (double)s0;
+        }
+        if (bB < a.B) {
+            a.latent[(size_t)bB * a.L + o] = s1;
+            if (a.latent64) a.latent64[(size_t)bB * a.L + o] = (double)s1;
+        }
+    }
+}
+
+hipError_t launch_vae_head(const VaeHeadArgs& a, hipStream_t s) {
+    if (a.B <= 0) return hipSuccess;
+    hipLaunchKernelGGL(vae_head_kernel, dim3((a.B + HD_IMG - 1) / HD_IMG), dim3(256), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace sdfn

@@ -99,3 +99,27 @@ def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None, sd
         yref = np.concatenate([yref, np.zeros((B, N, 1))], axis=-1)
         W = np.concatenate([W, np.full((B, N, 1), 20.0)], axis=-1)
     return dict(x=x, u=u, p=p, dt=np.asarray(dt, float), yref=yref, W=W, yN=yN, WN=WN, x0=x0, latent=latent)
+
+
+def depth_images(B: int, H: int = 270, W: int = 480, seed: int = 0, kind: str = "m") -> np.ndarray:
+    """Seeded synthetic depth images [B, H, W] for the VAE path (1x270x480 ~ U(0, 5 m)).
+
+    A smooth scene (two walls + a box) plus uniform noise, with ~5 % invalid (zero) pixels and ~5 %
+    beyond dmax.  kind 'm': float32 metres; 'mm': uint16 millimetres (mm_resolution = 1 sensors).
+    """
+    from .weights import prng_uniform
+
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float64)
+    out = np.empty((B, H, W), np.float64)
+    for b in range(B):
+        u = prng_uniform(seed * 7919 + b, 40, 3 * H * W).reshape(3, H, W)
+        ph = prng_uniform(seed * 7919 + b, 41, 6)
+        wall = 1.0 + 3.0 * (0.5 + 0.5 * np.sin(xx / (20 + 40 * ph[0]) + 6.3 * ph[1])) * (0.6 + 0.4 * np.cos(yy / (15 + 30 * ph[2])))
+        box = (np.abs(xx - W * ph[3]) < W * 0.15) & (np.abs(yy - H * ph[4]) < H * 0.2)
+        d = np.where(box, 0.6 + 0.8 * ph[5], wall) + 0.3 * u[0]
+        d = np.where(u[1] < 0.05, 0.0, d)
+        d = np.where(u[2] < 0.05, 6.0 + 2.0 * u[0], d)
+        out[b] = d
+    if kind == "mm":
+        return np.round(out * 1000.0).astype(np.uint16)
+    return out.astype(np.float32)

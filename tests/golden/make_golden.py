@@ -27,6 +27,11 @@ What is pinned to what:
                           TorchScript archive, which would carry the reference's code, is committed).
   * refgen_golden.npz  -- the reference's own ``RefGen`` (ref_gen.py:7-130): gen_ref_list_wps over random
                           paths for every yaw mode, stop-and-turn on/off, gen_ref_joystick, from_x0.
+  * vae_golden.npz     -- the reference's own ``Encoder`` (network/vae.py:6-46, resnet.py:5-56) in eval
+                          mode and its preprocessing chain (vae.py:15-24: Reshape, ClipDistance,
+                          Depth2Range from utils/preprocessing.py), weights from
+                          sdf_nmpc_amd.vae.synthetic_encoder, images from synth.depth_images: latent
+                          means in fp32 and fp64, sampled preprocessed pixels, per-stage channel sums.
   * params_golden.npz  -- the reference's own ``Nmpc.set_latent`` / ``Nmpc.set_ref`` /
                           ``Quad.formate_ref`` (controller.py:50-54,133-142, quad_rollpitchyawrate.py:
                           62-65) called unbound on small stand-in objects; ``Config`` from the
@@ -472,9 +477,66 @@ def ts_golden():
     print("ts_golden.npz", len(out))
 
 
+def vae_golden():
+    import copy as _copy
+    from sdf_nmpc.network.vae import Encoder
+    from sdf_nmpc.utils import preprocessing as P
+    from sdf_nmpc_amd import synth
+    from sdf_nmpc_amd import vae as V
+
+    spec = V.DEFAULT_ENCODER
+    enc = Encoder(spec.nb_chan, spec.size_latent, dropout_rate=0.1, batchnorm=spec.batchnorm).eval()
+    sd = enc.state_dict()
+    names = [k for k in sd.keys() if not k.endswith("num_batches_tracked")]
+    assert names == [n for n, _ in spec.param_shapes()], "param order"
+    params = V.synthetic_encoder(spec, 0)
+    for k, shape in spec.param_shapes():
+        assert tuple(sd[k].shape) == shape, k
+        sd[k] = torch.from_numpy(params[k].copy())
+    enc.load_state_dict(sd)
+    enc64 = _copy.deepcopy(enc).double()
+    shape = list(CFG.sensor.shape_imgs)
+    d2r = P.Depth2Range(shape, CFG.sensor.hfov, CFG.sensor.vfov)
+    cases = [  # (image, mm_resolution)
+        (synth.depth_images(1, 270, 480, seed=0)[0], 1000),
+        (synth.depth_images(1, 270, 480, seed=1)[0], 1000),
+        (synth.depth_images(1, 270, 480, seed=2, kind="mm")[0], 1),
+        (synth.depth_images(1, 240, 424, seed=3)[0], 1000),  # Reshape's bilinear resize path
+    ]
+    rng = np.random.default_rng(5)
+    out = {"names": np.array(names), "n_cases": np.array(len(cases)),
+           "yz_sqrt_sample": d2r.yz_sqrt.numpy()[::7, ::11].copy(), "flops": np.int64(spec.n_flops())}
+    for c, (img, mmr) in enumerate(cases):
+        pre = torch.nn.Sequential(P.ToDevice("cpu"), torch.jit.script(P.Reshape(shape)),
+                                  torch.jit.script(P.ClipDistance(CFG.sensor.dmax, mmr)),
+                                  torch.jit.script(P.Depth2Range(shape, CFG.sensor.hfov, CFG.sensor.vfov, "cpu")))
+        x = pre(img)
+        with torch.no_grad():
+            lat = enc(x).numpy()[0]
+            lat64 = enc64(x.double()).numpy()[0]
+        iy = rng.integers(0, shape[1], 4096)
+        ix = rng.integers(0, shape[2], 4096)
+        out[f"c{c}/seed"] = np.array([c, 2 if mmr == 1 else 0])
+        out[f"c{c}/in_shape"] = np.array(img.shape)
+        out[f"c{c}/mm_resolution"] = np.float64(mmr)
+        out[f"c{c}/pre_idx"] = np.stack([iy, ix])
+        out[f"c{c}/pre_val"] = x.numpy()[0, 0, iy, ix]
+        out[f"c{c}/latent"] = lat
+        out[f"c{c}/latent64"] = lat64
+        if c == 0:  # per-stage channel sums of the fp64 run (debugging aid for the oracle / kernels)
+            h = x.double()
+            with torch.no_grad():
+                for i, m in enumerate(enc64.layers["resnet"]):
+                    h = m(h)
+                    if i in (2, 3, 4, 5, 6):
+                        out[f"c0/stage{i}"] = h.sum(dim=(0, 2, 3)).numpy()
+    np.savez_compressed(os.path.join(HERE, "vae_golden.npz"), **out)
+    print("vae_golden.npz", len(out))
+
+
 if __name__ == "__main__":
     only = sys.argv[1:]
     for name, fn in (("sdf", sdf_golden), ("lin", lin_golden), ("grid", grid_golden), ("params", params_golden),
-                     ("ts", ts_golden), ("refgen", refgen_golden)):
+                     ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden)):
         if not only or name in only:
             fn()
