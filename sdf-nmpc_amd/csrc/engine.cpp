@@ -74,7 +74,7 @@ struct sdfnmpc_ctx {
     bool lin_first = false;
     int tile_rows = 32;
     bool timing = false;
-    DevBuf c13, sdf4, lat, out4, glat, qpw, qpst;
+    DevBuf c13, sdf4, lat, out4, glat, qpw, qpst, wws;
     std::vector<float> h_in;  // host staging for sdf_eval_host
     std::map<std::string, KStat> stats;
     std::mutex mu;  // serialises the host-pointer path (CasADi externals may be called concurrently)
@@ -298,13 +298,21 @@ void alloc_params(HostNet& h) {
     for (size_t i = 0; i < v.size(); ++i) v[i]->assign((size_t)sh[i].first * sh[i].second, 0.0f);
 }
 
+// wide networks (every layer a multiple of 128, e.g. config C5's [1024,1024,512,256]) run the
+// layer-by-layer GEMM schedule of sdf_wide.hip; the deployed [256,256,128,64] the fused sdf_mlp.hip
+bool is_wide(const HostNet& h) {
+    return !(h.n1 == N1 && h.n2 == N2 && h.n3 == N3 && h.n4 == N4) && h.n1 % 128 == 0 && h.n2 % 128 == 0 &&
+           h.n3 % 128 == 0 && h.n4 % 128 == 0;
+}
+
 int check_supported(const HostNet& h) {
-    if (h.nb_states != 3 || h.L != L || h.n1 != N1 || h.n2 != N2 || h.n3 != N3 || h.n4 != N4 || h.nd != EMB_ND ||
-        h.nf != EMB_NF) {
+    const bool arch_ok = (h.n1 == N1 && h.n2 == N2 && h.n3 == N3 && h.n4 == N4) || is_wide(h);
+    if (h.nb_states != 3 || h.L != L || !arch_ok || h.nd != EMB_ND || h.nf != EMB_NF) {
         char buf[256];
         snprintf(buf, sizeof buf,
                  "network architecture (states %d, latent %d, layers [%d,%d,%d,%d], dirs %d, freqs %d) is not "
-                 "built for; this build supports latent 128, [256,256,128,64], 'oct' embedding, 5 freqs",
+                 "built for; this build supports latent 128, 'oct' embedding, 5 freqs and layers [256,256,128,64] or "
+                 "all multiples of 128 (e.g. [1024,1024,512,256])",
                  h.nb_states, h.L, h.n1, h.n2, h.n3, h.n4, h.nd, h.nf);
         return fail(SDFNMPC_E_UNSUPPORTED, buf);
     }
@@ -392,6 +400,13 @@ void pack_operand(std::vector<float>& dst, int N, int K, F&& W) {
 
 }  // namespace
 
+struct WideDev {  // plain row-major [N][K] fp32 operands of the wide schedule (sdf_wide.hip)
+    const float *F1 = nullptr, *F2 = nullptr, *F3 = nullptr, *F4 = nullptr;
+    const float *B4 = nullptr, *B3h = nullptr, *B3e = nullptr, *B2 = nullptr, *B1e = nullptr;
+    const float *Hz = nullptr, *bz = nullptr, *b2 = nullptr, *b4 = nullptr, *w5 = nullptr;
+    const float4* emb_tab = nullptr;
+};
+
 struct sdfnmpc_net {
     int device = 0;
     HostNet host;
@@ -400,9 +415,99 @@ struct sdfnmpc_net {
     const float4* WzT = nullptr;
     const float* bias13 = nullptr;
     uint64_t fingerprint = 0;
+    bool wide = false;
+    WideDev wd;
 };
 
+static void emb_table(const HostNet& h, std::vector<float>& blob) {
+    for (int m = 0; m < NE; ++m) {
+        float v[4] = {0, 0, 0, 0};
+        int j = -1;
+        if (m >= 3 && m < 3 + EMB_NB) j = m - 3;
+        else if (m >= 3 + EMB_NB && m < E) j = m - 3 - EMB_NB;
+        if (j >= 0) {
+            const int d = j / EMB_NF, f = j % EMB_NF;
+            for (int c = 0; c < 3; ++c) v[c] = h.dirs[c * EMB_ND + d] * h.freqs[f];  // freq = 2^f: exact
+        }
+        blob.insert(blob.end(), v, v + 4);
+    }
+}
+
+static uint64_t net_fingerprint(HostNet& h) {  // FNV-1a over the parameters in torch order
+    uint64_t fp = 1469598103934665603ULL;
+    auto sh = param_shapes(h);
+    auto pl = param_list(h);
+    for (size_t t = 0; t < pl.size(); ++t) {
+        const unsigned char* b = (const unsigned char*)pl[t];
+        const size_t nb = (size_t)sh[t].first * sh[t].second * 4;
+        for (size_t q = 0; q < nb; ++q) fp = (fp ^ b[q]) * 1099511628211ULL;
+    }
+    return fp;
+}
+
+static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
+    const int n1 = h.n1, n2 = h.n2, n3 = h.n3, n4 = h.n4, c1 = E + L, c3 = n2 + E + L;
+    const float *W1 = h.W1.data(), *W2 = h.W2.data(), *W3 = h.W3.data(), *W4 = h.W4.data();
+    std::vector<float> blob;
+    std::vector<size_t> off;
+    auto mat = [&](int N, int K, auto&& f) {
+        off.push_back(blob.size());
+        for (int j = 0; j < N; ++j)
+            for (int k = 0; k < K; ++k) blob.push_back(f(j, k));
+    };
+    mat(n1, NE, [&](int j, int k) { return k < E ? W1[(size_t)j * c1 + k] : 0.0f; });                      // F1
+    mat(n2, n1, [&](int j, int k) { return W2[(size_t)j * n1 + k]; });                                      // F2
+    mat(n3, n2 + NE, [&](int j, int k) { return k < n2 + E ? W3[(size_t)j * c3 + k] : 0.0f; });            // F3
+    mat(n4, n3, [&](int j, int k) { return W4[(size_t)j * n3 + k]; });                                      // F4
+    mat(n3, n4, [&](int j, int k) { return W4[(size_t)k * n3 + j]; });                                      // B4
+    mat(n2, n3, [&](int j, int k) { return W3[(size_t)k * c3 + j]; });                                      // B3h
+    mat(128, n3, [&](int j, int k) { return j < E ? W3[(size_t)k * c3 + n2 + j] : 0.0f; });                 // B3e
+    mat(n1, n2, [&](int j, int k) { return W2[(size_t)k * n1 + j]; });                                      // B2
+    mat(128, n1, [&](int j, int k) { return j < E ? W1[(size_t)k * c1 + j] : 0.0f; });                      // B1e
+    mat(n1 + n3, L, [&](int j, int k) {                                                                     // Hz
+        return j < n1 ? W1[(size_t)j * c1 + E + k] : W3[(size_t)(j - n1) * c3 + n2 + E + k];
+    });
+    off.push_back(blob.size());  // bz
+    blob.insert(blob.end(), h.b1.begin(), h.b1.end());
+    blob.insert(blob.end(), h.b3.begin(), h.b3.end());
+    off.push_back(blob.size());
+    blob.insert(blob.end(), h.b2.begin(), h.b2.end());
+    off.push_back(blob.size());
+    blob.insert(blob.end(), h.b4.begin(), h.b4.end());
+    off.push_back(blob.size());
+    blob.insert(blob.end(), h.W5.begin(), h.W5.end());
+    while (blob.size() % 4) blob.push_back(0.0f);
+    off.push_back(blob.size());
+    emb_table(h, blob);
+    for (size_t o : off)
+        if (o % 4) return fail(SDFNMPC_E_FORMAT, "internal: misaligned wide operand");
+    auto* net = new sdfnmpc_net();
+    net->device = ctx->device;
+    net->wide = true;
+    ScopedDevice sd(ctx->device);
+    if (hipMalloc(&net->dmem, blob.size() * sizeof(float)) != hipSuccess ||
+        hipMemcpy(net->dmem, blob.data(), blob.size() * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) {
+        if (net->dmem) (void)hipFree(net->dmem);
+        delete net;
+        return fail(SDFNMPC_E_HIP, "wide net: device upload failed");
+    }
+    const float* d = (const float*)net->dmem;
+    WideDev& w = net->wd;
+    int i = 0;
+    w.F1 = d + off[i++]; w.F2 = d + off[i++]; w.F3 = d + off[i++]; w.F4 = d + off[i++];
+    w.B4 = d + off[i++]; w.B3h = d + off[i++]; w.B3e = d + off[i++]; w.B2 = d + off[i++]; w.B1e = d + off[i++];
+    w.Hz = d + off[i++]; w.bz = d + off[i++]; w.b2 = d + off[i++]; w.b4 = d + off[i++]; w.w5 = d + off[i++];
+    w.emb_tab = (const float4*)(d + off[i++]);
+    net->args.b5 = h.b5[0];
+    net->args.w0 = h.w0;
+    net->fingerprint = net_fingerprint(h);
+    net->host = std::move(h);
+    *out = net;
+    return SDFNMPC_OK;
+}
+
 static int upload_net(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
+    if (is_wide(h)) return upload_wide(ctx, std::move(h), out);
     const int Ein = h.E(), Lh = h.L;
     const float* W1 = h.W1.data();
     const float* W2 = h.W2.data();
@@ -435,17 +540,7 @@ static int upload_net(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     mark(); blob.insert(blob.end(), h.W5.begin(), h.W5.end());
     while (blob.size() % 4) blob.push_back(0.0f);
     mark();
-    for (int m = 0; m < NE; ++m) {
-        float v[4] = {0, 0, 0, 0};
-        int j = -1;
-        if (m >= 3 && m < 3 + EMB_NB) j = m - 3;
-        else if (m >= 3 + EMB_NB && m < E) j = m - 3 - EMB_NB;
-        if (j >= 0) {
-            const int d = j / EMB_NF, f = j % EMB_NF;
-            for (int c = 0; c < 3; ++c) v[c] = h.dirs[c * EMB_ND + d] * h.freqs[f];  // freq = 2^f: exact
-        }
-        blob.insert(blob.end(), v, v + 4);
-    }
+    emb_table(h, blob);
     for (size_t o : off)
         if (o % 4) return fail(SDFNMPC_E_FORMAT, "internal: misaligned packed operand");
 
@@ -486,15 +581,7 @@ static int upload_net(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     a.emb_tab = (const float4*)(d + off[i++]);
     a.b5 = h.b5[0];
     a.w0 = h.w0;
-    // fingerprint: FNV-1a over the parameters in torch order
-    uint64_t fp = 1469598103934665603ULL;
-    auto sh = param_shapes(h);
-    auto pl = param_list(h);
-    for (size_t t = 0; t < pl.size(); ++t) {
-        const unsigned char* b = (const unsigned char*)pl[t];
-        const size_t nb = (size_t)sh[t].first * sh[t].second * 4;
-        for (size_t q = 0; q < nb; ++q) fp = (fp ^ b[q]) * 1099511628211ULL;
-    }
+    const uint64_t fp = net_fingerprint(h);
     net->fingerprint = fp;
     net->host = std::move(h);
     *out = net;
@@ -563,6 +650,69 @@ static int run_sdf(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, con
     return SDFNMPC_OK;
 }
 
+// wide schedule (sdf_wide.hip): hoist, embedding, 4 forward + 5 backward GEMMs, final contraction.
+// Latent: fp32 [n_inst][L] (zf) or fp64 at a stride (zd, the stage parameters).  Geometry: pos4, or
+// x / p (then also the constraint epilogue when cons->h is set).
+static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, const float4* pos4, const float* zf,
+                    const double* zd, long long zstride, int n_inst, int rows_per_inst, float4* out4,
+                    const SdfArgs* cons) {
+    if (rows > 0x7fffffffLL / 2) return fail(SDFNMPC_E_ARG, "too many rows");
+    const HostNet& hn = net->host;
+    const WideDev& w = net->wd;
+    const int n1 = hn.n1, n2 = hn.n2, n3 = hn.n3, n4 = hn.n4, nz = n1 + n3, R = (int)rows;
+    const size_t per_row = 2 * NE + 2 * (size_t)(n1 + n2 + n3 + n4) + 2 * 128;
+    const size_t nfl = per_row * rows + (size_t)n_inst * (L + nz);
+    HIPCHK(ctx->wws.ensure(nfl * sizeof(float)));
+    float* q = (float*)ctx->wws.p;
+    auto take = [&](size_t n) { float* r = q; q += n; return r; };
+    float *Eb = take((size_t)R * NE), *Gb = take((size_t)R * NE);
+    float *H1 = take((size_t)R * n1), *D1 = take((size_t)R * n1), *H2 = take((size_t)R * n2), *D2 = take((size_t)R * n2);
+    float *H3 = take((size_t)R * n3), *D3 = take((size_t)R * n3), *H4 = take((size_t)R * n4), *D4 = take((size_t)R * n4);
+    float *GE3 = take((size_t)R * 128), *GE1 = take((size_t)R * 128);
+    float* z = take((size_t)n_inst * L);
+    float* c13 = take((size_t)n_inst * nz);
+    hipStream_t st = ctx->stream;
+    if (zd) {
+        HIPCHK(timed(ctx, "sdf_wide_hoist", [&] { return launch_wide_latent(zd, zstride, n_inst, z, st); }));
+        zf = z;
+    }
+    const float w0 = net->args.w0;
+    auto gemm = [&](const float* A1, int K1, const float* A2, int K2, const float* W, int M, int N, int epi,
+                    const float* bias, const float* c, const float* d, int ldd, float* o1, float* o2,
+                    const char* name) -> hipError_t {
+        WideGemmArgs g{};
+        g.A1 = A1; g.lda1 = K1; g.K1 = K1;
+        g.A2 = A2; g.lda2 = K2; g.K2 = K2;
+        g.W = W; g.M = M; g.N = N;
+        g.bias = bias; g.c = c; g.ldc = nz; g.rows_per_inst = rows_per_inst;
+        g.d = d; g.ldd = ldd; g.w5 = w.w5;
+        g.out1 = o1; g.ld1 = N; g.out2 = o2; g.ld2 = N; g.w0 = w0;
+        return timed(ctx, name, [&] { return launch_wide_gemm(g, epi, st); });
+    };
+    HIPCHK(gemm(zf, L, nullptr, 0, w.Hz, n_inst, nz, WIDE_EPI_STORE, w.bz, nullptr, nullptr, 0, c13, nullptr,
+                "sdf_wide_hoist"));
+    WideSdfArgs ea{};
+    ea.rows = R; ea.n4 = n4; ea.pos = pos4; ea.emb_tab = w.emb_tab; ea.E = Eb; ea.G = Gb;
+    if (cons) { ea.x = cons->x; ea.p = cons->p; ea.np = cons->np; ea.h = cons->h; ea.Jh = cons->Jh; ea.max_df = cons->max_df; }
+    HIPCHK(timed(ctx, "sdf_wide_emb", [&] { return launch_wide_emb(ea, st); }));
+    // forward: L1..L4
+    HIPCHK(gemm(Eb, NE, nullptr, 0, w.F1, R, n1, WIDE_EPI_SIN, nullptr, c13, nullptr, 0, H1, D1, "sdf_wide_gemm"));
+    HIPCHK(gemm(H1, n1, nullptr, 0, w.F2, R, n2, WIDE_EPI_SIN, w.b2, nullptr, nullptr, 0, H2, D2, "sdf_wide_gemm"));
+    HIPCHK(gemm(H2, n2, Eb, NE, w.F3, R, n3, WIDE_EPI_SIN, nullptr, c13 + n1, nullptr, 0, H3, D3, "sdf_wide_gemm"));
+    HIPCHK(gemm(H3, n3, nullptr, 0, w.F4, R, n4, WIDE_EPI_SIN_L4, w.b4, nullptr, nullptr, 0, H4, D4, "sdf_wide_gemm"));
+    // backward (deltas overwrite the consumed activations): delta3 -> H3, delta2 -> H2, delta1 -> H1
+    HIPCHK(gemm(D4, n4, nullptr, 0, w.B4, R, n3, WIDE_EPI_BWD, nullptr, nullptr, D3, n3, H3, nullptr, "sdf_wide_gemm"));
+    HIPCHK(gemm(H3, n3, nullptr, 0, w.B3h, R, n2, WIDE_EPI_BWD, nullptr, nullptr, D2, n2, H2, nullptr, "sdf_wide_gemm"));
+    HIPCHK(gemm(H3, n3, nullptr, 0, w.B3e, R, 128, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, GE3, nullptr,
+                "sdf_wide_gemm"));
+    HIPCHK(gemm(H2, n2, nullptr, 0, w.B2, R, n1, WIDE_EPI_BWD, nullptr, nullptr, D1, n1, H1, nullptr, "sdf_wide_gemm"));
+    HIPCHK(gemm(H1, n1, nullptr, 0, w.B1e, R, 128, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, GE1, nullptr,
+                "sdf_wide_gemm"));
+    ea.H4 = H4; ea.GE3 = GE3; ea.GE1 = GE1; ea.w5 = w.w5; ea.b5 = net->args.b5; ea.out = out4;
+    HIPCHK(timed(ctx, "sdf_wide_final", [&] { return launch_wide_final(ea, st); }));
+    return SDFNMPC_OK;
+}
+
 template <typename T>
 static int run_hoist(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const T* latent, long long stride, int n_inst,
                      float* c13) {
@@ -580,6 +730,12 @@ extern "C" int sdfnmpc_sdf_eval(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long l
     if (rows == 0) return SDFNMPC_OK;
     ScopedDevice sd(ctx->device);
     const int n_inst = (int)((rows + rows_per_inst - 1) / rows_per_inst);
+    if (net->wide) {
+        if (grad_latent)
+            return fail(SDFNMPC_E_UNSUPPORTED, "latent gradient (the 131-wide jac_sdf_l4c) is not built for wide networks");
+        return run_wide(ctx, net, rows, (const float4*)pos4, latent, nullptr, 0, n_inst, rows_per_inst, (float4*)out4,
+                        nullptr);
+    }
     HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
     int rc = run_hoist<float>(ctx, net, latent, L, n_inst, (float*)ctx->c13.p);
     if (rc) return rc;
@@ -644,7 +800,7 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
         sdf4 = (float4*)ctx->sdf4.p;
     }
     const int n_inst = a->latent_mode == 0 ? a->B : (int)rows;
-    HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
+    if (!net->wide) HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
     // dynamics / cost / FOV constraints (independent of the network): forked onto the low-priority
     // aux stream so they fill the CUs the SDF kernel leaves idle (its tail), joined at the end
     LinArgs la{};
@@ -667,10 +823,6 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
     if (ctx->lin_first && (rc = fork_lin())) return rc;
     // 2. latent hoisting (latent = p[.][17:] as fp32)
     const long long stride = a->latent_mode == 0 ? (long long)(a->N + 1) * a->np : (long long)a->np;
-    rc = run_hoist<double>(ctx, net, a->p + 17, stride, n_inst, (float*)ctx->c13.p);
-    if (rc) return rc;
-    if (!ctx->lin_first && (rc = fork_lin())) return rc;
-    // 3. network forward + position gradient, with the sdf row of h / J_h in its epilogue
     SdfArgs cons{};
     cons.x = a->x;
     cons.p = a->p;
@@ -678,6 +830,18 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
     cons.h = a->h;
     cons.Jh = a->Jh;
     cons.max_df = net->host.max_df;
+    if (net->wide) {  // layer-by-layer schedule, linearisation forked first so it overlaps the GEMMs
+        if (!ctx->lin_first && (rc = fork_lin())) return rc;
+        rc = run_wide(ctx, net, rows, nullptr, nullptr, a->p + 17, stride, n_inst, a->latent_mode == 0 ? a->N + 1 : 1,
+                      sdf4, &cons);
+        if (rc) return rc;
+        HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+        return SDFNMPC_OK;
+    }
+    rc = run_hoist<double>(ctx, net, a->p + 17, stride, n_inst, (float*)ctx->c13.p);
+    if (rc) return rc;
+    if (!ctx->lin_first && (rc = fork_lin())) return rc;
+    // 3. network forward + position gradient, with the sdf row of h / J_h in its epilogue
     rc = run_sdf(ctx, net, rows, nullptr, (const float*)ctx->c13.p,
                  a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows, &cons);
     if (rc) return rc;

@@ -72,6 +72,43 @@ constexpr int HOIST_ROWS = 32;                    // instances per hoist workgro
 constexpr int HOIST_COLS = 128;                   // output columns per hoist workgroup (4 waves x 32)
 constexpr int SZ = L + 4;                         // LDS row stride of the latent tile
 
+// ---- wide networks (layer sizes multiples of 128, e.g. C5's [1024,1024,512,256]): sdf_wide.hip
+enum { WIDE_EPI_SIN = 0, WIDE_EPI_SIN_L4 = 1, WIDE_EPI_BWD = 2, WIDE_EPI_STORE = 3 };
+
+// out[M x N] = [A1 | A2][M x (K1 + K2)] . W^T,  W [N][K1 + K2] row-major (K contiguous)
+struct WideGemmArgs {
+    const float* A1; int lda1, K1;
+    const float* A2; int lda2, K2;   // optional second K segment (A2 = NULL, K2 = 0)
+    const float* W;
+    int M, N;
+    const float* bias;               // [N] (SIN / SIN_L4 / STORE) or NULL
+    const float* c; int ldc;         // per-instance additive term c[m / rows_per_inst][n] (SIN), or NULL
+    int rows_per_inst;
+    const float* d; int ldd;         // BWD: cos(w0 a) of the layer
+    const float* w5;                 // SIN_L4: final-layer weights
+    float* out1; int ld1;            // SIN: sin(w0 a) | BWD: ((acc * d) * w0) | STORE: acc + bias
+    float* out2; int ld2;            // SIN: cos(w0 a) | SIN_L4: (w5 * cos(w0 a)) * w0
+    float w0;
+};
+
+struct WideSdfArgs {
+    int rows, n4, np;
+    const double* x; const double* p;  // Co_p_B from the iterate (or pos when x == NULL)
+    const float4* pos;
+    const float4* emb_tab;
+    float* E; float* G;               // [rows][NE]
+    const float* H4;                  // [rows][n4]
+    const float* GE3; const float* GE1;  // [rows][128]
+    const float* w5; float b5;
+    float4* out;                      // [rows] (df, d df / d pos) or NULL
+    double* h; double* Jh; double max_df;
+};
+
+hipError_t launch_wide_gemm(const WideGemmArgs& a, int epi, hipStream_t s);
+hipError_t launch_wide_latent(const double* lat, long long stride, int n_inst, float* z, hipStream_t s);
+hipError_t launch_wide_emb(const WideSdfArgs& a, hipStream_t s);
+hipError_t launch_wide_final(const WideSdfArgs& a, hipStream_t s);
+
 size_t sdf_lds_bytes(int M);
 hipError_t sdf_set_lds_limits();
 hipError_t launch_sdf_mlp(const SdfArgs& a, int M, bool latent_grad, hipStream_t s);

@@ -32,6 +32,8 @@ What is pinned to what:
                           Depth2Range from utils/preprocessing.py), weights from
                           sdf_nmpc_amd.vae.synthetic_encoder, images from synth.depth_images: latent
                           means in fp32 and fp64, sampled preprocessed pixels, per-stage channel sums.
+  * wide_golden.npz    -- the reference's own ``NeuralDF`` at config C5's widths [1024,1024,512,256]
+                          (SIREN-init seed 0): df and d df / d pos in fp32 and fp64.
   * params_golden.npz  -- the reference's own ``Nmpc.set_latent`` / ``Nmpc.set_ref`` /
                           ``Quad.formate_ref`` (controller.py:50-54,133-142, quad_rollpitchyawrate.py:
                           62-65) called unbound on small stand-in objects; ``Config`` from the
@@ -477,6 +479,26 @@ def ts_golden():
     print("ts_golden.npz", len(out))
 
 
+def wide_golden(n=128):
+    """The reference's own NeuralDF at config C5's widths [1024,1024,512,256] (SIREN-init, seed 0)."""
+    out = {}
+    rng = np.random.default_rng(4321)
+    spec = W.WIDE_SPEC
+    inp = sample_inputs(rng, n, spec.size_latent)
+    params = W.siren_weights(spec, seed=0)
+    out["input"] = inp
+    out["sha256"] = np.frombuffer(hashlib.sha256(W.pack(spec, params)).digest(), dtype=np.uint8)
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        net = ref_net(spec, params, dt)
+        x = torch.from_numpy(inp).to(dt).requires_grad_(True)
+        df = net(x)
+        (g,) = torch.autograd.grad(df.sum(), x)
+        out[f"df_{tag}"] = df.detach().numpy()[:, 0]
+        out[f"grad_{tag}"] = g.numpy()[:, :3]
+    np.savez_compressed(os.path.join(HERE, "wide_golden.npz"), **out)
+    print("wide_golden.npz", {k: v.shape for k, v in out.items()})
+
+
 def vae_golden():
     import copy as _copy
     from sdf_nmpc.network.vae import Encoder
@@ -537,6 +559,6 @@ def vae_golden():
 if __name__ == "__main__":
     only = sys.argv[1:]
     for name, fn in (("sdf", sdf_golden), ("lin", lin_golden), ("grid", grid_golden), ("params", params_golden),
-                     ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden)):
+                     ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden), ("wide", wide_golden)):
         if not only or name in only:
             fn()

@@ -108,9 +108,9 @@ def test_weight_blob_roundtrip_and_fingerprint(gpu_ctx):
     assert _lib.Net.siren(gpu_ctx, 1).fingerprint != a.fingerprint
     with pytest.raises(_lib.SdfnmpcError):
         _lib.Net.from_blob(gpu_ctx, b"SDFNMPCW" + b"\0" * 40)
-    wide = W.pack(W.WIDE_SPEC, W.siren_weights(W.WIDE_SPEC, 0))
+    odd = W.NetSpec(layer_sizes=(200, 200, 100, 50))  # neither the deployed nor a 128-multiple net
     with pytest.raises(_lib.SdfnmpcError, match="not built for"):
-        _lib.Net.from_blob(gpu_ctx, wide)
+        _lib.Net.from_blob(gpu_ctx, W.pack(odd, W.siren_weights(odd, 0)))
 
 
 def test_l4c_shim_casadi_calls(golden, tmp_path):

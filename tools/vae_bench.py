@@ -5,7 +5,8 @@ import time
 import numpy as np
 import torch
 
-sys.path.insert(0, ".")
+import os  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from sdf_nmpc_amd import _lib, synth  # noqa: E402
 from sdf_nmpc_amd import vae as V  # noqa: E402
 from sdf_nmpc_amd.config import Config  # noqa: E402
