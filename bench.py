@@ -59,7 +59,12 @@ def main():
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--prep-steps", type=int, default=50, help="timed preparation-only steps (0: skip)")
     ap.add_argument("--no-b1", action="store_true", help="skip the B=1 latency probe (profiling runs)")
+    ap.add_argument("--config", choices=("c3", "c5"), default="c3",
+                    help="c3: the headline 1024 x 40 RTI (default); c5: 4x-wide SDF MLP + in-loop VAE encode, "
+                         "N = 60, 4096 instances over 8 GPUs (512 per GPU)")
     args = ap.parse_args()
+    if args.config == "c5":
+        return main_c5(args)
 
     import torch
     import torch.distributed as dist
@@ -291,6 +296,150 @@ def main():
                                "frac": lin_gbs / HBM_PEAK_GBS, "bytes_per_launch": lin_b},
         "cpu_baseline": cpu,
         "prep": prep_out,
+    }
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_c5(args):
+    """BASELINE.json configs[4]: per control step and instance, a new 1x270x480 depth image is encoded by
+    the VAE (sdf_nmpc/vae.py:37-40) into the latent that parameterises the 4x-wide SDF
+    (set_latent, controller.py:50-54), then one SQP-RTI solve at N = 60 runs with that SDF.  Weak scaling:
+    512 instances per GPU (4096 over 8 GPUs)."""
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+    from sdf_nmpc_amd import _lib, shard, synth, vae as V, weights as W
+    from sdf_nmpc_amd.config import Config
+    from sdf_nmpc_amd.model import Quad
+
+    N = args.horizon if args.horizon != 40 else 60
+    B = args.batch if args.batch != 1024 else 512
+    if args.global_batch > 0:
+        lo, hi = shard.instance_range(args.global_batch, world, rank)
+        B = hi - lo
+    cfg = Config(mpc__N=N)
+    ctx = _lib.Context(local, stream=torch.cuda.current_stream(dev).cuda_stream)
+    blob = W.pack(W.WIDE_SPEC, W.siren_weights(W.WIDE_SPEC, seed=0)) if rank == 0 else None
+    vblob = V.pack(V.DEFAULT_ENCODER, V.synthetic_encoder(V.DEFAULT_ENCODER, 0)) if rank == 0 else None
+    if world > 1:
+        blob = shard.broadcast_blob(blob, dev)
+        vblob = shard.broadcast_blob(vblob, dev)
+    net = _lib.Net.from_blob(ctx, blob)
+    vae = _lib.Vae(ctx, vblob)
+    model = _lib.quad_model(cfg)
+    quad = Quad(cfg)
+    nodes, dt = _lib.shooting_grid(N, cfg.mpc.T)
+    prob = synth.make_problem(cfg, B, N, seed=1000 + rank, dt=dt)
+    bufs = {k: torch.from_numpy(np.ascontiguousarray(prob[k])).to(dev) for k in ("x", "u", "p", "dt")}
+    for k, sh in dict(xn=(B, N, 10), AB=(B, N, 14, 10), y=(B, N, 11), Jy=(B, N, 14, 11), yN=(B, 4),
+                      JyN=(B, 10, 4), h=(B, N + 1, 3), Jh=(B, N + 1, 10, 3)).items():
+        bufs[k] = torch.empty(sh, dtype=torch.float64, device=dev)
+    np_ = prob["p"].shape[-1]
+    x0 = prob["x"][:, 0] + np.random.default_rng(2000 + rank).normal(0, 0.05, (B, 10))
+    for k, v in dict(x0=x0, yref=prob["yref"], W=prob["W"], yNref=prob["yN"], WN=prob["WN"]).items():
+        bufs[k] = torch.from_numpy(np.ascontiguousarray(v)).to(dev)
+    for k, sh in dict(dx=(B, N + 1, 10), du=(B, N, 4), res=(B, 2)).items():
+        bufs[k] = torch.empty(sh, dtype=torch.float64, device=dev)
+    bufs["status"] = torch.empty(B, dtype=torch.int32, device=dev)
+    bufs["iters"] = torch.empty(B, dtype=torch.int32, device=dev)
+    u0 = torch.empty((B, 4), dtype=torch.float64, device=dev)
+    qopts = _lib.qp_opts(quad)
+    # depth images (resident in HBM), Depth2Range table, latents, camera pose at image time
+    imgs = torch.from_numpy(synth.depth_images(min(B, 16), 270, 480, seed=rank)).to(dev)
+    imgs = imgs.repeat((B + 15) // 16, 1, 1)[:B].contiguous()
+    yz = torch.from_numpy(V.depth2range_table(cfg.sensor.shape_imgs, cfg.sensor.hfov, cfg.sensor.vfov)).to(dev)
+    vopts = _lib.vae_opts(cfg, V.clip_scale(cfg))
+    lat32 = torch.empty((B, 128), dtype=torch.float32, device=dev)
+    lat64 = torch.empty((B, 128), dtype=torch.float64, device=dev)
+    W_p_Bo = torch.from_numpy(np.ascontiguousarray(prob["x"][:, 0, :3])).to(dev)
+    from sdf_nmpc_amd.model import quat2rot
+    W_R_Bo = torch.from_numpy(np.ascontiguousarray(quat2rot(prob["x"][:, 0, 3:7]).reshape(B, 9))).to(dev)
+    ropts = _lib.ref_opts(cfg, -1)
+    rargs = {"latent": lat64, "W_p_Bo": W_p_Bo, "W_R_Bo": W_R_Bo, "p": bufs["p"]}
+    x_init, u_init = bufs["x"].clone(), bufs["u"].clone()
+
+    def step():  # image -> latent -> p (set_latent) -> SQP-RTI solve from the initial iterate
+        _lib.vae_encode(ctx, vae, vopts, imgs, yz, lat32, lat64)
+        _lib.pack_refs(ctx, ropts, B, N, np_, 11, rargs, L=128)
+        bufs["x"].copy_(x_init)
+        bufs["u"].copy_(u_init)
+        _lib.linearize(ctx, net, model, B, N, np_, bufs)
+        _lib.qp_solve(ctx, qopts, B, N, bufs)
+        _lib.rti_apply(ctx, B, N, bufs["x"], bufs["u"], bufs["dx"], bufs["du"], u0)
+
+    def timed(fn, k):
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(k):
+            fn()
+        torch.cuda.synchronize(dev)
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        return shard.max_over_ranks(el, dev) if world > 1 else el
+
+    steps = args.steps if args.steps != 50 else 10
+    warm = args.warmup if args.warmup != 10 else 3
+    for _ in range(warm):
+        step()
+    el = timed(step, steps)
+    total = args.global_batch if args.global_batch > 0 else world * B
+    it = bufs["iters"].cpu().numpy()
+    st = bufs["status"].cpu().numpy()
+    ctx.enable_timing(True)
+    ctx.reset_stats()
+    reps = 5
+    for _ in range(reps):
+        step()
+    names = ("vae_pre", "vae_stem", "vae_conv", "vae_head", "sdf_wide_hoist", "sdf_wide_emb", "sdf_wide_gemm",
+             "sdf_wide_final", "linearize", "ref_pack", "rti_qp_pack", "rti_qp", "rti_apply")
+    kms = {k: ctx.kernel_stats(k)[0] / reps for k in names}  # ms per step (all launches of that name)
+    ctx.enable_timing(False)
+    spec = V.DEFAULT_ENCODER
+    vae_flop = spec.n_flops() * B
+    conv_flop = vae_flop - 2 * B * (135 * 240 * 64 * 49 + 2048 * 128)
+    rows = B * (N + 1)
+    wide_flop = rows * 7_326_976 + B * 2 * 128 * (1024 + 512)
+    vae_ms = sum(kms[k] for k in ("vae_pre", "vae_stem", "vae_conv", "vae_head"))
+    wide_ms = sum(kms[k] for k in ("sdf_wide_hoist", "sdf_wide_emb", "sdf_wide_gemm", "sdf_wide_final"))
+    conv_tf = conv_flop / (kms["vae_conv"] * 1e-3) / 1e12
+    wide_tf = (wide_flop - B * 2 * 128 * 1536) / (kms["sdf_wide_gemm"] * 1e-3) / 1e12
+    out = {
+        "metric": "NMPC solves/sec, config C5: 4x-wide SDF MLP + in-loop VAE encode, N=60, batch 4096 over 8 GPUs",
+        "value": total * steps / el,
+        "unit": "instance-RTI-solves/s (incl. VAE encode)",
+        "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": el / steps * 1e3,
+        "higher_is_better": True, "scaling": "strong" if args.global_batch > 0 else "weak", "vs_baseline": None,
+        "dtype": "f32 (VAE convs, wide SDF MLP on MFMA) + f64 (linearisation, QP)",
+        "data": "synthetic depth images (seeded scenes + noise), synthetic VAE weights, SIREN-init wide SDF seed 0",
+        "config": {"workload": f"C5: batch={B} instances per GPU x N={N}; per step: VAE encode of B 1x270x480 depth "
+                               "images -> latent -> p, then one SQP-RTI solve with the [1024,1024,512,256] SDF",
+                   "global_batch": total, "horizon": N, "parallelism": f"instances sharded over {world} GPU(s)"},
+        "qp_iters_mean": float(it.mean()), "qp_iters_max": int(it.max()), "qp_converged_frac": float((st == 0).mean()),
+        "kernel_ms_per_step": kms,
+        "roofline": {"bound": "mfma", "kernel": "vae_conv (11 launches)", "achieved": conv_tf,
+                     "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": conv_tf / FP32_MFMA_PEAK_TFLOPS,
+                     "traffic": None, "flop_per_step": conv_flop},
+        "roofline_wide_sdf": {"bound": "mfma", "kernel": "sdf_wide_gemm (9 launches)", "achieved": wide_tf,
+                              "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": wide_tf / FP32_MFMA_PEAK_TFLOPS},
+        "vae_ms": vae_ms, "wide_sdf_ms": wide_ms,
+        "cpu_baseline": None,
     }
     if rank == 0:
         print(json.dumps(out))
