@@ -181,23 +181,46 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubl
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------------
-// Stage records, one block per (instance, node): AB, c = xn_k - xbar_{k+1}, g = s_k J^T W r,
-// C^T = J_h^T, H = s_k J^T W J + lm I (upper); terminal: H_N = J_N^T W_N J_N + lm I (10x10 upper in the
-// H field), g_N (first 10 of g), C_N.
-__global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
+// Stage records, one wavefront per (instance, node), four nodes per workgroup: AB, c = xn_k - xbar_{k+1},
+// g = s_k J^T W r, C^T = J_h^T, H = s_k J^T W J + lm I (upper); terminal: H_N = J_N^T W_N J_N + lm I
+// (10x10 upper in the H field), g_N (first 10 of g), C_N.  Lane e writes record entries e, e + 64, ...
+// (coalesced); the upper-triangle positions come from a constant table instead of a search.
+struct PackTri {
+    unsigned char a14[105], c14[105], a10[55], c10[55];
+};
+constexpr PackTri make_tri() {
+    PackTri t{};
+    int q = 0;
+    for (int a = 0; a < 14; ++a)
+        for (int c = a; c < 14; ++c, ++q) t.a14[q] = (unsigned char)a, t.c14[q] = (unsigned char)c;
+    q = 0;
+    for (int a = 0; a < 10; ++a)
+        for (int c = a; c < 10; ++c, ++q) t.a10[q] = (unsigned char)a, t.c10[q] = (unsigned char)c;
+    return t;
+}
+__constant__ PackTri c_tri = make_tri();
+
+constexpr int PACK_NODES = 4;  // wavefronts (nodes) per workgroup
+
+__global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) {
     const int N = A.N, N1 = N + 1;
-    const int b = blockIdx.x / N1, k = blockIdx.x - b * N1;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int node = blockIdx.x * PACK_NODES + wv;
+    if (node >= A.B * N1) return;  // whole wavefronts only: no workgroup barrier below
+    const int b = node / N1, k = node - b * N1;
     double* Rk = A.work + (size_t)b * qp_work_doubles(N) + (size_t)k * REC;
     const double* Jh = A.Jh + ((size_t)b * N1 + k) * 30;
-    __shared__ double Js[14 * 12], Ws[12], rs[12];  // J_y as [14][ny], weights x s_k, residuals
+    __shared__ double Js_[PACK_NODES][14 * 12], Ws_[PACK_NODES][12], rs_[PACK_NODES][12];  // J_y [14][ny], s_k W, r
+    double* Js = Js_[wv];
+    double* Ws = Ws_[wv];
+    double* rs = rs_[wv];
     const int ny = A.ny;
     if (k < N) {
         const size_t bk = (size_t)b * N + k;
         const double sk = A.cost_scaling ? A.dt[k] : 1.0;
-        for (int e = threadIdx.x; e < 154; e += 256) Js[(e / 11) * ny + e % 11] = A.Jy[bk * 154 + e];
-        if (threadIdx.x < ny) {
-            const int i = threadIdx.x;
-            Ws[i] = sk * A.W[bk * ny + i];
+        for (int e = lane; e < 154; e += 64) Js[(e / 11) * ny + e % 11] = A.Jy[bk * 154 + e];
+        if (lane < ny) {
+            const int i = lane;
             double y;
             if (i < 11) {
                 y = A.y[bk * 11 + i];
@@ -205,33 +228,45 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
                 const double t = 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2];
                 y = t * t * t * t;
             }
+            Ws[i] = sk * A.W[bk * ny + i];
             rs[i] = y - A.yref[bk * ny + i];
         }
-        if (ny == 12 && threadIdx.x < 14) {  // d/dw of the sdf cost: -2 (1 - s/2)^3 J_h[2] on the state part
-            const int a = threadIdx.x;
+        if (ny == 12 && lane < 14) {  // d/dw of the sdf cost: -2 (1 - s/2)^3 J_h[2] on the state part
+            const int a = lane;
             const double t = 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2];
             Js[a * 12 + 11] = a < 10 ? -2.0 * t * t * t * Jh[a * 3 + 2] : 0.0;
         }
-        __syncthreads();
+        wave_sync();
         const double* AB = A.AB + bk * 140;
         const double* xn = A.xn + bk * 10;
         const double* xb1 = A.x + ((size_t)b * N1 + k + 1) * 10;
-        for (int e = threadIdx.x; e < REC; e += 256) {
-            double v = 0.0;
+        // e = lane, lane + 64: [A B]; lane + 128: AB tail | c | g | C^T; lane + 192, + 256: C^T tail | H | 0
+        Rk[lane] = AB[lane];
+        Rk[64 + lane] = AB[64 + lane];
+        {
+            const int e = 128 + lane;
+            double v;
             if (e < R_C) {
                 v = AB[e];
             } else if (e < R_G) {
                 v = xn[e - R_C] - xb1[e - R_C];
             } else if (e < R_CT) {
                 const int a = e - R_G;
+                v = 0.0;
                 for (int i = 0; i < ny; ++i) v += Js[a * ny + i] * Ws[i] * rs[i];
-            } else if (e < R_H) {  // C^T: row j = d h_j / d x
+            } else {
+                const int q = e - R_CT, j = q / 10;
+                v = Jh[(q - 10 * j) * 3 + j];
+            }
+            Rk[e] = v;
+        }
+        for (int e = 192 + lane; e < REC; e += 64) {
+            double v = 0.0;
+            if (e < R_H) {
                 const int q = e - R_CT, j = q / 10;
                 v = Jh[(q - 10 * j) * 3 + j];
             } else if (e < R_H + 105) {
-                int q = e - R_H, a = 0;
-                while (q >= 14 - a) { q -= 14 - a; ++a; }
-                const int c = a + q;
+                const int a = c_tri.a14[e - R_H], c = c_tri.c14[e - R_H];
                 for (int i = 0; i < ny; ++i) v += Js[a * ny + i] * Ws[i] * Js[c * ny + i];
                 v += (a == c ? A.lm : 0.0);
             }
@@ -242,7 +277,7 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
         const double* Wn = A.WN + (size_t)b * 4;
         const double* yn = A.yN + (size_t)b * 4;
         const double* rn = A.yNref + (size_t)b * 4;
-        for (int e = threadIdx.x; e < REC; e += 256) {
+        for (int e = lane; e < REC; e += 64) {
             double v = 0.0;
             if (e >= R_G && e < R_G + 10) {
                 const int a = e - R_G;
@@ -251,9 +286,7 @@ __global__ __launch_bounds__(256) void rti_qp_pack_kernel(QpArgs A) {
                 const int q = e - R_CT, j = q / 10;
                 v = Jh[(q - 10 * j) * 3 + j];
             } else if (e >= R_H && e < R_H + 55) {
-                int q = e - R_H, a = 0;
-                while (q >= 10 - a) { q -= 10 - a; ++a; }
-                const int c = a + q;
+                const int a = c_tri.a10[e - R_H], c = c_tri.c10[e - R_H];
                 for (int i = 0; i < 4; ++i) v += J[a * 4 + i] * Wn[i] * J[c * 4 + i];
                 v += (a == c ? A.lm : 0.0);
             }
@@ -955,7 +988,8 @@ hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx
 
 hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    hipLaunchKernelGGL(rti_qp_pack_kernel, dim3((unsigned)(a.B * (a.N + 1))), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(rti_qp_pack_kernel, dim3((unsigned)((a.B * (a.N + 1) + PACK_NODES - 1) / PACK_NODES)),
+                       dim3(64 * PACK_NODES), 0, s, a);
     return hipGetLastError();
 }
 
