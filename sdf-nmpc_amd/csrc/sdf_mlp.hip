@@ -28,7 +28,12 @@ namespace sdfn {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
+#ifdef SDF_NO_MFMA  // diagnostic build (tools/build_variant.sh): the kernel's time without its matrix work
+    c[0] = fmaf(a, b, c[0]);
+    return c;
+#else
     return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+#endif
 }
 
 // Row held by accumulator register `reg` of lane half `h` (32x32 f32 MFMA C/D layout, gfx950).

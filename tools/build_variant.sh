@@ -1,0 +1,16 @@
+#!/bin/bash
+# Diagnostic builds of libsdfnmpc.so with extra defines into _build/<name>/ (never the product library):
+#   tools/build_variant.sh nomfma -DSDF_NO_MFMA
+set -euo pipefail
+name=$1; shift
+R=$(cd "$(dirname "$0")/.." && pwd)
+O=$R/_build/$name
+mkdir -p $O
+cd $R/sdf-nmpc_amd/csrc
+for f in sdf_mlp sdf_wide linearize rti_qp ref_pack vae_enc; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function "$@" -c $f.hip -o $O/$f.o &
+done
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" -c engine.cpp -o $O/engine.o &
+wait
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o $O/libsdfnmpc.so $O/*.o
+echo $O/libsdfnmpc.so

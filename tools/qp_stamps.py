@@ -37,4 +37,4 @@ with open(path, "wb") as f:
         f.write(np.ascontiguousarray(t[k].double().cpu().numpy()).tobytes())
     f.write(np.concatenate([model.lbu, model.ubu, model.lh, model.uh, model.zl, model.Zl, [10.0, 1e-8]]).astype(np.float64).tobytes())
 del t; torch.cuda.synchronize()
-sys.exit(subprocess.call([os.path.join(ROOT, "tools", "_qp_stamps_drv"), path]))
+sys.exit(subprocess.call([os.path.join(ROOT, "tools", "_qp_stamps_drv" + os.environ.get("DRV", "")), path]))
