@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define SDFNMPC_ABI_VERSION 3
+#define SDFNMPC_ABI_VERSION 4
 
 enum {
     SDFNMPC_OK = 0,
@@ -95,10 +95,13 @@ typedef struct {
     double lm;             /* levenberg_marquardt (ocp.py:120, mpc.lm_reg) */
     int cost_scaling;      /* 1: stage cost and slack penalties x dt_k, terminal x 1 (acados default) */
     int max_iter;          /* qp_solver_iter_max (ocp.py:115) */
-    double tol;            /* IPM stop: mean complementarity and max primal residual below tol */
+    double tol;            /* IPM stop: max complementarity max_i t_i lambda_i and max primal residual below
+                              tol (HPIPM's res_m / res_b tests) */
     int ny;                /* stage residuals: 11, or 12 with flags.sdf_cost (gen_model.py:65-66): the 12th,
                               (1 - s/2)^4 of the flagged SDF value s = h[2], and its Jacobian
                               -2 (1 - s/2)^3 J_h[2] are formed from h / J_h by the QP (yref, W: [B][N][ny]) */
+    int lm_scaling;        /* 1: Levenberg-Marquardt term lm dt_k at stages k < N and lm at N (acados adds
+                              Ts[k] * levenberg_marquardt); 0: lm at every node */
 } sdfnmpc_qp_opts;
 
 /* Batched QP of the RTI feedback phase, built from sdfnmpc_linearize outputs. */
@@ -116,9 +119,11 @@ typedef struct {
     double* dx;          /* [B][N+1][10] solution: the RTI step */
     double* du;          /* [B][N][4] */
     double* slack;       /* [B][N+1][3][2] optional: (sl, su) of the soft rows */
-    int* status;         /* [B] optional: 0 converged, 1 max_iter reached */
+    int* status;         /* [B] optional: 0 converged, 1 max_iter reached (acados status 2: the step is
+                            kept), 2 numerical failure -- a NaN / Inf in the data (acados QP failure,
+                            status 4: sdfnmpc_rti_apply given this array keeps the instance's iterate) */
     int* iters;          /* [B] optional */
-    double* res;         /* [B][2] optional: (mean complementarity, max primal residual) */
+    double* res;         /* [B][2] optional: (max complementarity, max primal residual) */
 } sdfnmpc_qp_args;
 
 /* Batched reference / parameter packing: RefGen (ref_gen.py:17-130) ->
@@ -205,9 +210,10 @@ int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_qu
 
 /* ---- batched QP (feedback phase) and the RTI step ---- */
 int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* opts, const sdfnmpc_qp_args* args);
-/* x[B][N+1][10] += dx, u[B][N][4] += du, u0[B][4] = u[:, 0] (u0 may be NULL) */
+/* x[B][N+1][10] += dx, u[B][N][4] += du, u0[B][4] = u[:, 0] (u0 may be NULL).  status [B] (may be NULL):
+ * instances with status >= 2 (QP failure) keep x and u; their u0 is the unchanged u[:, 0]. */
 int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, const double* dx, const double* du,
-                      double* u0);
+                      double* u0, const int* status);
 
 /* ---- batched reference / parameter packing into the OCP device buffers (sdfnmpc_ref_args) ---- */
 int sdfnmpc_pack_refs(sdfnmpc_ctx* ctx, const sdfnmpc_ref_opts* opts, const sdfnmpc_ref_args* args);

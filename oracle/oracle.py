@@ -168,7 +168,12 @@ def linearize_batch(m, net, x, u, p, dt, nthreads=1):
 QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", "W", "yNref", "WN")
 
 
-def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_scaling=True, nthreads=1):
+# IPM starting point / step fraction of csrc/rti_qp.hip (QP_T0, QP_L0, QP_LC, QP_TAU_LO, QP_TAU_HI)
+QP_START = dict(t0=0.5, l0=1.0, lc=0.5, tau_lo=0.995, tau_hi=0.995)
+
+
+def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_scaling=True, nthreads=1, lm_scaling=True,
+                 start=None):
     """Structured Riccati IPM (qp_ipm.c) over a batch: the CPU restatement of the feedback-phase QP.
 
     lin: linearisation outputs (xn, AB, y, Jy, yN, JyN, h, Jh) with a leading batch dimension;
@@ -179,7 +184,8 @@ def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_sca
     arrs.update(x=prob["x"], u=prob["u"], x0=x0, yref=prob["yref"], W=prob["W"], yNref=prob["yN"], WN=prob["WN"])
     arrs = {k: np.ascontiguousarray(arrs[k], dtype=np.float64) for k in QP_IN}
     dt = np.ascontiguousarray(prob["dt"], dtype=np.float64)
-    opts = np.concatenate([model.lbu, model.ubu, model.lh, model.uh, model.zl, model.Zl, [lm, tol]]).astype(np.float64)
+    opts = np.concatenate([model.lbu, model.ubu, model.lh, model.uh, model.zl, model.Zl, [lm, tol, float(bool(lm_scaling))],
+                           [v for v in {**QP_START, **(start or {})}.values()]]).astype(np.float64)
     out = dict(dx=np.zeros((B, N + 1, 10)), du=np.zeros((B, N, 4)), slack=np.zeros((B, N + 1, 3, 2)),
                iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32), res=np.zeros((B, 2)))
     d = C.c_double

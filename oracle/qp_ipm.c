@@ -12,8 +12,9 @@
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg call it.
  *
  * QP of one instance (w_k = [dx_k; du_k]; s_k = dt_k for k < N with cost scaling, else 1; s_N = 1):
- *   min  sum_{k<N} s_k 1/2 |J_y,k w_k + r_k|^2_{W_k} + lm/2 |w_k|^2 + s_N 1/2 |J_yN dx_N + r_N|^2_{W_N}
+ *   min  sum_{k<N} s_k 1/2 |J_y,k w_k + r_k|^2_{W_k} + lm_k/2 |w_k|^2 + s_N 1/2 |J_yN dx_N + r_N|^2_{W_N}
  *        + lm/2 |dx_N|^2 + sum_{k<=N} s_k (zl.sl_k + Zl/2 sl_k^2 + zl.su_k + Zl/2 su_k^2)
+ *   lm_k = lm dt_k with lm_scaling (acados adds Ts[k] * levenberg_marquardt for k < N), else lm
  *   s.t. dx_0 = x0 - xbar_0,  dx_{k+1} = A_k dx_k + B_k du_k + (xn_k - xbar_{k+1})
  *        u_k + du_k in [lbu, ubu];  lh - sl_k <= h_k + C_k dx_k <= uh + su_k;  sl, su >= 0
  * Inputs use the sdfnmpc_linearize layouts (include/sdfnmpc.h): AB [N][14][10] with AB[j][i] =
@@ -27,7 +28,8 @@ enum { NX = 10, NU = 4, NS = 3, NW = 14 };
 
 typedef struct {
     double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3], lm, tol;
-    int max_iter, cost_scaling;
+    int max_iter, cost_scaling, lm_scaling;
+    double t0, l0, lc, tau_lo, tau_hi;  /* starting point / step fraction (rti_qp.hip's QP_T0 ... QP_TAU_HI) */
 } qp_opts_c;
 
 typedef struct {                  /* stage k < N, or the terminal node k = N (x part only) */
@@ -115,8 +117,12 @@ static int lqr(ipm_t* Q, const double* sig, const double* v, double* dx, double*
             const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
             const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
             const double gl = zs - v[r0] - v[r0 + 2], gu = zs - v[r0 + 1] - v[r0 + 3];
-            const double fw = sig[r0] * (Hl - sig[r0]) / Hl + sig[r0 + 1] * (Hu - sig[r0 + 1]) / Hu;
-            const double fg = -(v[r0] + sig[r0] * gl / Hl) + (v[r0 + 1] + sig[r0 + 1] * gu / Hu);
+            /* written without the cancellation of Hl - sig (sig -> inf on an active row); equal to
+             * sig (Hl - sig) / Hl and -(v + sig gl / Hl) + ... */
+            (void)gl; (void)gu;
+            const double fw = sig[r0] * (Zs + sig[r0 + 2]) / Hl + sig[r0 + 1] * (Zs + sig[r0 + 3]) / Hu;
+            const double fg = -(v[r0] * (Zs + sig[r0 + 2]) + sig[r0] * (zs - v[r0 + 2])) / Hl +
+                              (v[r0 + 1] * (Zs + sig[r0 + 3]) + sig[r0 + 1] * (zs - v[r0 + 3])) / Hu;
             for (int a = 0; a < NX; ++a) {
                 for (int b = 0; b < NX; ++b) Qx[a * NX + b] += fw * S->C[j][a] * S->C[j][b];
                 qx[a] += fg * S->C[j][a];
@@ -177,18 +183,57 @@ static int lqr(ipm_t* Q, const double* sig, const double* v, double* dx, double*
         for (int i = 0; i < NU; ++i) kf[i] = r[i];
         chol_solve(NU, Rm, kf);
         for (int i = 0; i < NU; ++i) kf[i] = -kf[i];
-        /* P = Q + A^T P A + S^T K,  p = q + A^T (P c + p) + S^T k_ff */
-        for (int a = 0; a < NX; ++a) {
-            for (int b = 0; b < NX; ++b) {
-                double s = Qx[a * NX + b];
-                for (int l = 0; l < NX; ++l) s += S->A[l][a] * PA[l * NX + b];
-                for (int i = 0; i < NU; ++i) s += Sm[i * NX + a] * Kk[i * NX + b];
-                Pk[a * NX + b] = s;
+        {   /* P = [I;K]^T Hh [I;K] + Ab^T P1 Ab (sum of PSD terms), Ab = A + B K */
+            double Ab[NX * NX], R0[NU * NU], S0[NU * NX], ru[NU], PB1[NX];
+            for (int i = 0; i < NU; ++i) {
+                for (int j = 0; j < NU; ++j) R0[i * NU + j] = S->H[NX + i][NX + j];
+                R0[i * NU + i] += sig[8 * k + i] + sig[8 * k + 4 + i];
+                for (int b = 0; b < NX; ++b) S0[i * NX + b] = S->H[NX + i][b];
+                ru[i] = S->g[NX + i] - v[8 * k + i] + v[8 * k + 4 + i];
             }
-            double s = qx[a];
-            for (int l = 0; l < NX; ++l) s += S->A[l][a] * Pc[l];
-            for (int i = 0; i < NU; ++i) s += Sm[i * NX + a] * kf[i];
-            pk[a] = s;
+            for (int a = 0; a < NX; ++a)
+                for (int b = 0; b < NX; ++b) {
+                    double s = S->A[a][b];
+                    for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * Kk[i * NX + b];
+                    Ab[a * NX + b] = s;
+                }
+            double xb[NX];  /* B kf + c */
+            for (int a = 0; a < NX; ++a) {
+                double s = S->c[a];
+                for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * kf[i];
+                xb[a] = s;
+            }
+            for (int a = 0; a < NX; ++a) {
+                double s = p1[a];
+                for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * xb[l];
+                PB1[a] = s;
+            }
+            double PAb[NX * NX];
+            for (int a = 0; a < NX; ++a)
+                for (int b = 0; b < NX; ++b) {
+                    double s = 0.0;
+                    for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * Ab[l * NX + b];
+                    PAb[a * NX + b] = s;
+                }
+            double KR[NX * NU];  /* S0^T + K^T R0 : [NX][NU] */
+            for (int a = 0; a < NX; ++a)
+                for (int j = 0; j < NU; ++j) {
+                    double s = S0[j * NX + a];
+                    for (int i = 0; i < NU; ++i) s += Kk[i * NX + a] * R0[i * NU + j];
+                    KR[a * NU + j] = s;
+                }
+            for (int a = 0; a < NX; ++a) {
+                for (int b = 0; b < NX; ++b) {
+                    double s = Qx[a * NX + b];
+                    for (int l = 0; l < NX; ++l) s += Ab[l * NX + a] * PAb[l * NX + b];
+                    for (int j = 0; j < NU; ++j) s += KR[a * NU + j] * Kk[j * NX + b] + Kk[j * NX + a] * S0[j * NX + b];
+                    Pk[a * NX + b] = s;
+                }
+                double s = qx[a];
+                for (int i = 0; i < NU; ++i) s += Kk[i * NX + a] * ru[i] + KR[a * NU + i] * kf[i];
+                for (int l = 0; l < NX; ++l) s += Ab[l * NX + a] * PB1[l];
+                pk[a] = s;
+            }
         }
     }
     /* forward: dx_0 fixed, du = K dx + k_ff, dx+ = A dx + B du + c; slacks from the eliminated rows */
@@ -294,7 +339,7 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
                 for (int j = 0; j < NW; ++j) {
                     double hs = 0.0;
                     for (int a = 0; a < ny; ++a) hs += J[i][a] * Ws[a] * J[j][a];
-                    S->H[i][j] = hs + (i == j ? o->lm : 0.0);
+                    S->H[i][j] = hs + (i == j ? (o->lm_scaling ? o->lm * dtv[k] : o->lm) : 0.0);
                 }
             }
             for (int i = 0; i < NU; ++i) {
@@ -316,7 +361,8 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     }
     for (int i = 0; i < NX; ++i) Q.x0[i] = x0[i] - x[i];
 
-    /* ---- starting point: dynamics-feasible with du = sl = su = 0; t = max(row, 1), lambda = 3 */
+    /* ---- starting point (rti_qp.hip's): dynamics-feasible with du = sl = su = 0; t = max(row, 0.7);
+     * lambda = 0.5 on box rows, max(0.5, 0.5 s_k zl_j) on the rows of soft group (k, j) */
     memcpy(zdx, Q.x0, sizeof(double) * NX);
     for (int k = 0; k < N; ++k)
         for (int a = 0; a < NX; ++a) {
@@ -325,12 +371,18 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
             zdx[(k + 1) * NX + a] = s;
         }
     rows_at(&Q, zdx, zdu, zsl, zsu, rv);
-    double rp = 0.0, mu = 0.0;
+    double rp = 0.0, mu = 0.0, cm = 0.0;  /* mean / max complementarity; stop on max (HPIPM's res_m) */
     for (int r = 0; r < m; ++r) {
-        t[r] = rv[r] > 1.0 ? rv[r] : 1.0;
-        lam[r] = 3.0;
+        t[r] = rv[r] > o->t0 ? rv[r] : o->t0;
+        lam[r] = o->l0;
+        if (r >= 8 * N) {
+            const int q = r - 8 * N, k = q / 12, j = (q - 12 * k) >> 2;
+            const double lj = o->lc * Q.st[k].s * o->zl[j];
+            if (lj > lam[r]) lam[r] = lj;
+        }
         if (fabs(rv[r] - t[r]) > rp) rp = fabs(rv[r] - t[r]);
         mu += t[r] * lam[r];
+        if (t[r] * lam[r] > cm) cm = t[r] * lam[r];
     }
     mu /= m;
     /* row constants d (rows at z = 0) for v = sig (t - d) */
@@ -341,7 +393,8 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         free(zero);
     }
     int it = 0, fail = 0;
-    while (!(mu < o->tol && rp < o->tol) && it < o->max_iter) {
+    double gap = 1.0;  /* prod (1 - alpha): the decay of the stationarity residual of the start point */
+    while (!(cm < o->tol && rp < o->tol && gap < o->tol) && it < o->max_iter && isfinite(mu + rp)) {
         /* predictor */
         for (int r = 0; r < m; ++r) {
             sig[r] = lam[r] / t[r];
@@ -357,7 +410,10 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         double mua = 0.0;
         for (int r = 0; r < m; ++r) mua += (t[r] + aa * dta[r]) * (lam[r] + aa * dla[r]);
         mua /= m;
-        const double sigmu = (mua / mu) * (mua / mu) * (mua / mu) * mu;
+        /* Mehrotra's centring target, floored at 1e-2 tol (HPIPM's tau_min): rows are never pushed below
+         * the complementarity the stop test needs, which keeps lambda / t -- and the Riccati data -- bounded */
+        double sigmu = (mua / mu) * (mua / mu) * (mua / mu) * mu;
+        if (sigmu < 1e-2 * o->tol) sigmu = 1e-2 * o->tol;
         /* corrector */
         for (int r = 0; r < m; ++r) v[r] = sig[r] * (t[r] - d0[r]) - (dta[r] * dla[r] - sigmu) / t[r];
         if (lqr(&Q, sig, v, cdx, cdu, csl, csu)) { fail = 1; break; }
@@ -366,18 +422,25 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
             dtc[r] = rv[r] - t[r];
             dlc[r] = -sig[r] * dtc[r] - lam[r] - (dta[r] * dla[r] - sigmu) / t[r];
         }
-        double al = 0.995 * step_max(m, t, lam, dtc, dlc);
+        double tau = 1.0 - mu;  /* step fraction min(tau_hi, max(tau_lo, 1 - mu)) */
+        if (tau < o->tau_lo) tau = o->tau_lo;
+        if (tau > o->tau_hi) tau = o->tau_hi;
+        double al = tau * step_max(m, t, lam, dtc, dlc);
         if (al > 1.0) al = 1.0;
         mu = 0.0;
+        cm = 0.0;
         for (int r = 0; r < m; ++r) {
             t[r] += al * dtc[r];
             lam[r] += al * dlc[r];
             mu += t[r] * lam[r];
+            if (t[r] * lam[r] > cm) cm = t[r] * lam[r];
         }
         mu /= m;
         for (int e = 0; e < nz; ++e) zs[e] += al * (zs[2 * nz + e] - zs[e]);
         rp *= (1.0 - al);
+        gap *= (1.0 - al);
         ++it;
+
     }
     memcpy(dx, zdx, sizeof(double) * N1 * NX);
     memcpy(du, zdu, sizeof(double) * N * NU);
@@ -386,14 +449,15 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
             slack[2 * e] = zsl[e];
             slack[2 * e + 1] = zsu[e];
         }
-    *conv = !fail && mu < o->tol && rp < o->tol;
-    if (res) { res[0] = mu; res[1] = rp; }
+    if (!isfinite(mu + rp)) fail = 1;
+    *conv = fail ? -1 : (cm < o->tol && rp < o->tol && gap < o->tol);
+    if (res) { res[0] = cm; res[1] = rp; }
     free(d0); free(buf); free(Q.st); free(Q.P); free(Q.p); free(Q.K); free(Q.kf);
     return it;
 }
 
-/* Batched entry point (OpenMP over instances).  opts: lbu 4, ubu 4, lh 3, uh 3, zl 3, Zl 3, lm, tol.
- * status: 0 converged, 1 max_iter / failure (rti_qp.hip's convention). */
+/* Batched entry point (OpenMP over instances).  opts: lbu 4, ubu 4, lh 3, uh 3, zl 3, Zl 3, lm, tol,
+ * lm_scaling, then the IPM start / step parameters t0, l0, lc, tau_lo, tau_hi.  status (rti_qp.hip's convention): 0 converged, 1 max_iter, 2 numerical failure. */
 void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const double* y, const double* Jy,
                       const double* yN, const double* JyN, const double* h, const double* Jh, const double* x,
                       const double* u, const double* x0, const double* yref, const double* W, const double* yNref,
@@ -408,6 +472,8 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
     memcpy(o.Zl, opts + 17, 3 * sizeof(double));
     o.lm = opts[20];
     o.tol = opts[21];
+    o.lm_scaling = opts[22] != 0.0;
+    o.t0 = opts[23]; o.l0 = opts[24]; o.lc = opts[25]; o.tau_lo = opts[26]; o.tau_hi = opts[27];
     o.max_iter = max_iter;
     o.cost_scaling = cost_scaling;
     const int N1 = N + 1;
@@ -421,6 +487,6 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
                              W + (size_t)b * N * ny, yNref + (size_t)b * 4, WN + (size_t)b * 4, dt, &o, ny,
                              dx + (size_t)b * N1 * NX, du + (size_t)b * N * NU,
                              slack ? slack + (size_t)b * N1 * NS * 2 : NULL, &conv, res ? res + 2 * b : NULL);
-        status[b] = conv ? 0 : 1;
+        status[b] = conv < 0 ? 2 : conv ? 0 : 1;
     }
 }

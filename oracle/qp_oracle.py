@@ -4,7 +4,7 @@ The QP is the one acados builds in the RTI preparation phase and HPIPM solves in
 (sdf_nmpc/ocp.py:54-120: NONLINEAR_LS + GAUSS_NEWTON, levenberg_marquardt = mpc.lm_reg, ERK, soft
 nonlinear constraints idxsh with L1/L2 slack penalties, input box constraints, x_0 fixed):
 
-  min  sum_{k<N} s_k [ 1/2 |J_y,k w_k + r_k|^2_{W_k} ] + 1/2 lm |w_k|^2
+  min  sum_{k<N} s_k [ 1/2 |J_y,k w_k + r_k|^2_{W_k} ] + 1/2 lm_k |w_k|^2   (lm_k = lm dt_k, see stage_qp)
      + s_N 1/2 |J_yN dx_N + r_N|^2_{W_N} + 1/2 lm |dx_N|^2
      + sum_{k<=N} s_k (zl.sl_k + 1/2 Zl.sl_k^2 + zu.su_k + 1/2 Zu.su_k^2)
   s.t. dx_0 = x0 - xbar_0,  dx_{k+1} = A_k dx_k + B_k du_k + (xn_k - xbar_{k+1})
@@ -20,7 +20,7 @@ pins it independently of the GPU solver's structure.
 import numpy as np
 
 
-def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=None):
+def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=None, lm_scaling=True):
     """Assemble the per-stage QP data of ONE instance from the linearisation outputs.
 
     lin: dict with xn [N,10], AB [N,14,10], y [N,11], Jy [N,14,11], yN [4], JyN [10,4], h [N+1,3],
@@ -40,7 +40,9 @@ def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=Non
         j[:, 0, :10] = (-2.0 * t ** 3)[:, None] * lin["Jh"][:N, :, 2]
         Jy = np.concatenate([Jy, j], axis=1)
         r = np.concatenate([r, (t ** 4 - yref[:, 11])[:, None]], axis=1)
-    q["H"] = np.einsum("kai,ka,kaj->kij", Jy, W, Jy) * s[:N, None, None] + lm * np.eye(14)
+    # Levenberg-Marquardt term: lm dt_k at k < N with lm_scaling (acados: Ts[k] * levenberg_marquardt), lm at N
+    lmk = lm * np.asarray(dt, float)[:N] if lm_scaling else np.full(N, float(lm))
+    q["H"] = np.einsum("kai,ka,kaj->kij", Jy, W, Jy) * s[:N, None, None] + lmk[:, None, None] * np.eye(14)
     q["g"] = np.einsum("kai,ka,ka->ki", Jy, W, r) * s[:N, None]
     JyN = lin["JyN"].T                                         # [4,10]
     rN = lin["yN"] - yNref
@@ -56,8 +58,9 @@ def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=Non
     return q
 
 
-def solve_dense(q, tol=1e-11, max_iter=100):
-    """Mehrotra IPM on the full KKT system.  Returns dict(dx [N+1,10], du [N,4], sl, su [N+1,3], iters)."""
+def dense_problem(q):
+    """The QP of stage_qp as one dense problem: min 1/2 z'Hz + g'z s.t. E z = e, G z + d >= 0, with
+    z = [dx_0..dx_N, du_0..du_{N-1}, sl_0..sl_N, su_0..su_N]."""
     N = q["N"]
     nx, nu, ns = 10, 4, 3
     ix = lambda k: k * nx
@@ -103,6 +106,45 @@ def solve_dense(q, tol=1e-11, max_iter=100):
             a = np.zeros(nz); a[isl(k) + j] = 1.0; rows.append(a); d.append(0.0)
             a = np.zeros(nz); a[isu(k) + j] = 1.0; rows.append(a); d.append(0.0)
     G = np.array(rows); d = np.array(d)
+    return H, g, E, e, G, d
+
+
+def _unpack(q, z):
+    N, nx, nu, ns = q["N"], 10, 4, 3
+    o1, o2, o3 = (N + 1) * nx, (N + 1) * nx + N * nu, (N + 1) * nx + N * nu + (N + 1) * ns
+    return {"dx": z[:o1].reshape(N + 1, nx), "du": z[o1:o2].reshape(N, nu), "sl": z[o2:o3].reshape(N + 1, ns),
+            "su": z[o3:].reshape(N + 1, ns)}
+
+
+def polish(q, sol, act_tol=1e-7):
+    """Active-set polish of an IPM solution: the rows with G z + d < act_tol become equalities and the
+    equality-constrained QP is solved directly (one dense KKT solve, no barrier terms, so no late-IPM
+    ill-conditioning).  Returns the polished solution and the KKT check (min dual, max row violation)."""
+    H, g, E, e, G, d = dense_problem(q)
+    z0 = np.concatenate([sol["dx"].ravel(), sol["du"].ravel(), sol["sl"].ravel(), sol["su"].ravel()])
+    act = (G @ z0 + d) < act_tol
+    Ga, da = G[act], d[act]
+    nz, ne, na = H.shape[0], E.shape[0], Ga.shape[0]
+    K = np.block([[H, E.T, -Ga.T], [E, np.zeros((ne, ne)), np.zeros((ne, na))], [Ga, np.zeros((na, ne + na))]])
+    sol_ = np.linalg.lstsq(K, np.concatenate([-g, e, -da]), rcond=None)[0]
+    z, lam = sol_[:nz], sol_[nz + ne:]
+    out = _unpack(q, z)
+    out["min_dual"] = lam.min() if na else 0.0
+    out["max_violation"] = max(0.0, -(G @ z + d).min())
+    return out
+
+
+def solve_dense(q, tol=1e-11, max_iter=100):
+    """Mehrotra IPM on the full KKT system.  Returns dict(dx [N+1,10], du [N,4], sl, su [N+1,3], iters)."""
+    N = q["N"]
+    nx, nu, ns = 10, 4, 3
+    ix = lambda k: k * nx
+    iu = lambda k: (N + 1) * nx + k * nu
+    isl = lambda k: (N + 1) * nx + N * nu + k * ns
+    isu = lambda k: (N + 1) * nx + N * nu + (N + 1) * ns + k * ns
+    nz = (N + 1) * nx + N * nu + 2 * (N + 1) * ns
+    ne = (N + 1) * nx
+    H, g, E, e, G, d = dense_problem(q)
     m = G.shape[0]
     z = np.zeros(nz)
     z = np.linalg.lstsq(E, e, rcond=None)[0]
@@ -110,12 +152,21 @@ def solve_dense(q, tol=1e-11, max_iter=100):
     lam = np.ones(m)
     y = np.zeros(ne)
     it = 0
+    # stationarity is measured relative to the data scale: at tight tolerances the dense LU solve of the
+    # (ill-conditioned, late-IPM) KKT system cannot push |rd| below ~1e-11 absolute, and iterating on
+    # then degrades the iterate -- so stop there, and otherwise return the best iterate seen
+    sd = max(1.0, np.abs(g).max(), np.abs(H).max())
+    best = None
     for it in range(1, max_iter + 1):
         rd = H @ z + g - G.T @ lam + E.T @ y
         rp = G @ z + d - t
         re = E @ z - e
         mu = t @ lam / m
-        if max(np.abs(rd).max(), np.abs(rp).max(), np.abs(re).max()) < tol and mu < tol:
+        merit = max(np.abs(rd).max() / sd, np.abs(rp).max(), np.abs(re).max(), mu)
+        if best is None or merit < best[0]:
+            best = (merit, z.copy(), t.copy(), lam.copy(), it)
+        if merit < tol:
+            best = None
             break
         Sig = lam / t
         K = np.block([[H + G.T @ (Sig[:, None] * G), E.T], [E, np.zeros((ne, ne))]])
@@ -139,6 +190,8 @@ def solve_dense(q, tol=1e-11, max_iter=100):
         dz, dy, dt_, dl = solve(t * lam + dt_ * dl - sig * mu)
         a = min(1.0, 0.995 * min(step(t, dt_), step(lam, dl)))
         z += a * dz; y += a * dy; t += a * dt_; lam += a * dl
+    if best is not None:  # max_iter without meeting tol: the best iterate seen
+        _, z, t, lam, it = best
     dx = np.array([z[ix(k):ix(k) + nx] for k in range(N + 1)])
     du = np.array([z[iu(k):iu(k) + nu] for k in range(N)])
     sl = np.array([z[isl(k):isl(k) + ns] for k in range(N + 1)])

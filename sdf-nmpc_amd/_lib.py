@@ -54,7 +54,7 @@ class LinArgsC(C.Structure):
 class QpOptsC(C.Structure):
     _fields_ = [("lbu", C.c_double * 4), ("ubu", C.c_double * 4), ("lh", C.c_double * 3), ("uh", C.c_double * 3),
                 ("zl", C.c_double * 3), ("Zl", C.c_double * 3), ("lm", C.c_double), ("cost_scaling", C.c_int),
-                ("max_iter", C.c_int), ("tol", C.c_double), ("ny", C.c_int)]
+                ("max_iter", C.c_int), ("tol", C.c_double), ("ny", C.c_int), ("lm_scaling", C.c_int)]
 
 
 class RefOptsC(C.Structure):
@@ -125,7 +125,7 @@ def load():
         "sdfnmpc_linearize": (i, [vp, vp, P(QuadModelC), P(LinArgsC)]),
         "sdfnmpc_shooting_grid": (i, [i, d, i, i, d, P(d), P(d)]),
         "sdfnmpc_qp_solve": (i, [vp, P(QpOptsC), P(QpArgsC)]),
-        "sdfnmpc_rti_apply": (i, [vp, i, i, vp, vp, vp, vp, vp]),
+        "sdfnmpc_rti_apply": (i, [vp, i, i, vp, vp, vp, vp, vp, vp]),
         "sdfnmpc_pack_refs": (i, [vp, P(RefOptsC), P(RefArgsC)]),
         "sdfnmpc_vae_load": (i, [vp, vp, sz, P(vp)]),
         "sdfnmpc_vae_free": (None, [vp]),
@@ -135,7 +135,7 @@ def load():
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    if lib.sdfnmpc_abi_version() != 3:
+    if lib.sdfnmpc_abi_version() != 4:
         raise SdfnmpcError("libsdfnmpc.so ABI version mismatch")
     _lib = lib
     return lib
@@ -292,11 +292,13 @@ def linearize(ctx: Context, net: Net, model: QuadModelC, B: int, N: int, np_: in
     _check(load().sdfnmpc_linearize(ctx.h, net.h, C.byref(model), C.byref(a)))
 
 
-def qp_opts(model, lm=10.0, cost_scaling=True, max_iter=100, tol=1e-8) -> QpOptsC:
-    """QP data of the 'att' model (model.Quad) + solver options (ocp.py:113-120 defaults)."""
+def qp_opts(model, lm=10.0, cost_scaling=True, max_iter=100, tol=1e-8, lm_scaling=True) -> QpOptsC:
+    """QP data of the 'att' model (model.Quad) + solver options (ocp.py:113-120 defaults).  lm_scaling: the
+    Levenberg-Marquardt term is lm dt_k at stages k < N and lm at N (acados' Ts-scaled term)."""
     v = lambda a, n: (C.c_double * n)(*[float(x) for x in a])
     return QpOptsC(v(model.lbu, 4), v(model.ubu, 4), v(model.lh, 3), v(model.uh, 3), v(model.zl, 3),
-                   v(model.Zl, 3), float(lm), int(bool(cost_scaling)), int(max_iter), float(tol), int(model.ny))
+                   v(model.Zl, 3), float(lm), int(bool(cost_scaling)), int(max_iter), float(tol), int(model.ny),
+                   int(bool(lm_scaling)))
 
 
 def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
@@ -305,8 +307,9 @@ def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
     _check(load().sdfnmpc_qp_solve(ctx.h, C.byref(opts), C.byref(a)))
 
 
-def rti_apply(ctx: Context, B: int, N: int, x, u, dx, du, u0=None):
-    _check(load().sdfnmpc_rti_apply(ctx.h, B, N, _ptr(x), _ptr(u), _ptr(dx), _ptr(du), _ptr(u0)))
+def rti_apply(ctx: Context, B: int, N: int, x, u, dx, du, u0=None, status=None):
+    """x += dx, u += du, u0 = u[:, 0]; instances whose QP status is >= 2 (numerical failure) keep x, u."""
+    _check(load().sdfnmpc_rti_apply(ctx.h, B, N, _ptr(x), _ptr(u), _ptr(dx), _ptr(du), _ptr(u0), _ptr(status)))
 
 
 def shooting_grid(N: int, T: float, uniform=True, nb_short_nodes=2, dt_short=0.01):

@@ -879,6 +879,7 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
     for (int i = 0; i < 4; ++i) { q.lbu[i] = o->lbu[i]; q.ubu[i] = o->ubu[i]; }
     for (int i = 0; i < 3; ++i) { q.lh[i] = o->lh[i]; q.uh[i] = o->uh[i]; q.zl[i] = o->zl[i]; q.Zl[i] = o->Zl[i]; }
     q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling; q.ny = o->ny;
+    q.lm_scaling = o->lm_scaling;
     HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(q, ctx->stream); }));
     HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
     return SDFNMPC_OK;
@@ -912,10 +913,10 @@ extern "C" int sdfnmpc_pack_refs(sdfnmpc_ctx* ctx, const sdfnmpc_ref_opts* o, co
 }
 
 extern "C" int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, const double* dx,
-                                 const double* du, double* u0) {
+                                 const double* du, double* u0, const int* status) {
     if (!ctx || B < 0 || N < 1 || (B > 0 && (!x || !u || !dx || !du))) return fail(SDFNMPC_E_ARG, "bad rti_apply arguments");
     ScopedDevice sd(ctx->device);
-    HIPCHK(timed(ctx, "rti_apply", [&] { return launch_rti_apply(B, N, x, u, dx, du, u0, ctx->stream); }));
+    HIPCHK(timed(ctx, "rti_apply", [&] { return launch_rti_apply(B, N, x, u, dx, du, u0, status, ctx->stream); }));
     return SDFNMPC_OK;
 }
 

@@ -22,6 +22,7 @@ struct QpArgs {
     double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3];
     double lm, tol;
     int max_iter, cost_scaling;
+    int lm_scaling;  // 1: lm dt_k at stages k < N, lm at N (acados' Ts-scaled Levenberg-Marquardt term)
     int ny;  // 11, or 12 with the sdf cost residual (formed in the pack kernel from h[2], J_h[2])
 };
 
@@ -54,6 +55,6 @@ __host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N)
 hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s);  // stage records into the workspace
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);       // the IPM (after launch_rti_qp_pack)
 hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx, const double* du, double* u0,
-                            hipStream_t s);
+                            const int* status, hipStream_t s);
 
 }  // namespace sdfn

@@ -56,8 +56,8 @@ using IC = std::integral_constant<int, V>;
 constexpr int NX = 10, NU = 4, NS = 3;
 // stage record: [AB 140 (column j = d xn / d (x,u)_j) | c 10 | g 14 | C^T 30 (row j = d h_j / d x) | H 105 upper | 0]
 constexpr int R_AB = 0, R_C = 140, R_G = 150, R_CT = 164, R_H = 194, R_Z = 299, REC = QP_REC;
-// factor record: [A~|b~ 10 x 11 | K|k_ff 4 x 11 | Y 4 x 10 | L 10 (lower packed, diagonal 1/L_ii) | P c 10 | junk 2]
-constexpr int F_AB = 0, F_K = 110, F_Y = 154, F_L = 194, F_PC = 204, F_J = 214, FREC = QP_FREC;
+// factor record: [A~|b~ 10 x 11 | K|k_ff 4 x 11 | (unused 4 x 10) | L 10 (lower packed, diagonal 1/L_ii) | P c 10 | junk 2]
+constexpr int F_AB = 0, F_K = 110, F_L = 194, F_PC = 204, F_J = 214, FREC = QP_FREC;
 constexpr int F_FW = 154;  // forward sweeps read [0, F_FW)
 constexpr int SLOT = QP_SLOT, PD = QP_RING;
 // Window of one stream position per sweep kind: n_loads(K) loads of 64 consecutive doubles (lanes
@@ -74,17 +74,28 @@ __host__ __device__ constexpr int load_at(int K, int j) {
 }
 static_assert(FREC == 216 && PD == 3 && SLOT == 6, "record layout");
 static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT, "window layout");
-// IPM starting point: t = max(row value, T0), lambda = L0.  The kernel waits for its slowest
-// instance, so these were chosen for the worst case over seeds / x0 spreads (profiles/r01/
-// qp_init_sweep.txt): (1, 3) converges every instance in <= 13 iterations where (1, 1) needs 16-17
-// and larger lambda_0 stalls a few instances.
+// IPM starting point and step fraction (the kernel waits for its slowest instance, so these were
+// chosen on the worst case over seeds / x0 spreads with the C restatement, oracle/qp_ipm.c):
+// t = max(row value, T0); lambda = L0 on the box rows and max(L0, LC s_k zl_j) on the four rows of
+// soft group (k, j) (the duals of the penalised slacks start near their optimal magnitude, and the
+// slack rows' stationarity s_k zl - lambda_h - lambda_s starts at 0); step fraction
+// tau = min(TAU_HI, max(TAU_LO, 1 - mu)).
 #ifndef QP_T0
-#define QP_T0 1.0
+#define QP_T0 0.5
 #endif
 #ifndef QP_L0
-#define QP_L0 3.0
+#define QP_L0 1.0
 #endif
-constexpr double T0 = QP_T0, L0 = QP_L0;
+#ifndef QP_LC
+#define QP_LC 0.5
+#endif
+#ifndef QP_TAU_LO
+#define QP_TAU_LO 0.995
+#endif
+#ifndef QP_TAU_HI
+#define QP_TAU_HI 0.995
+#endif
+constexpr double T0 = QP_T0, L0 = QP_L0, LC = QP_LC, TAU_LO = QP_TAU_LO, TAU_HI = QP_TAU_HI;
 
 __device__ __forceinline__ int tri10(int a, int c) { return a * 10 - a * (a - 1) / 2 + (c - a); }  // a <= c
 __device__ __forceinline__ int tri14(int a, int c) { return a * 14 - a * (a - 1) / 2 + (c - a); }  // a <= c
@@ -218,6 +229,7 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
     if (k < N) {
         const size_t bk = (size_t)b * N + k;
         const double sk = A.cost_scaling ? A.dt[k] : 1.0;
+        const double lmk = A.lm_scaling ? A.lm * A.dt[k] : A.lm;  // acados: Ts_k lm for k < N, lm at N
         for (int e = lane; e < 154; e += 64) Js[(e / 11) * ny + e % 11] = A.Jy[bk * 154 + e];
         if (lane < ny) {
             const int i = lane;
@@ -268,7 +280,7 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
             } else if (e < R_H + 105) {
                 const int a = c_tri.a14[e - R_H], c = c_tri.c14[e - R_H];
                 for (int i = 0; i < ny; ++i) v += Js[a * ny + i] * Ws[i] * Js[c * ny + i];
-                v += (a == c ? A.lm : 0.0);
+                v += (a == c ? lmk : 0.0);
             }
             Rk[e] = v;
         }
@@ -442,7 +454,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             h_i[r] = (a < 14 && c < 14) ? R_H + tri14(lo, hi) : (a < 14 && c == 14) ? R_G + a : R_Z;
         }
         // fold operands: A = C[c][g] (g < 3), B = w_g C[c][g] (c < 10) | gamma_g (c = 14)
-        const int cgi = (c < NX && g < NS) ? R_CT + g * 10 + c : R_Z, gj = g < NS ? g : 0;
+        const int cgi = (c < NX && g < NS) ? R_CT + g * 10 + c : R_Z, gj = g < NS ? g : 0, gj4 = g;
         const double m14 = c == 14 ? 1.0 : 0.0, mg3 = g < NS ? 1.0 : 0.0;
         // closed loop: [A | c][a][c] at ab01 + 4 r (r = 0, 1), ab2; A operand B[a = c][g] at bmi
         const bool xcol = c < NX || c == 14;           // columns of [P | p], [A | c], [K | k_ff]
@@ -472,7 +484,13 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             sab[r] = 8u * ((xcol && a < NX) ? F_AB + a * 11 + xo : F_J);
         }
         const unsigned sk_ = 8u * (xcol ? F_K + g * 11 + xo : F_J);
-        const unsigned sy_ = 8u * (c < NX ? F_Y + g * 10 + c : F_J);
+        // Joseph form operands (window indices; R_Z reads 0):  A operand H^_xu[c][g] (c < 10);
+        // A operand R^0[c][g] = H_uu[c][g] (+ box diagonal, c < 4); C init H^[10 + g][c] of V's row g
+        const int hxu_i = c < NX ? R_H + tri14(c, NX + g) : R_Z;
+        const int huu_i = c < NU ? R_H + tri14(NX + (c < g ? c : g), NX + (c < g ? g : c)) : R_Z;
+        const double huu_b = c == g ? 1.0 : 0.0;  // box diagonal of R^0 (c == g < 4)
+        const int v0_i = c < 14 ? R_H + tri14(c < NX + g ? c : NX + g, c < NX + g ? NX + g : c) : c == 14 ? R_G + NX + g : R_Z;
+        const double v0_bd = c == NX + g ? 1.0 : 0.0, v0_bv = c == 14 ? 1.0 : 0.0;
 
         const int k = N - q;
         const double cg = win[cgi];
@@ -508,7 +526,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         Ab[2] = win[ab2];
         Ab[3] = 0.0;
         const double bm = win[bmi];
+        const double hxa = win[hxu_i];
+        const double hua = win[huu_i] + huu_b * s.bd[k * NU + gj4];
+        const double hv0 = win[v0_i] + v0_bd * s.bd[k * NU + gj4] + v0_bv * s.bv[k * NU + gj4];
         M = mfma(cg, fb, M);
+        d4 Hh = M;  // H^ = [H | g] + fold + box terms (the Joseph form's stage term)
 #pragma unroll
         for (int r = 0; r < 3; ++r) bst(W[r], rsF, spc[r], sko);
 #pragma unroll
@@ -530,24 +552,36 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double i2 = rsqrt_nr(r22 - l20 * l20 - l21 * l21);
         const double l32 = (r32 - l30 * l20 - l31 * l21) * i2;
         const double i3 = rsqrt_nr(r33 - l30 * l30 - l31 * l31 - l32 * l32);
-        // column c of [Y | w] = L^-1 [S | m_u];  [P | p] <- M' - Y^T [Y | w]  (the critical chain ends here)
+        // column c of [Y | w] = L^-1 [S | m_u],  [K | k_ff] = -L^-T [Y | w]
         const double y0 = s0 * i0;
         const double y1 = (s1 - l10 * y0) * i1;
         const double y2 = (s2 - l20 * y0 - l21 * y1) * i2;
         const double y3 = (s3 - l30 * y0 - l31 * y1 - l32 * y2) * i3;
-        const double yg = mg[0] * y0 + mg[1] * y1 + mg[2] * y2 + mg[3] * y3;
-        Pa = mfma(-yg, yg, M);
-        __builtin_amdgcn_sched_barrier(0);  // hand P to the next stage before the off-chain work
-        // ---- off the chain: [K | k_ff] = -L^-T [Y | w], [A~ | b~] = [A | c] + B [K | k_ff]
         const double k3 = -y3 * i3;
         const double k2 = (-y2 - l32 * k3) * i2;
         const double k1 = (-y1 - l21 * k2 - l31 * k3) * i1;
         const double k0 = (-y0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
         const double kg = mg[0] * k0 + mg[1] * k1 + mg[2] * k2 + mg[3] * k3;
-        Ab = mfma(bm, kg, Ab);
+        // ---- Joseph form: [P | p] <- T^T H^ T + A~^T [P A~ | P b~ + p],  T = [I 0; K k_ff; 0 1]
+        // (a sum of PSD terms: no cancellation of M'_xx - Y^T Y when a hard state row puts a huge fold
+        // into P; that cancellation costs ~1e-6 absolute accuracy and the IPM its worst-case iterations)
+        Ab = mfma(bm, kg, Ab);                                      // [A~ | b~] = [A | c] + B [K | k_ff]
+        d4 V = {hv0, 0.0, 0.0, 0.0};
+        V = mfma(hua, kg, V);                                       // rows 10..13 of H^ T, in rows 0..3
+        d4 W2 = {0.0, 0.0, 0.0, 0.0};
+        W2 = mfma(Pa[0], Ab[0], W2);
+        W2 = mfma(Pa[1], Ab[1], W2);
+        W2 = mfma(Pa[2], Ab[2], W2);
+        Hh = mfma(hxa, kg, Hh);                                     // H^_x T
+        Hh = mfma(kg, V[0], Hh);                                    // + K^T (H^_u T)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) W2[r] = fma(m14, Pa[r], W2[r]);  // column 14: P b~ + p
+        Pa = mfma(Ab[0], W2[0], Hh);
+        Pa = mfma(Ab[1], W2[1], Pa);
+        Pa = mfma(Ab[2], W2[2], Pa);
+        __builtin_amdgcn_sched_barrier(0);  // hand P to the next stage before the record stores
         // ---- factor record (and its LDS copy for the first forward stages)
         bst(kg, rsF, sk_, sko);
-        bst(yg, rsF, sy_, sko);
         {  // the (uniform) Cholesky factor: every lane stores the same 16 bytes, no lane selection
             d2* Lp = (d2*)(F + (size_t)k * FREC + F_L);
             Lp[0] = d2{i0, l10}; Lp[1] = d2{i1, l20}; Lp[2] = d2{l21, i2}; Lp[3] = d2{l30, l31}; Lp[4] = d2{l32, i3};
@@ -647,7 +681,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     auto rows_init = [&]() -> double {
     double rp = 0.0;
     for (int r = lane; r < m; r += 64) {
-        double v;
+        double v, l0 = L0;
         if (r < 8 * N) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
             v = box_d(k, i, up);
@@ -655,10 +689,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const int q = r - 8 * N, k = q / 12, w = q - 12 * k, j = w >> 2, kind = w & 3;
             const double h = s.hv[k * 3 + j];
             v = kind == 0 ? s.cxa[k * NS + j] + (h - s.cst[8 + j]) : kind == 1 ? -s.cxa[k * NS + j] + (s.cst[11 + j] - h) : 0.0;
+            l0 = fmax(L0, LC * s.skv[k] * s.cst[14 + j]);
         }
         const double t = fmax(v, T0);
         s.t[r] = t;
-        s.lam[r] = L0;
+        s.lam[r] = l0;
         rp = fmax(rp, fabs(v - t));
     }
     return wmax(rp);
@@ -719,8 +754,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         for (int e = lane; e < N1 * NS; e += 64) {
             const int k = e / NS, j = e - NS * k;
             const Grp g = group(k, j, phase, sigmu);
-            if (!phase) s.fw[e] = g.s1 * (g.Hl - g.s1) * g.iHl + g.s3 * (g.Hu - g.s3) * g.iHu;
-            s.fg[e] = -(g.v1 + g.s1 * g.gl * g.iHl) + (g.v3 + g.s3 * g.gu * g.iHu);
+            // fold of the eliminated slack pair, written without the cancellation of H - s1 (H = Zs + s1 + s2
+            // with s1 -> inf on an active row):  w = s1 (Zs + s2) / Hl + ...,  gamma = -(v1 + s1 gl / Hl) + ...
+            const double Zs = s.skv[k] * s.cst[17 + j], zs = s.skv[k] * s.cst[14 + j];
+            if (!phase) s.fw[e] = g.s1 * (Zs + g.s2) * g.iHl + g.s3 * (Zs + g.s4) * g.iHu;
+            s.fg[e] = -(g.v1 * (Zs + g.s2) + g.s1 * (zs - g.v2)) * g.iHl + (g.v3 * (Zs + g.s4) + g.s3 * (zs - g.v4)) * g.iHu;
         }
         for (int e = lane; e < N * NU; e += 64) {
             const int k = e >> 2, i = e & 3;
@@ -743,7 +781,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
 
     // ------------------------------------------------------------ IPM: sweep driver
     // predictor rows: affine step length, mu_aff -> sigma mu (Mehrotra)
-    double mu = 0.0, rp = 0.0;
+    // mu: mean complementarity (Mehrotra's centring); cm: max complementarity -- the stop test is
+    // HPIPM's, max_i t_i lambda_i <= tol and max primal residual <= tol
+    // gap = prod (1 - alpha): the stationarity residual of the starting point decays by exactly this
+    // factor (every Newton system is solved for the new iterate), the stand-in for HPIPM's res_g test
+    double mu = 0.0, cm = 0.0, rp = 0.0, gap = 1.0;
     auto rows_pred = [&]() -> double {
         double amax = 1.0;
         auto bound = [&](double t, double l, double dt, double dl) {
@@ -788,7 +830,9 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
         const double mua = wsum(lmua) / m;
         const double sig = (mua / mu) * (mua / mu) * (mua / mu);
-        return sig * mu;
+        // centring target floored at 1e-2 tol (HPIPM's tau_min): no row is pushed below the complementarity
+        // the stop test needs, which keeps lambda / t -- and the Riccati data -- bounded
+        return fmax(sig * mu, 1e-2 * A.tol);
     };
     // corrector rows: step length, update of (t, lambda, du, dx), mu and the primal residual
     auto rows_update = [&](double sigmu) {
@@ -821,9 +865,10 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             bound(t, l, dt, -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it);
             }
         }
-        const double al = fmin(1.0, 0.995 * wmin(amax));
+        const double tau = fmin(TAU_HI, fmax(TAU_LO, 1.0 - mu));
+        const double al = fmin(1.0, tau * wmin(amax));
         // -------- update (rows read everything they need before writing their own entries)
-        double lmu = 0.0;
+        double lmu = 0.0, lcm = 0.0;
         for (int r = lane; r < 8 * N; r += 64) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
             const double t = s.t[r], l = s.lam[r];
@@ -833,6 +878,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const double dl = -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it;
             const double tn = t + al * dt, ln = l + al * dl;
             lmu += tn * ln;
+            lcm = fmax(lcm, tn * ln);
             s.t[r] = tn;
             s.lam[r] = ln;
         }
@@ -852,6 +898,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
                 tn[q] = t + al * dt;
                 ln[q] = l + al * dl;
                 lmu += tn[q] * ln[q];
+                lcm = fmax(lcm, tn[q] * ln[q]);
             }
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -862,7 +909,9 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         for (int e = lane; e < N1 * NX; e += 64) s.dx[e] += al * (s.dxc[e] - s.dx[e]);
         for (int e = lane; e < N * NU; e += 64) s.du[e] += al * (s.duc[e] - s.du[e]);
         mu = wsum(lmu) / m;
+        cm = wmax(lcm);
         rp *= (1.0 - al);
+        gap *= (1.0 - al);
     };
 
     // ------------------------------------------------------------ IPM: sweeps over the record stream
@@ -918,13 +967,18 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     STAMP(1);
     rp = rows_init();
     {
-        double lmu = 0.0;
-        for (int r = lane; r < m; r += 64) lmu += s.t[r] * s.lam[r];
+        double lmu = 0.0, lcm = 0.0;
+        for (int r = lane; r < m; r += 64) {
+            lmu += s.t[r] * s.lam[r];
+            lcm = fmax(lcm, s.t[r] * s.lam[r]);
+        }
         mu = wsum(lmu) / m;
+        cm = wmax(lcm);
     }
     wave_sync();
     int it = 0;
-    while (!(mu < A.tol && rp < A.tol) && it < A.max_iter) {
+    // a non-finite iterate (NaN / Inf in the linearisation) stops the instance at once: status 2
+    while (!(cm < A.tol && rp < A.tol && gap < A.tol) && it < A.max_iter && __builtin_isfinite(mu + rp)) {
         terms(0, 0.0);
         STAMP(6);
         sweep(IC<1>{});
@@ -959,30 +1013,37 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
     if (lane == 0) {
         A.iters[b] = it;
-        A.status[b] = (mu < A.tol && rp < A.tol) ? 0 : 1;  // 1: max_iter reached (acados status 2)
-        A.res[b * 2] = mu;
+        // 0 converged; 1 max_iter reached (acados status 2, the step is kept); 2 numerical failure (acados
+        // QP failure, status 4: rti_apply keeps this instance's iterate)
+        A.status[b] = !__builtin_isfinite(mu + rp) ? 2 : (cm < A.tol && rp < A.tol && gap < A.tol) ? 0 : 1;
+        A.res[b * 2] = cm;
         A.res[b * 2 + 1] = rp;
     }
 }
 
 __global__ __launch_bounds__(256) void rti_apply_kernel(int B, int N, double* x, double* u, const double* dx,
-                                                       const double* du, double* u0) {
+                                                       const double* du, double* u0, const int* status) {
     const long long nx = (long long)B * (N + 1) * 10, nu = (long long)B * N * 4;
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < nx) x[i] += dx[i];
+    if (i < nx) {
+        const bool keep = status && status[i / ((long long)(N + 1) * 10)] >= 2;
+        if (!keep) x[i] += dx[i];
+    }
     if (i < nu) {
-        const double v = u[i] + du[i];
-        u[i] = v;
         const long long bb = i / ((long long)N * 4), r = i - bb * N * 4;
+        const bool keep = status && status[bb] >= 2;
+        const double v = keep ? u[i] : u[i] + du[i];
+        u[i] = v;
         if (u0 && r < 4) u0[bb * 4 + r] = v;
     }
 }
 
 hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx, const double* du, double* u0,
-                            hipStream_t s) {
+                            const int* status, hipStream_t s) {
     const long long n = (long long)B * (N + 1) * 10;
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(rti_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, B, N, x, u, dx, du, u0);
+    hipLaunchKernelGGL(rti_apply_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, B, N, x, u, dx, du, u0,
+                       status);
     return hipGetLastError();
 }
 

@@ -182,14 +182,17 @@ class Ocp:
         t0 = time.perf_counter()
         _lib.linearize(self.ctx, self.net, self.cmodel, self.B, N, m.np, b)
         _lib.qp_solve(self.ctx, self.qp_opts, self.B, N, b)
-        _lib.rti_apply(self.ctx, self.B, N, b["x"], b["u"], b["dx"], b["du"], b["u0"])
+        _lib.rti_apply(self.ctx, self.B, N, b["x"], b["u"], b["dx"], b["du"], b["u0"], status=b["status"])
         self.ctx.synchronize()
         self.t = time.perf_counter() - t0
         self.status = b["status"].cpu().numpy()
         u0 = b["u0"].cpu().numpy()
         self.u = u0[0] if self.B == 1 else u0
-        if (self.status != 0).any():  # acados status 2 (QP max_iter): solve_for_x0 warns, keeps the step
-            warnings.warn(f"QP reached qp_solver_iter_max on {(self.status != 0).sum()} of {self.B} instances")
+        if (self.status == 1).any():  # acados status 2 (QP max_iter): solve_for_x0 warns, keeps the step
+            warnings.warn(f"QP reached qp_solver_iter_max on {(self.status == 1).sum()} of {self.B} instances")
+        if (self.status >= 2).any():  # acados QP failure (status 4): solve_for_x0 raises; the iterate is kept
+            raise _lib.SdfnmpcError(f"QP failure (non-finite data) on instances {np.flatnonzero(self.status >= 2)[:8]}"
+                                    f" ({(self.status >= 2).sum()} of {self.B}); their iterate is unchanged")
         return self.u
 
     def get_u(self):

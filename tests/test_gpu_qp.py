@@ -1,4 +1,5 @@
-"""Batched RTI QP (rti_qp.hip via sdfnmpc_qp_solve) vs the dense reference IPM (oracle/qp_oracle.py)."""
+"""Batched RTI QP (rti_qp.hip via sdfnmpc_qp_solve) vs the exact QP solution (oracle/qp_oracle.py: dense
+KKT IPM + active-set polish) and vs the structured C IPM (oracle/qp_ipm.c, the same algorithm)."""
 import numpy as np
 import pytest
 
@@ -7,8 +8,10 @@ from sdf_nmpc_amd.model import Quad
 
 pytestmark = pytest.mark.gpu
 
-QP_TOL = 1e-10          # IPM stop tolerance used for the parity runs
-SOL_ATOL = 1e-5         # |du - du_ref|, |dx - dx_ref| (IPM solutions agree to ~sqrt(mu) level)
+QP_TOL = 1e-8           # HPIPM's default stop tolerance, the production value (ocp.py:113-116)
+SOL_ATOL = 5e-6         # |du - du_ref|, |dx - dx_ref| vs the exact solution; the C restatement of the same
+                        # IPM is within 3e-7 of it at QP_TOL on these instances (tests/test_qp_oracle.py)
+ORC_ATOL = 5e-6         # GPU vs the C restatement (same algorithm, same iterations; rounding differences)
 
 
 def setup(gpu_ctx, cfg, B, N, seed, x0_noise=0.05, sdf_cost=False):
@@ -43,8 +46,8 @@ def solve(gpu_ctx, cfg, t, B, N, sdf_cost=False, **kw):
     return model
 
 
-@pytest.mark.parametrize("B,N,seed", [(3, 20, 1), (2, 40, 2)])
-def test_qp_matches_dense_oracle(gpu_ctx, oracle_lib, cfg, B, N, seed):
+@pytest.mark.parametrize("B,N,seed", [(3, 20, 1), (2, 40, 2), (2, 60, 5)])
+def test_qp_matches_exact_solution(gpu_ctx, oracle_lib, cfg, B, N, seed):
     import qp_oracle
     prob, x0, t = setup(gpu_ctx, cfg, B, N, seed)
     model = solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL)
@@ -53,7 +56,8 @@ def test_qp_matches_dense_oracle(gpu_ctx, oracle_lib, cfg, B, N, seed):
     for b in range(B):
         q = qp_oracle.stage_qp({k: v[b] for k, v in lin.items()}, prob["x"][b], prob["u"][b], x0[b], prob["yref"][b],
                                prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], model, 10.0)
-        ref = qp_oracle.solve_dense(q)
+        ref = qp_oracle.polish(q, qp_oracle.solve_dense(q))
+        assert ref["max_violation"] < 1e-9 and ref["min_dual"] > -1e-9
         np.testing.assert_allclose(t["du"][b].cpu().numpy(), ref["du"], rtol=0, atol=SOL_ATOL)
         np.testing.assert_allclose(t["dx"][b].cpu().numpy(), ref["dx"], rtol=0, atol=SOL_ATOL)
         sl = t["slack"][b].cpu().numpy()
@@ -95,20 +99,69 @@ def test_rti_apply(gpu_ctx):
     _lib.rti_apply(gpu_ctx, B, N, xd, ud, dxd, dud, u0)
     gpu_ctx.synchronize()
     assert torch.equal(xd.cpu(), x + dx) and torch.equal(ud.cpu(), u + du) and torch.equal(u0.cpu(), (u + du)[:, 0])
+    # with the QP status: a failed instance (status 2) keeps its iterate, max_iter (1) applies the step
+    st = torch.tensor([0, 2, 1, 2, 0], dtype=torch.int32, device=dev)
+    xd, ud = x.to(dev), u.to(dev)
+    torch.cuda.synchronize()
+    _lib.rti_apply(gpu_ctx, B, N, xd, ud, dxd, dud, u0, status=st)
+    gpu_ctx.synchronize()
+    keep = torch.tensor([False, True, False, True, False])
+    assert torch.equal(xd.cpu()[keep], x[keep]) and torch.equal(ud.cpu()[keep], u[keep])
+    assert torch.equal(xd.cpu()[~keep], (x + dx)[~keep]) and torch.equal(ud.cpu()[~keep], (u + du)[~keep])
+    assert torch.equal(u0.cpu()[keep], u[keep][:, 0]) and torch.equal(u0.cpu()[~keep], (u + du)[~keep][:, 0])
 
 
-@pytest.mark.parametrize("B,N,seed,noise", [(64, 40, 3, 0.05), (32, 20, 9, 0.5)])
+def test_qp_nan_instance_fails_alone(gpu_ctx, cfg):
+    """A NaN in one instance's linearisation: that instance stops at once with status 2 (acados QP
+    failure) instead of looping to max_iter; every other instance is bit-identical to a clean solve."""
+    B, N = 6, 40
+    prob, x0, t = setup(gpu_ctx, cfg, B, N, seed=8)
+    solve(gpu_ctx, cfg, t, B, N)
+    good_du, good_it = t["du"].cpu().numpy(), t["iters"].cpu().numpy()
+    t["Jh"][3, 7, 1, 2] = float("nan")
+    solve(gpu_ctx, cfg, t, B, N)
+    st, it = t["status"].cpu().numpy(), t["iters"].cpu().numpy()
+    assert list(st) == [0, 0, 0, 2, 0, 0] and it[3] <= 1
+    others = [0, 1, 2, 4, 5]
+    assert np.array_equal(t["du"].cpu().numpy()[others], good_du[others]) and np.array_equal(it[others], good_it[others])
+
+
+def _agree(prob, x0, lin, model, got, ref, atol=ORC_ATOL):
+    """GPU vs the C restatement of the same IPM, instance by instance.  Both stop at the same iteration;
+    on most instances the iterates agree to ~1e-7.  On a degenerate instance (a row with both its slack
+    and its dual -> 0) the stopped iterate still moves along the flat direction by up to ~1e-4 at tol
+    1e-8 -- for the C solver as much as for the GPU (tools/qp_diff.py) -- so there the check is on what
+    is determined: the QP objective (to the duality-gap bound m * tol) and feasibility of both points."""
+    import qp_oracle
+    d = np.abs(got["du"] - ref["du"]).max(axis=(1, 2))
+    assert (d <= atol).mean() >= 0.9, f"only {(d <= atol).mean():.2f} of the instances agree to {atol}"
+    for b in np.flatnonzero(d > atol):
+        q = qp_oracle.stage_qp({k: v[b] for k, v in lin.items()}, prob["x"][b], prob["u"][b], x0[b], prob["yref"][b],
+                               prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], model, 10.0)
+        H, g, E, e, G, dd = qp_oracle.dense_problem(q)
+        z = [np.concatenate([s["dx"][b].ravel(), s["du"][b].ravel(), s["slack"][b][..., 0].ravel(),
+                             s["slack"][b][..., 1].ravel()]) for s in (got, ref)]
+        f = [0.5 * v @ H @ v + g @ v for v in z]
+        # each stopped iterate is within its duality gap sum_i t_i lambda_i <= m * tol of the optimum
+        gap = G.shape[0] * QP_TOL
+        assert abs(f[0] - f[1]) <= 2 * gap, f"instance {b}: objective {f[0]} vs {f[1]} (gap bound {gap:.1e})"
+        for v in z:
+            assert np.abs(E @ v - e).max() < 1e-9 and (G @ v + dd).min() > -1e-8
+
+
+@pytest.mark.parametrize("B,N,seed,noise", [(64, 40, 3, 0.05), (32, 20, 9, 0.5), (32, 60, 4, 0.2)])
 def test_qp_matches_riccati_oracle_batch(gpu_ctx, oracle_lib, cfg, B, N, seed, noise):
-    """A wider batch against the structured C IPM (oracle/qp_ipm.c), itself pinned to the dense IPM."""
+    """A wider batch against the structured C IPM (oracle/qp_ipm.c), itself pinned to the exact solution."""
     prob, x0, t = setup(gpu_ctx, cfg, B, N, seed, x0_noise=noise)
     model = solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL)
     assert (t["status"].cpu().numpy() == 0).all()
     lin = {k: t[k].cpu().numpy() for k in ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh")}
     ref = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, nthreads=8)
     assert (ref["status"] == 0).all()
-    np.testing.assert_allclose(t["du"].cpu().numpy(), ref["du"], rtol=0, atol=SOL_ATOL)
-    np.testing.assert_allclose(t["dx"].cpu().numpy(), ref["dx"], rtol=0, atol=SOL_ATOL)
-    np.testing.assert_allclose(t["slack"].cpu().numpy(), ref["slack"], rtol=0, atol=SOL_ATOL)
+    got = {k: t[k].cpu().numpy() for k in ("du", "dx", "slack")}
+    _agree(prob, x0, lin, model, got, ref)
+    # same algorithm, same starting point: the iteration counts agree up to a rounding-level tie
+    assert np.abs(t["iters"].cpu().numpy() - ref["iters"]).max() <= 1
 
 
 def test_qp_sdf_cost_matches_riccati_oracle(gpu_ctx, oracle_lib, cfg):
@@ -120,8 +173,7 @@ def test_qp_sdf_cost_matches_riccati_oracle(gpu_ctx, oracle_lib, cfg):
     lin = {k: t[k].cpu().numpy() for k in ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh")}
     ref = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, nthreads=8)
     assert (ref["status"] == 0).all()
-    np.testing.assert_allclose(t["du"].cpu().numpy(), ref["du"], rtol=0, atol=SOL_ATOL)
-    np.testing.assert_allclose(t["dx"].cpu().numpy(), ref["dx"], rtol=0, atol=SOL_ATOL)
+    _agree(prob, x0, lin, model, {k: t[k].cpu().numpy() for k in ("du", "dx", "slack")}, ref)
     # and the residual changes the solution (the term is live)
     _, _, t2 = setup(gpu_ctx, cfg, B, N, 21, x0_noise=0.2)
     solve(gpu_ctx, cfg, t2, B, N, tol=QP_TOL)

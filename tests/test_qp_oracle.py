@@ -12,7 +12,9 @@ import pytest
 from sdf_nmpc_amd import synth, weights as W
 from sdf_nmpc_amd.model import Quad
 
-SOL_ATOL = 1e-6   # both IPMs stopped at tol 1e-10: solutions agree to ~sqrt(mu)
+QP_TOL = 1e-8     # HPIPM's default stop tolerance (max complementarity / primal residual), the production value
+SOL_ATOL = 2e-6   # Riccati IPM at QP_TOL vs the exact (active-set polished) solution: measured <= 3e-7
+DENSE_ATOL = 1e-7  # dense IPM vs its own polished solution
 
 
 def _with_flags(cfg, **flags):
@@ -31,23 +33,67 @@ def _instance_set(oracle_lib, cfg, B, N, seed, noise, sdf_cost=False):
     return prob, x0, lin
 
 
-@pytest.mark.parametrize("B,N,seed,noise,sdf_cost", [(3, 20, 1, 0.05, False), (2, 40, 2, 0.05, False),
-                                                     (2, 12, 7, 0.5, False), (2, 20, 4, 0.2, True)])
-def test_riccati_ipm_matches_dense_ipm(oracle_lib, cfg, B, N, seed, noise, sdf_cost):
+def _exact(q):
+    """The unique solution of the QP, pinned two ways: the dense KKT IPM, and its active-set polish (one
+    equality-constrained KKT solve on the IPM's active rows, no barrier ill-conditioning)."""
+    import qp_oracle
+    d = qp_oracle.solve_dense(q)
+    p = qp_oracle.polish(q, d)
+    assert p["max_violation"] < 1e-9 and p["min_dual"] > -1e-9  # a KKT point: feasible, duals >= 0
+    for k in ("du", "dx", "sl", "su"):
+        np.testing.assert_allclose(d[k], p[k], rtol=0, atol=DENSE_ATOL)
+    return p
+
+
+@pytest.mark.parametrize("B,N,seed,noise,sdf_cost,lm_scaling", [
+    (3, 20, 1, 0.05, False, True), (2, 40, 2, 0.05, False, True), (2, 12, 7, 0.5, False, True),
+    (2, 20, 4, 0.2, True, True), (3, 60, 5, 0.1, False, True), (2, 40, 2, 0.05, False, False)])
+def test_riccati_ipm_matches_dense_ipm(oracle_lib, cfg, B, N, seed, noise, sdf_cost, lm_scaling):
     import qp_oracle
     model = Quad(_with_flags(cfg, sdf_cost=sdf_cost))
     assert model.ny == (12 if sdf_cost else 11)
     prob, x0, lin = _instance_set(oracle_lib, cfg, B, N, seed, noise, sdf_cost)
-    r = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=1e-10)
+    r = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, lm_scaling=lm_scaling)
     assert (r["status"] == 0).all()
+    assert (r["res"] < QP_TOL).all()
     for b in range(B):
         q = qp_oracle.stage_qp({k: v[b] for k, v in lin.items()}, prob["x"][b], prob["u"][b], x0[b], prob["yref"][b],
-                               prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], model, 10.0)
-        ref = qp_oracle.solve_dense(q)
+                               prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], model, 10.0,
+                               lm_scaling=lm_scaling)
+        ref = _exact(q)
         np.testing.assert_allclose(r["du"][b], ref["du"], rtol=0, atol=SOL_ATOL)
         np.testing.assert_allclose(r["dx"][b], ref["dx"], rtol=0, atol=SOL_ATOL)
         np.testing.assert_allclose(r["slack"][b][..., 0], ref["sl"], rtol=0, atol=SOL_ATOL)
         np.testing.assert_allclose(r["slack"][b][..., 1], ref["su"], rtol=0, atol=SOL_ATOL)
+
+
+def test_lm_scaling_changes_the_qp(oracle_lib, cfg):
+    """acados adds Ts_k * levenberg_marquardt at k < N and lm at N: the option is live in both oracles."""
+    import qp_oracle
+    model = Quad(cfg)
+    prob, x0, lin = _instance_set(oracle_lib, cfg, 1, 20, 1, 0.05)
+    a = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, lm_scaling=True)
+    b = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, lm_scaling=False)
+    assert np.abs(a["du"] - b["du"]).max() > 1e-3
+    q = qp_oracle.stage_qp({k: v[0] for k, v in lin.items()}, prob["x"][0], prob["u"][0], x0[0], prob["yref"][0],
+                           prob["W"][0], prob["yN"][0], prob["WN"][0], prob["dt"], model, 10.0)
+    np.testing.assert_allclose(np.diag(q["H"][3]) - np.diag(qp_oracle.stage_qp(
+        {k: v[0] for k, v in lin.items()}, prob["x"][0], prob["u"][0], x0[0], prob["yref"][0], prob["W"][0],
+        prob["yN"][0], prob["WN"][0], prob["dt"], model, 10.0, lm_scaling=False)["H"][3]),
+        10.0 * prob["dt"][3] - 10.0, rtol=1e-12)
+
+
+def test_riccati_ipm_nan_instance_fails_alone(oracle_lib, cfg):
+    """A NaN in one instance's linearisation: status 2 (QP failure) for it, the others unaffected."""
+    model = Quad(cfg)
+    prob, x0, lin = _instance_set(oracle_lib, cfg, 3, 20, 1, 0.05)
+    good = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL)
+    lin["Jh"][1, 5, 2, 2] = np.nan
+    bad = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL)
+    assert list(bad["status"]) == [0, 2, 0]
+    assert bad["iters"][1] <= 1
+    for b in (0, 2):
+        assert np.array_equal(good["du"][b], bad["du"][b])
 
 
 def test_riccati_ipm_threads_and_batch_invariance(oracle_lib, cfg):
@@ -65,7 +111,7 @@ def test_riccati_ipm_threads_and_batch_invariance(oracle_lib, cfg):
 def test_riccati_ipm_solution_is_feasible(oracle_lib, cfg):
     model = Quad(cfg)
     prob, x0, lin = _instance_set(oracle_lib, cfg, 4, 40, 11, 0.3)
-    r = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=1e-9)
+    r = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL)
     assert (r["status"] == 0).all()
     u = prob["u"] + r["du"]
     assert (u >= model.lbu - 1e-7).all() and (u <= model.ubu + 1e-7).all()
