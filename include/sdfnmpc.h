@@ -28,6 +28,12 @@
  *   sdfnmpc_rti_apply                  the SQP-RTI full step x <- x + dx, u <- u + du and u_0
  *                                      (solve_for_x0's return value, ocp.py:169)
  *   sdfnmpc_shooting_grid              Ocp.__init__ shooting nodes / time steps (ocp.py:18-27)
+ *   sdfnmpc_solver_*                   the AcadosOcpSolver object Ocp builds (ocp.py:127) and drives:
+ *                                      solver.set(k, 'x'|'u'|'p') / cost_set(k, 'yref'|'W') (ocp.py:
+ *                                      146-170) -> _upload; solver.get -> _download; reset + init
+ *                                      (ocp.py:144-153) -> _init; shift (ocp.py:156-160) -> _shift;
+ *                                      solve_for_x0 (ocp.py:169) -> _step + _wait.  It owns the device
+ *                                      workspace of B instances, so a controller needs no tensor library
  *
  * The CasADi external-function symbols that acados links (sdf_l4c, jac_sdf_l4c, ...) are in
  * sdf_l4c.h / libsdf_l4c.so.
@@ -173,6 +179,7 @@ int sdfnmpc_ctx_set_stream(sdfnmpc_ctx* ctx, void* hip_stream);
 /* launch on the legacy null stream (handle 0, e.g. PyTorch's default stream) */
 int sdfnmpc_ctx_use_null_stream(sdfnmpc_ctx* ctx);
 void* sdfnmpc_ctx_stream(sdfnmpc_ctx* ctx);
+int sdfnmpc_ctx_device(const sdfnmpc_ctx* ctx);
 int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx);
 /* rows per SDF workgroup: 32 (2 workgroups / CU) or 64 (1 workgroup / CU); default 32 */
 int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows);
@@ -244,6 +251,49 @@ int sdfnmpc_vae_size_latent(const sdfnmpc_vae* vae);
  * is owned by the encoder object and grows with B. */
 int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* vae, const sdfnmpc_vae_opts* opts, const void* img,
                        float* latent, double* latent64);
+
+/* ---- device memory on a context (inputs of the device-side setters without a tensor library) ----
+ * memcpy kind: 1 host -> device, 2 device -> host, 3 device -> device; ordered on the context stream,
+ * synchronous (returns when the copy has completed). */
+int sdfnmpc_dev_alloc(sdfnmpc_ctx* ctx, size_t bytes, void** out);
+void sdfnmpc_dev_free(sdfnmpc_ctx* ctx, void* ptr);
+int sdfnmpc_memcpy(sdfnmpc_ctx* ctx, void* dst, const void* src, size_t bytes, int kind);
+
+/* ---- the batched SQP-RTI solver object (owns its device workspace) ----
+ * Fields (name: [B][nodes][width] fp64 unless noted): x [N+1][10], u [N][4], p [N+1][np], x0 [1][10],
+ * yref / W [N][ny], yNref / WN [1][4], u0 [1][4], dx [N+1][10], du [N][4], the sdfnmpc_lin_args outputs
+ * xn, AB, y, Jy, yN, JyN, h, Jh, res [1][2], status / iters [1][1] int32.  A field's device pointer may
+ * be handed to the lower-level entry points (e.g. sdfnmpc_pack_refs or sdfnmpc_vae_encode writing p). */
+typedef struct sdfnmpc_solver sdfnmpc_solver;
+
+typedef struct {
+    int B, N, np, ny;          /* instances, horizon, parameters per node, stage residuals (11 / 12) */
+    int latent_mode;           /* as sdfnmpc_lin_args.latent_mode */
+    const double* dt;          /* [N] shooting-grid steps (host; copied) */
+    sdfnmpc_quad_model model;
+    sdfnmpc_qp_opts qp;        /* qp.ny == ny */
+} sdfnmpc_solver_opts;
+
+int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_solver_opts* opts,
+                          sdfnmpc_solver** out);
+void sdfnmpc_solver_destroy(sdfnmpc_solver* s);
+int sdfnmpc_solver_field(sdfnmpc_solver* s, const char* name, void** dev, int* nodes, int* width);
+/* host [B][nodes][width] (the caller's full mirror of the field): columns [col0, col0 + ncol) of the rows
+ * r = b * nodes + k with row_mask[r] != 0 (row_mask NULL: every row) -> device.  Asynchronous: the data
+ * is staged in pinned memory before the call returns, so host may be reused at once. */
+int sdfnmpc_solver_upload(sdfnmpc_solver* s, const char* name, int col0, int ncol, const unsigned char* row_mask,
+                          const double* host);
+/* the whole field -> host [B][nodes][width] (synchronous) */
+int sdfnmpc_solver_download(sdfnmpc_solver* s, const char* name, void* host);
+/* reset + init (ocp.py:144-153): x0 = x_k = x0[b] for k = 0..N, u_k = u_init[4], dx = du = 0 */
+int sdfnmpc_solver_init(sdfnmpc_solver* s, const double* x0, const double* u_init);
+/* shift (ocp.py:156-160): x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (k <= 0 or k >= N: no-op) */
+int sdfnmpc_solver_shift(sdfnmpc_solver* s, int k);
+/* enqueue one SQP-RTI iteration: x_0 = x0, preparation phase, QP, full step (failed instances keep their
+ * iterate), then u_0 / status / iterations into pinned host memory.  Asynchronous. */
+int sdfnmpc_solver_step(sdfnmpc_solver* s);
+/* wait for the stream; copy the last step's u0 [B][4], status [B], iters [B] (each may be NULL) */
+int sdfnmpc_solver_wait(sdfnmpc_solver* s, double* u0, int* status, int* iters);
 
 /* ---- shooting grid (host, bit-exact numpy.linspace/diff semantics of ocp.py:21-27) ---- */
 int sdfnmpc_shooting_grid(int N, double T, int uniform, int nb_short_nodes, double dt_short, double* nodes,

@@ -28,6 +28,10 @@ SYMBOLS = [
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
     "sdfnmpc_linearize", "sdfnmpc_shooting_grid", "sdfnmpc_qp_solve", "sdfnmpc_rti_apply", "sdfnmpc_pack_refs",
     "sdfnmpc_vae_load", "sdfnmpc_vae_free", "sdfnmpc_vae_size_latent", "sdfnmpc_vae_encode",
+    "sdfnmpc_ctx_device", "sdfnmpc_dev_alloc", "sdfnmpc_dev_free", "sdfnmpc_memcpy",
+    "sdfnmpc_solver_create", "sdfnmpc_solver_destroy", "sdfnmpc_solver_field", "sdfnmpc_solver_upload",
+    "sdfnmpc_solver_download", "sdfnmpc_solver_init", "sdfnmpc_solver_shift", "sdfnmpc_solver_step",
+    "sdfnmpc_solver_wait",
 ]
 L4C_SYMBOLS = [
     f"{p}sdf_l4c{s}" for p in ("", "jac_", "adj1_")
@@ -82,6 +86,11 @@ class VaeOptsC(C.Structure):
                 ("yz", C.c_void_p)]
 
 
+class SolverOptsC(C.Structure):
+    _fields_ = [("B", C.c_int), ("N", C.c_int), ("np", C.c_int), ("ny", C.c_int), ("latent_mode", C.c_int),
+                ("dt", C.POINTER(C.c_double)), ("model", QuadModelC), ("qp", QpOptsC)]
+
+
 class QpArgsC(C.Structure):
     _fields_ = [("B", C.c_int), ("N", C.c_int)] + [(n, C.c_void_p) for n in QP_IN + QP_OUT]
 
@@ -131,6 +140,19 @@ def load():
         "sdfnmpc_vae_free": (None, [vp]),
         "sdfnmpc_vae_size_latent": (i, [vp]),
         "sdfnmpc_vae_encode": (i, [vp, vp, P(VaeOptsC), vp, vp, vp]),
+        "sdfnmpc_ctx_device": (i, [vp]),
+        "sdfnmpc_dev_alloc": (i, [vp, sz, P(vp)]),
+        "sdfnmpc_dev_free": (None, [vp, vp]),
+        "sdfnmpc_memcpy": (i, [vp, vp, vp, sz, i]),
+        "sdfnmpc_solver_create": (i, [vp, vp, P(SolverOptsC), P(vp)]),
+        "sdfnmpc_solver_destroy": (None, [vp]),
+        "sdfnmpc_solver_field": (i, [vp, C.c_char_p, P(vp), P(i), P(i)]),
+        "sdfnmpc_solver_upload": (i, [vp, C.c_char_p, i, i, vp, vp]),
+        "sdfnmpc_solver_download": (i, [vp, C.c_char_p, vp]),
+        "sdfnmpc_solver_init": (i, [vp, vp, vp]),
+        "sdfnmpc_solver_shift": (i, [vp, i]),
+        "sdfnmpc_solver_step": (i, [vp]),
+        "sdfnmpc_solver_wait": (i, [vp, vp, vp, vp]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -191,6 +213,10 @@ class Context:
     @property
     def stream(self) -> int:
         return load().sdfnmpc_ctx_stream(self.h)
+
+    @property
+    def device_index(self) -> int:
+        return int(load().sdfnmpc_ctx_device(self.h))
 
     def enable_timing(self, on=True):
         _check(load().sdfnmpc_ctx_enable_timing(self.h, int(on)))
@@ -377,9 +403,137 @@ def vae_opts(cfg, clip: float) -> VaeOptsC:
 
 
 def vae_encode(ctx: Context, vae: Vae, opts: VaeOptsC, img, yz, latent, latent64=None, depth2range=True):
-    """Enqueue sdfnmpc_vae_encode: img device tensor [B][H][W] (float32 or uint16), latent [B][L] fp32."""
-    import torch
-
-    o = VaeOptsC(int(img.shape[0]), int(img.shape[-2]), int(img.shape[-1]), 1 if img.dtype == torch.uint16 else 0,
+    """Enqueue sdfnmpc_vae_encode: img device array [B][H][W] (float32 or uint16; a DeviceArray or a torch
+    tensor), latent [B][L] fp32."""
+    o = VaeOptsC(int(img.shape[0]), int(img.shape[-2]), int(img.shape[-1]), 1 if "uint16" in str(img.dtype) else 0,
                  float(opts.clip), _ptr(yz) if depth2range else None)
     _check(load().sdfnmpc_vae_encode(ctx.h, vae.h, C.byref(o), _ptr(img), _ptr(latent), _ptr(latent64)))
+
+
+class DeviceArray:
+    """A device buffer on a context, with numpy-style shape / dtype (the tensor-free way to hand device
+    inputs to the entry points).  ``data_ptr()`` makes it usable wherever a torch tensor is accepted."""
+
+    def __init__(self, ctx: Context, shape, dtype=np.float64):
+        self.ctx, self.shape, self.dtype = ctx, tuple(int(v) for v in shape), np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        p = C.c_void_p()
+        _check(load().sdfnmpc_dev_alloc(ctx.h, self.nbytes, C.byref(p)))
+        self.ptr = p.value
+
+    @classmethod
+    def from_numpy(cls, ctx: Context, a, dtype=None):
+        a = np.ascontiguousarray(a, dtype=dtype)
+        d = cls(ctx, a.shape, a.dtype)
+        d.upload(a)
+        return d
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+    def upload(self, a):
+        a = np.ascontiguousarray(a, dtype=self.dtype)
+        if a.nbytes != self.nbytes:
+            raise ValueError(f"upload of {a.nbytes} bytes into a {self.nbytes}-byte device array")
+        _check(load().sdfnmpc_memcpy(self.ctx.h, self.ptr, a.ctypes.data, self.nbytes, 1))
+
+    def numpy(self) -> np.ndarray:
+        out = np.empty(self.shape, self.dtype)
+        _check(load().sdfnmpc_memcpy(self.ctx.h, out.ctypes.data, self.ptr, self.nbytes, 2))
+        return out
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            load().sdfnmpc_dev_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class FieldView:
+    """A solver field's device memory (borrowed: owned by the Solver) -- data_ptr() / shape for the
+    lower-level entry points that write it in place (sdfnmpc_pack_refs, sdfnmpc_vae_encode)."""
+
+    def __init__(self, ptr: int, shape, dtype):
+        self.ptr, self.shape, self.dtype = ptr, tuple(shape), np.dtype(dtype)
+
+    def data_ptr(self) -> int:
+        return self.ptr
+
+
+class Solver:
+    """sdfnmpc_solver: B instances' SQP-RTI workspace on one context, driven with host arrays."""
+
+    INT_FIELDS = ("status", "iters")
+
+    def __init__(self, ctx: Context, net: Net, model: QuadModelC, qp: QpOptsC, B: int, N: int, np_: int, ny: int,
+                 dt, latent_mode: int = 0):
+        self.ctx, self.net, self.B, self.N, self.np, self.ny = ctx, net, int(B), int(N), int(np_), int(ny)
+        self._dt = np.ascontiguousarray(dt, dtype=np.float64)
+        o = SolverOptsC(self.B, self.N, self.np, self.ny, int(latent_mode),
+                        self._dt.ctypes.data_as(C.POINTER(C.c_double)), model, qp)
+        h = C.c_void_p()
+        _check(load().sdfnmpc_solver_create(ctx.h, net.h, C.byref(o), C.byref(h)))
+        self.h = h
+        self.u0 = np.zeros((self.B, 4))
+        self.status = np.zeros(self.B, np.int32)
+        self.iters = np.zeros(self.B, np.int32)
+
+    def shape(self, name: str):
+        nodes, width = C.c_int(), C.c_int()
+        _check(load().sdfnmpc_solver_field(self.h, name.encode(), None, C.byref(nodes), C.byref(width)))
+        return (self.B, nodes.value, width.value)
+
+    def field(self, name: str) -> FieldView:
+        p, nodes, width = C.c_void_p(), C.c_int(), C.c_int()
+        _check(load().sdfnmpc_solver_field(self.h, name.encode(), C.byref(p), C.byref(nodes), C.byref(width)))
+        return FieldView(p.value, (self.B, nodes.value, width.value), np.int32 if name in self.INT_FIELDS else np.float64)
+
+    def upload(self, name: str, host, col0: int = 0, ncol=None, mask=None):
+        """host: the full [B][nodes][width] mirror (or anything broadcastable to it); mask [B][nodes] of rows."""
+        shp = self.shape(name)
+        a = np.ascontiguousarray(np.broadcast_to(np.asarray(host, dtype=np.float64), shp))
+        ncol = shp[2] - col0 if ncol is None else int(ncol)
+        m = None
+        if mask is not None:
+            m = np.ascontiguousarray(np.broadcast_to(np.asarray(mask, dtype=bool), shp[:2]), dtype=np.uint8)
+            if not m.any():
+                return
+        _check(load().sdfnmpc_solver_upload(self.h, name.encode(), int(col0), ncol,
+                                             None if m is None else m.ctypes.data, a.ctypes.data))
+
+    def download(self, name: str) -> np.ndarray:
+        shp = self.shape(name)
+        out = np.empty(shp, np.int32 if name in self.INT_FIELDS else np.float64)
+        _check(load().sdfnmpc_solver_download(self.h, name.encode(), out.ctypes.data))
+        return out
+
+    def init(self, x0, u_init):
+        x0 = np.ascontiguousarray(np.broadcast_to(np.asarray(x0, dtype=np.float64), (self.B, 10)))
+        u = np.ascontiguousarray(u_init, dtype=np.float64)
+        _check(load().sdfnmpc_solver_init(self.h, x0.ctypes.data, u.ctypes.data))
+
+    def shift(self, k: int):
+        _check(load().sdfnmpc_solver_shift(self.h, int(k)))
+
+    def step(self):
+        _check(load().sdfnmpc_solver_step(self.h))
+
+    def wait(self):
+        _check(load().sdfnmpc_solver_wait(self.h, self.u0.ctypes.data, self.status.ctypes.data, self.iters.ctypes.data))
+        return self.u0
+
+    def close(self):
+        if getattr(self, "h", None):
+            load().sdfnmpc_solver_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -12,6 +12,12 @@ an optional leading batch dimension (``batch`` instances solved together, one SQ
   solve()                              controller.py:74    shift + one RTI iteration; returns fail_count
   get_matrices(), get_u(), get_cmd_acc(), get_cmd_TRPYr(), get_openloop_traj(), eval(k), set_ref(ref, k)
 
+Host setters write the host arrays (``p``, ``y``, ``W``, ``yN``, ``WN``) and mark the rows and columns
+they touched; ``solve`` uploads exactly those regions.  Device-side setters (``gen_refs_device``,
+``set_latent_device``, ``VaeWrapper.encode_to``) write the solver's device buffers directly and clear
+the host marks of what they wrote.  The last writer of a region wins, whichever side it is on.
+No tensor library is used on this path.
+
 ``get_cmd_props`` exists in the reference only for the 'props' model; this build is the 'att' model
 (model.Quad), where the reference raises AttributeError too.
 """
@@ -48,10 +54,41 @@ class Nmpc:
     def _shape(self, *s):
         return s if self.B == 1 else (self.B,) + s
 
+    # ---- dirty regions of the host arrays: (field, col0, ncol) -> row mask [B][nodes]
+    def _groups(self):
+        idx, m = self.cfg.mpc.p_idx, self.model
+        return {"flag": ("p", int(idx.flag), 1), "pose": ("p", int(idx.W_p_Co[0]), 12),
+                "q_d": ("p", int(idx.q_d[0]), 4), "latent": ("p", int(idx.latent), m.np - int(idx.latent)),
+                "yref": ("yref", 0, m.ny), "W": ("W", 0, m.ny), "yNref": ("yNref", 0, m.nyN), "WN": ("WN", 0, m.nyN)}
+
+    def _mark(self, group, b=None, k=None):
+        """Mark rows (instance b or all, node k or all) of a column group dirty."""
+        field, _, _ = self._groups()[group]
+        nodes = {"p": self.N + 1, "yref": self.N, "W": self.N}.get(field, 1)
+        m = self._dirty.setdefault(group, np.zeros((max(self.B, 1), nodes), bool))
+        m[(slice(None) if b is None else b), (slice(None) if k is None else k)] = True
+
+    def _flush(self):
+        """Upload the dirty host regions into the solver's device buffers."""
+        host = {"p": self.p, "yref": self.y, "W": self.W, "yNref": self.yN, "WN": self.WN}
+        groups = self._groups()
+        for g, mask in self._dirty.items():
+            field, col0, ncol = groups[g]
+            a = host[field]
+            a = a[None] if self.B == 1 else a
+            if field in ("yNref", "WN"):
+                a = a[:, None]
+            self.ocp.upload(field, a, col0, ncol, mask)
+        self._dirty = {}
+
+    def _clean(self, *groups):
+        for g in groups:
+            self._dirty.pop(g, None)
+
     def reset(self):
         """Reset internal matrices to default values (controller.py:35-44)."""
         m = self.model
-        self._dev_params = False
+        self._dirty = {}
         self.x0 = None
         self.p = np.zeros(self._shape(self.N + 1, m.np))
         self.y = np.zeros(self._shape(self.N, m.ny))
@@ -61,24 +98,27 @@ class Nmpc:
         self.fail_count = 0
         self.set_sdf_flag(False)
         self.reset_latent()
+        for g in ("q_d", "yref", "W", "yNref", "WN"):
+            self._mark(g)
 
     # ---- parameter setters
     def set_sdf_flag(self, flag):
         """Enable/disable the sdf constraint (controller.py:47-49); flag: scalar or [B]."""
         f = np.asarray(flag, dtype=float)
-        self._dev_params = False
         self.p[..., self.cfg.mpc.p_idx.flag] = f[..., None] if f.ndim else f
+        self._mark("flag")
 
     def set_latent(self, latent, W_p_Bo, W_R_Bo):
         """Latent and camera pose at the time of the image (controller.py:52-56), batched over a leading dim."""
         idx = self.cfg.mpc.p_idx
-        self._dev_params = False
         W_R_Bo = np.asarray(W_R_Bo, dtype=float)
         W_p_Co = W_R_Bo @ np.asarray(self.cfg.sensor.B_p_C, dtype=float).ravel() + W_p_Bo
         W_R_Co = (W_R_Bo @ np.asarray(self.cfg.sensor.B_R_C, dtype=float)).reshape(W_R_Bo.shape[:-2] + (9,))
         self.p[..., idx.W_p_Co] = np.asarray(W_p_Co)[..., None, :]
         self.p[..., idx.W_R_Co] = W_R_Co[..., None, :]
         self.p[..., idx.latent:] = np.asarray(latent, dtype=float)[..., None, :]
+        self._mark("pose")
+        self._mark("latent")
 
     def reset_latent(self):
         """controller.py:59-63."""
@@ -86,6 +126,8 @@ class Nmpc:
         self.p[..., idx.W_p_Co] = 0
         self.p[..., idx.W_R_Co] = 0
         self.p[..., idx.latent:] = 0
+        self._mark("pose")
+        self._mark("latent")
 
     # ---- control iteration
     def set_x0(self, x0):
@@ -99,10 +141,8 @@ class Nmpc:
         """One SQP-RTI iteration for every instance (controller.py:74-83)."""
         try:
             self.ocp.shift(self.cfg.mpc.shift)
-            if self._dev_params:  # references / parameters live in the device buffers (gen_refs_device)
-                self.ocp.solve(self.x0, None, None, None, None, None)
-            else:
-                self.ocp.solve(self.x0, self.y, self.yN, self.W, self.WN, self.p)
+            self._flush()  # host-set regions; device-set regions are already in place
+            self.ocp.solve(self.x0, None, None, None, None, None)
             self.fail_count = 0
         except Exception as e:  # same contract as the reference: report, count, keep running
             print("solver failed:", e)
@@ -112,8 +152,8 @@ class Nmpc:
     # ---- getters
     def get_matrices(self):
         """x [.., N+1, nx], u [.., N, nu] of the current iterate (controller.py:87-96)."""
-        x = self.ocp.bufs["x"].cpu().numpy()
-        u = self.ocp.bufs["u"].cpu().numpy()
+        x = self.ocp.download("x")
+        u = self.ocp.download("u")
         return (x[0], u[0]) if self.B == 1 else (x, u)
 
     def get_u(self):
@@ -145,7 +185,7 @@ class Nmpc:
         """The model's evaluation vector at node k: the SDF value with flag = 1 (gen_model.py:64,
         controller.py:128-133), at the current iterate, computed by the HIP SDF kernel."""
         idx = self.cfg.mpc.p_idx
-        x = self.ocp.bufs["x"][:, k].cpu().numpy()
+        x = self.ocp.download("x")[:, k]
         p = self.p if self.B > 1 else self.p[None]
         pk = p[:, k]
         W_R_Co = pk[:, idx.W_R_Co].reshape(-1, 3, 3)
@@ -154,44 +194,36 @@ class Nmpc:
         return df[:1] if self.B == 1 else df[:, None]
 
     # ---- device-side parameter packing (csrc/ref_pack.hip)
-    def _dev(self, a, dtype=None):
-        import torch
-        if torch.is_tensor(a):  # already a tensor (e.g. VaeWrapper's device latents): no host round trip
-            return a.to(device=self.ocp.device, dtype=torch.float64).contiguous()
-        return torch.as_tensor(np.array(a, dtype=np.float64, order="C"), device=self.ocp.device)
-
-    def _to_device(self):
-        """First switch to the device path: upload the host parameters once."""
-        if not self._dev_params:
-            m = self.model
-            for name, v, shape in (("p", self.p, (self.N + 1, m.np)), ("yref", self.y, (self.N, m.ny)),
-                                   ("W", self.W, (self.N, m.ny)), ("yNref", self.yN, (m.nyN,)),
-                                   ("WN", self.WN, (m.nyN,))):
-                self.ocp._put(name, v, shape)
+    def _dev(self, a):
+        """Host array -> device (fp64); a device array (DeviceArray / FieldView / torch tensor) passes through."""
+        from . import _lib
+        if hasattr(a, "data_ptr"):
+            if np.dtype(str(a.dtype).replace("torch.", "")) != np.float64:
+                raise TypeError(f"device input must be float64, got {a.dtype}")
+            return a
+        return _lib.DeviceArray.from_numpy(self.ocp.ctx, np.asarray(a, dtype=np.float64))
 
     def gen_refs_device(self, mode="wps", wps=None, vw=None, weights=None):
         """RefGen + formate_ref + set_ref for every instance and node in one kernel launch, written straight
-        into the OCP's device buffers (p[:, :, q_d], y, W, yN, WN).
+        into the solver's device buffers (p[:, :, q_d], y, W, yN, WN).
 
         mode 'wps': ``RefGen.gen_ref_list_wps`` (ref_gen.py:25-99) from x0 (``set_x0``) through the
         waypoints ``wps = (p [B][n][3], q [B][n][4])`` (or a list of ``Waypoint`` for B = 1); 'joystick':
         ``gen_ref_joystick(vw)`` (ref_gen.py:101-130), vw [B][4]; 'hover': ``from_x0`` (ref_gen.py:17-23).
         ``weights`` is the weight set formate_ref reads (e.g. ``Ref(cfg).W_on``); the joystick mode zeroes
-        its position weights as gen_ref_joystick does.  Until a host setter is called again, ``solve``
-        uses the device buffers for y, W, yN, WN and p.
+        its position weights as gen_ref_joystick does.  The host arrays of these regions are not updated;
+        a later host setter of a region (e.g. set_ref at one node) overrides it at the next ``solve``.
         """
         from . import _lib
-        from .ref_gen import weight_row
         from .reference import Ref
         if self.x0 is None:
             raise ValueError("set_x0 before gen_refs_device (the references start at the current state)")
         Bn = max(self.B, 1)
         ws = weights if weights is not None else Ref(self.cfg).W_on
-        wrow = weight_row(self.model, ws)
+        wrow = self.model.weight_row(ws)
         code = {"wps": 0, "joystick": 1, "hover": 2}[mode]
         if code == 1:
             wrow[:3] = 0.0  # ref.Wp = [0, 0, 0] (ref_gen.py:122)
-        bufs = self.ocp.bufs
         args = {"x0": self._dev(np.reshape(self.x0, (Bn, -1))), "wrow": self._dev(wrow)}
         n_wp = 0
         if code == 0:
@@ -203,38 +235,42 @@ class Nmpc:
             args.update(wp_p=self._dev(wp_p), wp_q=self._dev(wp_q))
         elif code == 1:
             args["vw"] = self._dev(np.reshape(np.asarray(vw, float), (Bn, 4)))
-        for k in ("p", "W", "WN"):
-            args[k] = bufs[k]
-        args["yref"], args["yNref"] = bufs["yref"], bufs["yNref"]
-        self._to_device()
+        for k in ("p", "yref", "W", "yNref", "WN"):
+            args[k] = self.ocp.field(k)
         _lib.pack_refs(self.ocp.ctx, _lib.ref_opts(self.cfg, code), Bn, self.N, self.model.np, self.model.ny, args,
                        n_wp=n_wp)
-        self._dev_params = True
+        self.ocp.ctx.synchronize()  # the temporary inputs are freed on return
+        self._clean("q_d", "yref", "W", "yNref", "WN")
 
     def set_latent_device(self, latent, W_p_Bo, W_R_Bo, flag=None):
-        """set_latent (+ set_sdf_flag) on the device buffers for every instance (controller.py:45-54)."""
+        """set_latent (+ set_sdf_flag) on the device buffers for every instance (controller.py:45-54);
+        latent: host array or a device array [B][L] fp64 (e.g. VaeWrapper's latents, no host round trip)."""
         from . import _lib
         Bn = max(self.B, 1)
-        self._to_device()
         L = int(self.cfg.nn.size_latent)
-        lat = latent.reshape(Bn, L) if hasattr(latent, "data_ptr") else np.reshape(latent, (Bn, L))
+        lat = latent if hasattr(latent, "data_ptr") else np.reshape(latent, (Bn, L))
         args = {"latent": self._dev(lat), "W_p_Bo": self._dev(np.reshape(W_p_Bo, (Bn, 3))),
-                "W_R_Bo": self._dev(np.reshape(W_R_Bo, (Bn, 9))), "p": self.ocp.bufs["p"]}
+                "W_R_Bo": self._dev(np.reshape(W_R_Bo, (Bn, 9))), "p": self.ocp.field("p")}
         if flag is not None:
             args["flag"] = self._dev(np.broadcast_to(np.asarray(flag, float), (Bn,)))
         _lib.pack_refs(self.ocp.ctx, _lib.ref_opts(self.cfg, -1), Bn, self.N, self.model.np, self.model.ny, args, L=L)
-        self._dev_params = True
+        self.ocp.ctx.synchronize()
+        self._clean("pose", "latent", *(("flag",) if flag is not None else ()))
 
     def set_ref(self, ref, k, b=None):
         """y, W and q_d of node k from a reference object (controller.py:136-142); b selects one instance
         of a batch (None: all)."""
         sel = () if self.B == 1 else (slice(None),) if b is None else (b,)
-        self._dev_params = False
         self.p[sel + (k, self.cfg.mpc.p_idx.q_d)] = ref.q
+        self._mark("q_d", b, k)
         y, W = self.model.formate_ref(ref)
         if k < self.N:
             self.y[sel + (k,)] = y
             self.W[sel + (k,)] = W
+            self._mark("yref", b, k)
+            self._mark("W", b, k)
         else:
             self.WN[sel] = W[: self.model.nyN]
             self.yN[sel] = y[: self.model.nyN]
+            self._mark("yNref", b)
+            self._mark("WN", b)

@@ -38,6 +38,8 @@ static int fail(int code, const std::string& msg) {
     } while (0)
 
 extern "C" int sdfnmpc_abi_version(void) { return SDFNMPC_ABI_VERSION; }
+// error reporting for solver.hip (same thread-local message)
+extern "C" int sdfnmpc_solver_fail_(int code, const char* msg) { return fail(code, msg); }
 extern "C" const char* sdfnmpc_last_error(void) { return g_err.c_str(); }
 
 // ------------------------------------------------------------------------------------------------
@@ -167,6 +169,33 @@ extern "C" void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx) {
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;  // device buffers are freed by their destructors, on ctx->device
+}
+
+extern "C" int sdfnmpc_ctx_device(const sdfnmpc_ctx* ctx) { return ctx ? ctx->device : -1; }
+
+extern "C" int sdfnmpc_dev_alloc(sdfnmpc_ctx* ctx, size_t bytes, void** out) {
+    if (!ctx || !out) return fail(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_dev_alloc");
+    ScopedDevice sd(ctx->device);
+    *out = nullptr;
+    HIPCHK(hipMalloc(out, bytes ? bytes : 16));
+    return SDFNMPC_OK;
+}
+
+extern "C" void sdfnmpc_dev_free(sdfnmpc_ctx* ctx, void* ptr) {
+    if (!ctx || !ptr) return;
+    ScopedDevice sd(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(ptr);
+}
+
+extern "C" int sdfnmpc_memcpy(sdfnmpc_ctx* ctx, void* dst, const void* src, size_t bytes, int kind) {
+    if (!ctx || (bytes && (!dst || !src)) || kind < 1 || kind > 3) return fail(SDFNMPC_E_ARG, "bad sdfnmpc_memcpy arguments");
+    if (!bytes) return SDFNMPC_OK;
+    ScopedDevice sd(ctx->device);
+    const hipMemcpyKind k = kind == 1 ? hipMemcpyHostToDevice : kind == 2 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, k, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return SDFNMPC_OK;
 }
 
 // The legacy default (null) stream: PyTorch's default stream has the handle 0, which

@@ -107,6 +107,12 @@ class Quad:
         acc = np.einsum("...ji,...j->...i", W_R_B, W_a)
         return np.concatenate([acc, wz[..., None]], axis=-1)
 
+    def weight_row(self, weights) -> np.ndarray:
+        """The W row formate_ref builds from a weight set (Ref.W_on / W_off), as one array: what the
+        device-side reference packing (csrc/ref_pack.hip) writes for every node."""
+        w = weights
+        return np.concatenate([w.Wp, [w.Wq[2]], w.Wv, w.Wq[:2], w.Ww[2:], [w.Wa], self.extra_W]).astype(np.float64)
+
     def formate_ref(self, ref):
         """(y_ref, W) in the residual layout y = [p, q_e[3], v, roll, pitch, wz, W_a[2]]."""
         yr = np.concatenate([ref.p, [0], ref.v, [0, 0], [ref.wz], [0], np.zeros_like(self.extra_W)])

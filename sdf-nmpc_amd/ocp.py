@@ -4,8 +4,9 @@ The reference builds an acados OCP (NONLINEAR_LS cost, ERK, SQP_RTI, FULL_CONDEN
 constraints, input boxes; ocp.py:17-128) for ONE quadrotor and calls ``solve_for_x0`` per control
 step.  Here the same iteration -- preparation phase (csrc/sdf_mlp.hip + csrc/linearize.hip),
 feedback QP (csrc/rti_qp.hip) and the full-step iterate update -- runs for ``batch`` independent
-instances at once on one GPU, through the C ABI of include/sdfnmpc.h.  The method names, argument
-meaning and array layouts are the reference's (plus an optional leading batch dimension):
+instances at once, through the solver object of include/sdfnmpc.h (``sdfnmpc_solver``, which owns the
+device workspace: no tensor library is involved).  The method names, argument meaning and array
+layouts are the reference's (plus an optional leading batch dimension):
 
   Ocp(model, build)                   ocp.py:17    shooting grid, solver buffers
   init(x0)                            ocp.py:148   x_k = x0, u_k = u_hover
@@ -13,6 +14,11 @@ meaning and array layouts are the reference's (plus an optional leading batch di
   solve(x0, y, yN, W, WN, p)          ocp.py:163   one SQP-RTI iteration, u = u_0
   get_u(), get_t()                    ocp.py:175   last u_0, solve wall time [s]
   solver.get(k, 'x' | 'u'), solver.set(k, ...), solver.reset(), solver.get_stats('time_tot')
+
+Occupancy gate (north_star): with several ``devices`` the batch is split over as
+many GPUs as it needs to fill (``shard.plan``: one GPU runs up to ``shard.gpu_capacity(N)`` instances
+concurrently -- 1024 at N = 40), each part a contiguous instance range with its own context, network
+copy and solver; a step enqueues every part before waiting on any.
 
 ``build_solver`` (ocp.py:9) installs what an acados user links instead of the L4CasADi library: the
 CasADi external-function shim ``libsdf_l4c.so`` (include/sdf_l4c.h) and its weights, in
@@ -31,6 +37,7 @@ import warnings
 import numpy as np
 
 from . import _lib
+from . import shard
 from . import weights as Wt
 from .config import Config
 from .model import Quad
@@ -76,37 +83,50 @@ class _SolverView:
     def __init__(self, ocp: "Ocp"):
         self.ocp = ocp
 
-    def _buf(self, field):
+    @staticmethod
+    def _field(field):
         if field not in ("x", "u"):
             raise KeyError(f"field {field!r}: only 'x' and 'u' are exposed")
-        return self.ocp.bufs[field]
+        return field
 
     def get(self, k, field):
-        v = self._buf(field)[:, k].cpu().numpy()
+        v = self.ocp.download(self._field(field))[:, k]
         return v[0] if self.ocp.B == 1 else v
 
     def set(self, k, field, value):
-        import torch
-        buf = self._buf(field)
-        buf[:, k] = torch.as_tensor(np.asarray(value, dtype=np.float64), device=buf.device).expand_as(buf[:, k])
+        name = self._field(field)
+        nodes = self.ocp.N + 1 if name == "x" else self.ocp.N
+        full = np.zeros((self.ocp.B, nodes, 10 if name == "x" else 4))
+        full[:, k] = np.asarray(value, dtype=np.float64)
+        mask = np.zeros((self.ocp.B, nodes), bool)
+        mask[:, k] = True
+        self.ocp.upload(name, full, mask=mask)
 
     def reset(self):
-        for k in ("x", "u", "dx", "du"):
-            self.ocp.bufs[k].zero_()
+        for name in ("x", "u", "dx", "du"):
+            self.ocp.upload(name, 0.0)
 
     def get_stats(self, name):
         if name == "time_tot":
             return self.ocp.t
         if name == "qp_iter":
-            return self.ocp.bufs["iters"].cpu().numpy()
+            return self.ocp.iters
+        if name == "status":
+            return self.ocp.status
         raise KeyError(name)
+
+
+class _Part:
+    """One device's share of the batch: instances [lo, hi) on their own context / network / solver."""
+
+    def __init__(self, lo, hi, ctx, net, solver, own_ctx, own_net):
+        self.lo, self.hi, self.ctx, self.net, self.solver = lo, hi, ctx, net, solver
+        self.own_ctx, self.own_net = own_ctx, own_net
 
 
 class Ocp:
     def __init__(self, model: Quad, build=False, batch: int = 1, device: int = 0, net=None, ctx=None,
-                 weights=None, lm=None, qp_tol=1e-8, qp_iter_max=100):
-        import torch
-
+                 weights=None, lm=None, qp_tol=1e-8, qp_iter_max=100, devices=None, lm_scaling=True):
         self.model = model
         cfg = model.cfg
         self.T = cfg.mpc.T
@@ -118,75 +138,72 @@ class Ocp:
                                                           cfg.mpc.control_loop_time * 1e-3)
         if build:
             build_solver(weights=weights)
-        self.device = torch.device("cuda", device)
-        self.ctx = ctx or _lib.Context(device, stream=torch.cuda.current_stream(self.device).cuda_stream)
-        self.net = net or load_net(self.ctx, cfg, weights)
         self.cmodel = _lib.quad_model(cfg)
         # QP data of the model + solver options (ocp.py:113-120: LM regularisation, <= 100 iterations)
         self.qp_opts = _lib.qp_opts(model, lm=float(cfg.mpc.lm_reg if lm is None else lm), max_iter=qp_iter_max,
-                                    tol=qp_tol)
-        f64 = dict(dtype=torch.float64, device=self.device)
-        sh = dict(x=(B, N + 1, 10), u=(B, N, 4), p=(B, N + 1, model.np), x0=(B, 10), yref=(B, N, model.ny), W=(B, N, model.ny),
-                  yNref=(B, 4), WN=(B, 4), xn=(B, N, 10), AB=(B, N, 14, 10), y=(B, N, 11), Jy=(B, N, 14, 11),
-                  yN=(B, 4), JyN=(B, 10, 4), h=(B, N + 1, 3), Jh=(B, N + 1, 10, 3), dx=(B, N + 1, 10), du=(B, N, 4),
-                  slack=(B, N + 1, 3, 2), res=(B, 2), u0=(B, 4))
-        self.bufs = {k: torch.zeros(s, **f64) for k, s in sh.items()}
-        self.bufs["dt"] = torch.as_tensor(self.dt, **f64)
-        self.bufs["sdf"] = torch.zeros((B, N + 1, 4), dtype=torch.float32, device=self.device)
-        self.bufs["status"] = torch.zeros(B, dtype=torch.int32, device=self.device)
-        self.bufs["iters"] = torch.zeros(B, dtype=torch.int32, device=self.device)
+                                    tol=qp_tol, lm_scaling=lm_scaling)
+        devs = list(devices) if devices else [device]
+        self.plan = shard.plan(B, N, len(devs)) if ctx is None else [(0, 0, B)]
+        self.parts = []
+        for slot, lo, hi in self.plan:
+            c = ctx if ctx is not None else _lib.Context(devs[slot])
+            n = net if (net is not None and slot == 0) else load_net(c, cfg, weights)
+            s = _lib.Solver(c, n, self.cmodel, self.qp_opts, hi - lo, N, model.np, model.ny, self.dt)
+            self.parts.append(_Part(lo, hi, c, n, s, ctx is None, n is not net))
+        self.ctx, self.net = self.parts[0].ctx, self.parts[0].net
         self.solver = _SolverView(self)
         self.u = np.zeros((B, model.nu)) if B > 1 else np.zeros(model.nu)
         self.t = 0.0
         self.status = np.zeros(B, dtype=np.int32)
+        self.iters = np.zeros(B, dtype=np.int32)
 
-    # ---- helpers
-    def _put(self, name, value, shape):
-        """Copy host (numpy) or device (torch) data into the named buffer; a missing batch dim broadcasts."""
-        import torch
-        buf = self.bufs[name]
-        if isinstance(value, torch.Tensor):
-            v = value.to(device=buf.device, dtype=buf.dtype)
-        else:
-            v = torch.as_tensor(np.array(value, dtype=np.float64), device=buf.device)
-        if tuple(v.shape) == tuple(shape):
-            v = v.unsqueeze(0)
-        buf.copy_(v.expand_as(buf))
+    # ---- device buffers (host views through the solver object)
+    def upload(self, name, host, col0=0, ncol=None, mask=None):
+        """host / mask: full-batch arrays [B][nodes][width] / [B][nodes] (a missing batch dim broadcasts);
+        each part uploads its own instance rows."""
+        shp = self.parts[0].solver.shape(name)
+        full = np.broadcast_to(np.asarray(host, dtype=np.float64), (self.B,) + shp[1:])
+        m = None if mask is None else np.broadcast_to(np.asarray(mask, bool), (self.B, shp[1]))
+        for p in self.parts:
+            p.solver.upload(name, full[p.lo:p.hi], col0, ncol, None if m is None else m[p.lo:p.hi])
+
+    def download(self, name):
+        return np.concatenate([p.solver.download(name) for p in self.parts])
+
+    def field(self, name):
+        """Device memory of a field (single-part Ocp): a view for the device-side setters."""
+        if len(self.parts) != 1:
+            raise ValueError("field(): the batch is split over several devices; use each part's solver")
+        return self.parts[0].solver.field(name)
 
     # ---- the reference API
     def init(self, x0):
         """ocp.py:148-153: reset, x_k = x0 for k = 0..N, u_k = u_hover."""
-        self.solver.reset()
-        self._put("x0", x0, (10,))
-        self.bufs["x"].copy_(self.bufs["x0"].unsqueeze(1).expand_as(self.bufs["x"]))
-        self._put("u", np.broadcast_to(self.model.u_hover, (self.N, 4)), (self.N, 4))
+        x0 = np.broadcast_to(np.asarray(x0, dtype=np.float64), (self.B, 10))
+        for p in self.parts:
+            p.solver.init(x0[p.lo:p.hi], self.model.u_hover)
 
     def shift(self, k=1):
         """ocp.py:156-160: x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (x_N and the tail keep their values)."""
-        k = int(k)
-        if k > 0 and k < self.N:
-            x, u = self.bufs["x"], self.bufs["u"]
-            x[:, : self.N - k] = x[:, k: self.N].clone()
-            u[:, : self.N - k] = u[:, k: self.N].clone()
+        for p in self.parts:
+            p.solver.shift(int(k))
 
     def solve(self, x0, y, yN, W, WN, p):
         """ocp.py:163-172: set x0 / references / weights (diagonals) / parameters, one SQP-RTI iteration.
-        An argument given as None keeps the device buffer as it is (written by ref_gen.pack_refs)."""
+        An argument given as None keeps the device buffer as it is (uploaded by Nmpc or written by a
+        device-side setter)."""
         N, m = self.N, self.model
-        for name, v, shape in (("x0", x0, (m.nx,)), ("yref", y, (N, m.ny)), ("W", W, (N, m.ny)),
-                               ("yNref", yN, (m.nyN,)), ("WN", WN, (m.nyN,)), ("p", p, (N + 1, m.np))):
+        for name, v, shape in (("x0", x0, (1, m.nx)), ("yref", y, (N, m.ny)), ("W", W, (N, m.ny)),
+                               ("yNref", yN, (1, m.nyN)), ("WN", WN, (1, m.nyN)), ("p", p, (N + 1, m.np))):
             if v is not None:
-                self._put(name, v, shape)
-        b = self.bufs
-        b["x"][:, 0] = b["x0"]
+                self.upload(name, np.reshape(np.asarray(v, dtype=np.float64), (-1,) + shape))
         t0 = time.perf_counter()
-        _lib.linearize(self.ctx, self.net, self.cmodel, self.B, N, m.np, b)
-        _lib.qp_solve(self.ctx, self.qp_opts, self.B, N, b)
-        _lib.rti_apply(self.ctx, self.B, N, b["x"], b["u"], b["dx"], b["du"], b["u0"], status=b["status"])
-        self.ctx.synchronize()
+        for part in self.parts:  # every device busy before the host waits on any
+            part.solver.step()
+        u0 = np.concatenate([part.solver.wait().copy() for part in self.parts])
         self.t = time.perf_counter() - t0
-        self.status = b["status"].cpu().numpy()
-        u0 = b["u0"].cpu().numpy()
+        self.status = np.concatenate([part.solver.status for part in self.parts])
+        self.iters = np.concatenate([part.solver.iters for part in self.parts])
         self.u = u0[0] if self.B == 1 else u0
         if (self.status == 1).any():  # acados status 2 (QP max_iter): solve_for_x0 warns, keeps the step
             warnings.warn(f"QP reached qp_solver_iter_max on {(self.status == 1).sum()} of {self.B} instances")
@@ -202,5 +219,10 @@ class Ocp:
         return float(self.t)
 
     def close(self):
-        self.net.close()
-        self.ctx.close()
+        for p in self.parts:
+            p.solver.close()
+            if p.own_net:
+                p.net.close()
+            if p.own_ctx:
+                p.ctx.close()
+        self.parts = []

@@ -253,22 +253,20 @@ class VaeWrapper:
     """Mirror of the reference's ``VaeWrapper`` (sdf_nmpc/vae.py:7-50) over a batch of B images.
 
     ``set_img(img)`` takes one raw image [H, W] (B = 1, as the reference) or a batch [B, H, W] (numpy
-    float32 / uint16 or a torch CUDA tensor); ``encode()`` runs preprocessing + the encoder on the GPU
-    and returns the latent means [L] / [B, L] as numpy.  ``encode_to(nmpc)`` writes them straight into
-    an ``Nmpc``'s device parameters (set_latent on the device, no host round trip).
-    ``decode`` is not provided: the decoder is only used for visualisation (out of scope).
+    float32 / uint16, or a device array -- ``_lib.DeviceArray`` or a torch tensor, used in place);
+    ``encode()`` runs preprocessing + the encoder on the GPU and returns the latent means [L] / [B, L] as
+    numpy.  ``encode_to(nmpc)`` writes them straight into an ``Nmpc``'s device parameters (set_latent on
+    the device, no host round trip).  ``decode`` is not provided: the decoder is only used for
+    visualisation (out of scope).  No tensor library is needed.
     """
 
     def __init__(self, cfg, weights=None, batch: int = 1, device: int = 0, ctx=None, seed: int = 0):
-        import torch
-
         from . import _lib
 
         self.cfg = cfg
         self.B = int(batch)
-        self.device = torch.device("cuda", device)
         self._own_ctx = ctx is None
-        self.ctx = ctx if ctx is not None else _lib.Context(device, torch.cuda.current_stream(device).cuda_stream)
+        self.ctx = ctx if ctx is not None else _lib.Context(device)
         spec = EncoderSpec(size_latent=int(cfg.nn.size_latent), shape=tuple(cfg.sensor.shape_imgs[-2:]))
         if weights is None:
             weights = cfg.nn.get("vae_weights")
@@ -282,36 +280,39 @@ class VaeWrapper:
         self.spec = spec
         self.vae = _lib.Vae(self.ctx, pack(spec, params), self.B)
         yz = depth2range_table(spec.shape, cfg.sensor.hfov, cfg.sensor.vfov)
-        self.yz = torch.from_numpy(yz).to(self.device)
+        self.yz = _lib.DeviceArray.from_numpy(self.ctx, yz)
         self.opts = _lib.vae_opts(cfg, clip_scale(cfg) if not cfg.sensor.get("is_normalized", False) else 1.0)
         self.depth2range = bool(cfg.sensor.get("is_depth", True))
         self.img = None
-        self.latent = torch.zeros(self.B, spec.size_latent, dtype=torch.float32, device=self.device)
-        self.latent64 = torch.zeros(self.B, spec.size_latent, dtype=torch.float64, device=self.device)
+        self.latent = _lib.DeviceArray.from_numpy(self.ctx, np.zeros((self.B, spec.size_latent), np.float32))
+        self.latent64 = _lib.DeviceArray.from_numpy(self.ctx, np.zeros((self.B, spec.size_latent), np.float64))
 
     def set_img(self, img):
-        import torch
+        from . import _lib
 
-        t = img if torch.is_tensor(img) else torch.from_numpy(np.ascontiguousarray(img))
-        if t.dtype not in (torch.float32, torch.uint16, torch.int32, torch.float64):
-            t = t.to(torch.float32)
-        if t.dtype in (torch.float64, torch.int32):
-            t = t.to(torch.float32)
-        if t.dim() == 2:
-            t = t[None]
-        if t.shape[0] != self.B:
-            raise ValueError(f"expected {self.B} images, got {t.shape[0]}")
-        self.img = t.to(self.device).contiguous()
+        if hasattr(img, "data_ptr"):  # already on the device: [B][H][W] float32 / uint16, used in place
+            if tuple(img.shape)[0] != self.B or len(img.shape) != 3:
+                raise ValueError(f"expected a device array [{self.B}, H, W], got {tuple(img.shape)}")
+            self.img = img
+            return
+        a = np.asarray(img)
+        if a.dtype != np.uint16:
+            a = a.astype(np.float32)
+        if a.ndim == 2:
+            a = a[None]
+        if a.shape[0] != self.B:
+            raise ValueError(f"expected {self.B} images, got {a.shape[0]}")
+        if self.img is None or not isinstance(self.img, _lib.DeviceArray) or self.img.shape != a.shape or \
+                self.img.dtype != a.dtype:
+            self.img = _lib.DeviceArray(self.ctx, a.shape, a.dtype)
+        self.img.upload(a)
 
     def set_latent(self, latent):
-        import torch
-
-        t = latent if torch.is_tensor(latent) else torch.from_numpy(np.asarray(latent, dtype=np.float32))
-        self.latent.copy_(t.reshape(self.B, -1).to(self.device, torch.float32))
+        self.latent.upload(np.reshape(np.asarray(latent, dtype=np.float32), (self.B, -1)))
 
     def encode(self):
         self._run()
-        out = self.latent.cpu().numpy()
+        out = self.latent.numpy()
         return out[0] if self.B == 1 else out
 
     def _run(self):
@@ -322,6 +323,9 @@ class VaeWrapper:
                         depth2range=self.depth2range)
 
     def encode_to(self, nmpc, W_p_Bo, W_R_Bo, flag=None):
-        """encode + ``nmpc.set_latent_device`` with the fp64 latents (no host round trip)."""
+        """encode + ``nmpc.set_latent_device`` with the fp64 latents (no host round trip).  The encoder and
+        the controller may use different streams: the encoder's is drained first."""
         self._run()
+        if nmpc.ocp.ctx is not self.ctx:
+            self.ctx.synchronize()
         nmpc.set_latent_device(self.latent64, W_p_Bo, W_R_Bo, flag)

@@ -24,6 +24,9 @@ class StubOcp:
     def solve(self, *a):
         self.calls.append(("solve",) + tuple(np.array(v) for v in a))
 
+    def upload(self, name, host, col0=0, ncol=None, mask=None):
+        self.calls.append(("upload", name, col0, ncol, None if mask is None else np.array(mask), np.array(host)))
+
     def get_u(self):
         return np.zeros(4)
 
@@ -79,9 +82,41 @@ def test_reset_and_control_iteration_calls():
     assert [c[0] for c in n.ocp.calls] == ["init"]
     np.testing.assert_array_equal(n.ocp.calls[0][1], x0[:10])
     assert n.solve() == 0
-    assert [c[0] for c in n.ocp.calls] == ["init", "shift", "solve"]
+    kinds = [c[0] for c in n.ocp.calls]
+    assert kinds[:2] == ["init", "shift"] and kinds[-1] == "solve" and set(kinds[2:-1]) == {"upload"}
     assert n.ocp.calls[1][1] == n.cfg.mpc.shift
-    np.testing.assert_array_equal(n.ocp.calls[2][1], x0[:10] + 1)
+    np.testing.assert_array_equal(n.ocp.calls[-1][1], x0[:10] + 1)
+    # reset() marked everything: every column group of p and every reference field went up whole
+    up = {(c[1], c[2]) for c in n.ocp.calls if c[0] == "upload"}
+    assert up == {("p", 0), ("p", 1), ("p", 13), ("p", 17), ("yref", 0), ("W", 0), ("yNref", 0), ("WN", 0)}
+
+
+def test_solve_uploads_only_dirty_regions():
+    """host setters mark what they wrote; solve uploads exactly that (device-side writes of
+    other regions survive), and nothing twice."""
+    n = make(N=20)
+    n.set_x0(np.zeros(10))
+    n.solve()
+    n.ocp.calls.clear()
+    n.solve()
+    assert [c[0] for c in n.ocp.calls] == ["shift", "solve"]  # nothing dirty
+    n.ocp.calls.clear()
+    r = Ref(n.cfg)
+    r.p, r.q = np.ones(3), np.array([1.0, 0, 0, 0])
+    r.use_weights(r.W_on)
+    n.set_ref(r, 3)
+    n.solve()
+    ups = [c for c in n.ocp.calls if c[0] == "upload"]
+    assert sorted((c[1], c[2]) for c in ups) == [("W", 0), ("p", 13), ("yref", 0)]
+    for c in ups:
+        rows = np.flatnonzero(c[4].ravel())
+        assert list(rows) == [3], (c[1], rows)
+    # a device-side setter clears the host marks of the regions it wrote
+    n.ocp.calls.clear()
+    n.set_ref(r, 5)
+    n._clean("q_d", "yref", "W", "yNref", "WN")
+    n.solve()
+    assert [c[0] for c in n.ocp.calls] == ["shift", "solve"]
 
 
 def test_solver_failure_counts():

@@ -1,8 +1,10 @@
-"""Device-side reference / parameter packing (csrc/ref_pack.hip) against the host
-mirror RefGen -> formate_ref -> set_ref / set_latent (pinned bit-exact to the reference's RefGen by
-tests/test_ref_gen.py).  Exact except the quaternions (atan2 / sin / cos of the device libm, within an ulp
-of glibc) and the rotated camera pose (3-term dot products vs numpy's BLAS matmul)."""
-import copy
+"""Device-side reference / parameter packing (csrc/ref_pack.hip), pinned directly
+to the reference's own RefGen outputs (tests/golden/refgen_golden.npz, made by tests/golden/make_golden.py
+from sdf_nmpc/ref_gen.py:7-130 over every yaw mode, stop-and-turn on/off, joystick and from_x0) through
+formate_ref -> set_ref (quad_rollpitchyawrate.py:62-65, controller.py:133-142).  Exact except the
+quaternions (atan2 / sin / cos of the device libm, within an ulp or two of glibc) and the rotated camera
+pose (3-term dot products vs numpy's BLAS matmul)."""
+import os
 
 import numpy as np
 import pytest
@@ -11,93 +13,118 @@ from sdf_nmpc_amd import _lib
 from sdf_nmpc_amd.config import Config
 from sdf_nmpc_amd.controller import Nmpc
 from sdf_nmpc_amd.model import Quad
-from sdf_nmpc_amd.ref_gen import RefGen, weight_row
-from sdf_nmpc_amd.reference import Ref, Waypoint, yaw2quat
+from sdf_nmpc_amd.reference import Ref, yaw2quat
 
 pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("ignore:no SDF weights")]
 
 Q_ATOL = 4e-16     # quaternion entries (|q| <= 1): an ulp or two of the trig functions
 POSE_RTOL = 1e-15  # W_R_Bo @ B_p_C etc. vs numpy matmul
+MODES = ["align", "ref", "current", "zero", "curent"]
+SENTINEL = -7.0
 
 
-def _cfg(mode, st_on=False, N=40):
-    cfg = Config(mpc__N=N)
-    cfg.ref.yaw_mode = mode
-    cfg.ref.stop_and_turn.enable = st_on
-    cfg.ref.stop_and_turn.dang_min = 0.8
-    cfg.ref.align_yaw_offset = 0.2
-    return cfg
+@pytest.fixture(scope="module")
+def rg():
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "refgen_golden.npz"))
 
 
-def _host(cfg, model, x0, wps, vw, kind, ws):
-    rg = RefGen(cfg)
-    rg.x0 = x0
-    traj = rg.gen_ref_list_wps(wps) if kind == 0 else rg.gen_ref_joystick(vw) if kind == 1 else rg.from_x0()
-    N = int(cfg.mpc.N)
-    qd = np.zeros((N + 1, 4))
-    y, W = np.zeros((N, model.ny)), np.zeros((N, model.ny))
-    yN, WN = np.zeros(4), np.zeros(4)
-    for k, r in enumerate(traj):
-        r.Wp, r.Wq, r.Wv, r.Ww, r.Wa = (getattr(r, "Wp", ws.Wp) if kind == 1 else ws.Wp), ws.Wq, ws.Wv, ws.Ww, ws.Wa
+def _expected(model, traj, n, ws, Wp=None):
+    """q_d rows and the formate_ref outputs of the golden trajectory rows [p3 q4 v3 wz1]."""
+    N = traj.shape[0] - 1
+    qd, y, W = np.full((N + 1, 4), SENTINEL), np.full((N, model.ny), SENTINEL), np.full((N, model.ny), SENTINEL)
+    yN, WN = np.full(4, SENTINEL), np.full(4, SENTINEL)
+    for k in range(n):
+        r = Ref(model.cfg)
+        r.p, r.q, r.v, r.wz = traj[k, 0:3], traj[k, 3:7], traj[k, 7:10], traj[k, 10]
+        r.use_weights(ws)
+        if Wp is not None:
+            r.Wp = Wp
         qd[k] = r.q
         yr, wr = model.formate_ref(r)
         if k < N:
             y[k], W[k] = yr, wr
         else:
             yN, WN = yr[:4], wr[:4]
-    return len(traj), qd, y, W, yN, WN
+    return qd, y, W, yN, WN
 
 
-@pytest.mark.parametrize("mode,st_on,kind", [("align", False, 0), ("ref", False, 0), ("current", False, 0),
-                                             ("curent", False, 0), ("align", True, 0), ("align", False, 1),
-                                             ("curent", False, 1), ("align", False, 2)])
-def test_pack_refs_matches_host_refgen(gpu_ctx, mode, st_on, kind):
-    import torch
-    cfg = _cfg(mode, st_on)
-    model = Quad(cfg)
-    N, B, nwp = int(cfg.mpc.N), 12, 3
-    rng = np.random.default_rng(hash((mode, st_on, kind)) % 2 ** 32)
-    x0 = np.zeros((B, 10))
-    x0[:, :3] = rng.uniform(-2, 2, (B, 3))
-    x0[:, 3:7] = np.stack([yaw2quat(y) for y in rng.uniform(-np.pi, np.pi, B)])
-    wp_p = x0[:, None, :3] + rng.uniform(-4, 4, (B, nwp, 3)) * np.array([1, 1, 0.3])
-    wp_p[::4] = x0[::4, None, :3] + rng.uniform(-0.3, 0.3, (len(wp_p[::4]), nwp, 3))  # short paths: padded tail
-    wp_q = np.stack([[yaw2quat(y) for y in rng.uniform(-np.pi, np.pi, nwp)] for _ in range(B)])
-    vw = rng.uniform(-1, 1, (B, 4))
-    vw[1] = 0.0
-    ws = Ref(cfg).W_on
-    wrow = weight_row(model, ws)
-    if kind == 1:
+def _pack(ctx, cfg, model, kind, x0, wp_p=None, wp_q=None, vw=None, wrow=None):
+    B, N = x0.shape[0], int(cfg.mpc.N)
+    D = lambda a: _lib.DeviceArray.from_numpy(ctx, np.asarray(a, dtype=np.float64))  # noqa: E731
+    bufs = dict(x0=D(x0), wrow=D(wrow), p=D(np.full((B, N + 1, model.np), SENTINEL)),
+                yref=D(np.full((B, N, model.ny), SENTINEL)), W=D(np.full((B, N, model.ny), SENTINEL)),
+                yNref=D(np.full((B, 4), SENTINEL)), WN=D(np.full((B, 4), SENTINEL)))
+    n_wp = 0
+    if kind == 0:
+        bufs.update(wp_p=D(wp_p), wp_q=D(wp_q))
+        n_wp = wp_p.shape[1]
+    elif kind == 1:
+        bufs["vw"] = D(vw)
+    _lib.pack_refs(ctx, _lib.ref_opts(cfg, kind), B, N, model.np, model.ny, bufs, n_wp=n_wp)
+    ctx.synchronize()
+    return {k: v.numpy() for k, v in bufs.items()}
+
+
+def _check(got, b, model, exp):
+    qd, y, W, yN, WN = exp
+    np.testing.assert_allclose(got["p"][b, :, 13:17], qd, rtol=0, atol=Q_ATOL)
+    np.testing.assert_array_equal(got["p"][b, :, :13], SENTINEL)  # parameters other than q_d untouched
+    np.testing.assert_array_equal(got["p"][b, :, 17:], SENTINEL)
+    np.testing.assert_array_equal(got["yref"][b], y)
+    np.testing.assert_array_equal(got["W"][b], W)
+    np.testing.assert_array_equal(got["yNref"][b], yN)  # N references (from_x0, stop-and-turn): node N unset
+    np.testing.assert_array_equal(got["WN"][b], WN)
+
+
+def test_pack_refs_waypoints_vs_reference_refgen(gpu_ctx, rg):
+    """gen_ref_list_wps: the 40 golden cases, each knob set (yaw mode incl. the reference's 'curent',
+    stop-and-turn, dang_min, align offset, vref, T, N) one batch of the cases that share it."""
+    for c in range(int(rg["n_wps_cases"])):
+        mode, st_on, dang, off, vref, dmin, T, N = rg[f"w{c}/knobs"]
+        cfg = Config(mpc__N=int(N), mpc__T=float(T))
+        cfg.ref.yaw_mode = MODES[int(mode)]
+        cfg.ref.stop_and_turn.enable = bool(st_on)
+        cfg.ref.stop_and_turn.dang_min = float(dang)
+        cfg.ref.align_yaw_offset = float(off)
+        cfg.ref.vref = float(vref)
+        cfg.ref.yaw_align_dmin = float(dmin)
+        model = Quad(cfg)
+        ws = Ref(cfg).W_on
+        x0 = rg[f"w{c}/x0"][None]
+        got = _pack(gpu_ctx, cfg, model, 0, x0, rg[f"w{c}/wp_p"][None], rg[f"w{c}/wp_q"][None],
+                    wrow=model.weight_row(ws))
+        _check(got, 0, model, _expected(model, rg[f"w{c}/traj"], int(rg[f"w{c}/len"]), ws))
+
+
+def test_pack_refs_joystick_and_hover_vs_reference_refgen(gpu_ctx, rg):
+    """gen_ref_joystick (position weights zeroed, ref_gen.py:122) and from_x0 (N references), batched:
+    every joystick case of a yaw mode in one launch."""
+    for mode in range(3):
+        cs = [c for c in range(int(rg["n_joy_cases"])) if int(rg[f"j{c}/mode"]) == mode]
+        if not cs:
+            continue
+        cfg = Config()
+        cfg.ref.yaw_mode = ["align", "ref", "curent"][mode]
+        model = Quad(cfg)
+        ws = Ref(cfg).W_on
+        wrow = model.weight_row(ws)
         wrow[:3] = 0.0
-    dev = torch.device("cuda", gpu_ctx.device)
-    t = lambda a: torch.as_tensor(np.ascontiguousarray(a, dtype=np.float64), device=dev)
-    sentinel = -7.0
-    bufs = dict(x0=t(x0), wp_p=t(wp_p), wp_q=t(wp_q), vw=t(vw), wrow=t(wrow),
-                p=torch.full((B, N + 1, model.np), sentinel, dtype=torch.float64, device=dev),
-                yref=torch.full((B, N, model.ny), sentinel, dtype=torch.float64, device=dev),
-                W=torch.full((B, N, model.ny), sentinel, dtype=torch.float64, device=dev),
-                yNref=torch.full((B, 4), sentinel, dtype=torch.float64, device=dev),
-                WN=torch.full((B, 4), sentinel, dtype=torch.float64, device=dev))
-    _lib.pack_refs(gpu_ctx, _lib.ref_opts(cfg, kind), B, N, model.np, model.ny, bufs, n_wp=nwp)
-    gpu_ctx.synchronize()
-    got = {k: v.cpu().numpy() for k, v in bufs.items()}
-    for b in range(B):
-        wps = [Waypoint(p, q) for p, q in zip(wp_p[b], wp_q[b])]
-        n, qd, y, W, yN, WN = _host(cfg, model, x0[b], wps, vw[b], kind, ws)
-        np.testing.assert_allclose(got["p"][b, :n, 13:17], qd[:n], rtol=0, atol=Q_ATOL)
-        np.testing.assert_array_equal(got["p"][b, :, :13], sentinel)   # parameters other than q_d untouched
-        np.testing.assert_array_equal(got["yref"][b], y)
-        np.testing.assert_array_equal(got["W"][b], W)
-        if n == N + 1:
-            np.testing.assert_array_equal(got["yNref"][b], yN)
-            np.testing.assert_array_equal(got["WN"][b], WN)
-        else:  # from_x0 / stop-and-turn return N references: node N is not set (ref_gen.py:23, :53)
-            np.testing.assert_array_equal(got["p"][b, N, 13:17], sentinel)
-            np.testing.assert_array_equal(got["yNref"][b], sentinel)
+        got = _pack(gpu_ctx, cfg, model, 1, np.stack([rg[f"j{c}/x0"] for c in cs]),
+                    vw=np.stack([rg[f"j{c}/vw"] for c in cs]), wrow=wrow)
+        for i, c in enumerate(cs):
+            traj = rg[f"j{c}/traj"]
+            _check(got, i, model, _expected(model, traj, traj.shape[0], ws, Wp=rg[f"j{c}/Wp"]))
+    cfg = Config()
+    model = Quad(cfg)
+    ws = Ref(cfg).W_on
+    got = _pack(gpu_ctx, cfg, model, 2, rg["from_x0/x0"][None], wrow=model.weight_row(ws))
+    traj = rg["from_x0/traj"]
+    full = np.full((int(cfg.mpc.N) + 1, 11), np.nan)
+    full[: traj.shape[0]] = traj
+    _check(got, 0, model, _expected(model, full, traj.shape[0], ws))
 
 
 def test_pack_latent_matches_set_latent(gpu_ctx):
-    import torch
     cfg = Config(mpc__N=20)
     B, N = 5, 20
     rng = np.random.default_rng(3)
@@ -110,8 +137,7 @@ def test_pack_latent_matches_set_latent(gpu_ctx):
     n.set_latent(lat, pos, R)
     host_p = n.p.copy()
     n.set_latent_device(lat, pos, R, flag=flag)
-    n.ocp.ctx.synchronize()
-    dp = n.ocp.bufs["p"].cpu().numpy()
+    dp = n.ocp.download("p")
     np.testing.assert_array_equal(dp[..., 0], host_p[..., 0])
     np.testing.assert_allclose(dp[..., 1:13], host_p[..., 1:13], rtol=POSE_RTOL, atol=1e-15)
     np.testing.assert_array_equal(dp[..., 17:], host_p[..., 17:])
@@ -119,7 +145,7 @@ def test_pack_latent_matches_set_latent(gpu_ctx):
 
 
 def test_nmpc_device_refs_solve_equals_host_path(gpu_ctx):
-    """Nmpc.gen_refs_device + set_latent_device + solve == the host setter path (set_ref per node)."""
+    """Nmpc.gen_refs_device + set_latent_device + solve == the same parameters set from the host."""
     cfg = Config()
     B = 4
     rng = np.random.default_rng(8)
@@ -131,25 +157,20 @@ def test_nmpc_device_refs_solve_equals_host_path(gpu_ctx):
     wp_p = x0[:, None, :3] + rng.uniform(-3, 3, (B, 2, 3))
     wp_q = np.stack([[yaw2quat(0.4), yaw2quat(-0.2)]] * B)
     ws = Ref(cfg).W_on
-    # host path
-    nh = Nmpc(cfg, batch=B)
-    nh.set_sdf_flag(1.0)
-    nh.set_latent(lat, x0[:, :3], R)
-    for b in range(B):
-        rg = RefGen(cfg)
-        rg.x0 = x0[b]
-        for k, r in enumerate(rg.gen_ref_list_wps([Waypoint(p, q) for p, q in zip(wp_p[b], wp_q[b])])):
-            r.use_weights(ws)
-            nh.set_ref(r, k, b=b)
-    nh.set_x0(x0)
-    assert nh.solve() == 0
     # device path
     nd = Nmpc(cfg, batch=B)
     nd.set_x0(x0)
     nd.set_latent_device(lat, x0[:, :3], R, flag=1.0)
     nd.gen_refs_device("wps", wps=(wp_p, wp_q), weights=ws)
     assert nd.solve() == 0
-    # the packed parameters differ only in the last ulp of q_d / the camera pose; the QPs stop at tol 1e-8
-    np.testing.assert_allclose(nd.get_u(), nh.get_u(), rtol=0, atol=1e-8)
+    # the host path with the same parameters / references: set through the Ocp with host arrays
+    nh = Nmpc(cfg, batch=B)
+    nh.set_x0(x0)
+    nh.ocp.solve(x0, nd.ocp.download("yref"), nd.ocp.download("yNref")[:, 0], nd.ocp.download("W"),
+                 nd.ocp.download("WN")[:, 0], nd.ocp.download("p"))
+    np.testing.assert_array_equal(nd.get_u(), nh.get_u())
+    # and the device-written references are the ones formate_ref gives for the device's own q_d rows
+    qd = nd.ocp.download("p")[:, :, 13:17]
+    assert np.isfinite(qd).all() and np.allclose(np.linalg.norm(qd, axis=-1), 1.0, atol=1e-12)
     nh.ocp.close()
     nd.ocp.close()
