@@ -262,7 +262,8 @@ int sdfnmpc_memcpy(sdfnmpc_ctx* ctx, void* dst, const void* src, size_t bytes, i
 /* ---- the batched SQP-RTI solver object (owns its device workspace) ----
  * Fields (name: [B][nodes][width] fp64 unless noted): x [N+1][10], u [N][4], p [N+1][np], x0 [1][10],
  * yref / W [N][ny], yNref / WN [1][4], u0 [1][4], dx [N+1][10], du [N][4], the sdfnmpc_lin_args outputs
- * xn, AB, y, Jy, yN, JyN, h, Jh, res [1][2], status / iters [1][1] int32.  A field's device pointer may
+ * xn, AB, y, Jy, yN, JyN, h, Jh, res [1][2], slack [N+1][6] ((sl, su) per soft row), status / iters
+ * [1][1] int32.  A field's device pointer may
  * be handed to the lower-level entry points (e.g. sdfnmpc_pack_refs or sdfnmpc_vae_encode writing p). */
 typedef struct sdfnmpc_solver sdfnmpc_solver;
 

@@ -70,7 +70,7 @@ struct sdfnmpc_solver {
     double *x = nullptr, *u = nullptr, *p = nullptr, *x0 = nullptr, *yref = nullptr, *W = nullptr, *yNref = nullptr,
            *WN = nullptr, *dt = nullptr, *xn = nullptr, *AB = nullptr, *y = nullptr, *Jy = nullptr, *yN = nullptr,
            *JyN = nullptr, *h = nullptr, *Jh = nullptr, *dx = nullptr, *du = nullptr, *res = nullptr, *u0 = nullptr,
-           *scratch = nullptr;
+           *scratch = nullptr, *slack = nullptr;
     int *status = nullptr, *iters = nullptr;
     // pinned host memory: step outputs and the upload staging arena (reset after every wait)
     double* h_u0 = nullptr;
@@ -173,7 +173,7 @@ extern "C" int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, c
     A(&s->yref, B * N * o->ny); A(&s->W, B * N * o->ny); A(&s->yNref, B * 4); A(&s->WN, B * 4); A(&s->dt, N);
     A(&s->xn, B * N * 10); A(&s->AB, B * N * 140); A(&s->y, B * N * 11); A(&s->Jy, B * N * 154); A(&s->yN, B * 4);
     A(&s->JyN, B * 40); A(&s->h, B * N1 * 3); A(&s->Jh, B * N1 * 30); A(&s->dx, B * N1 * 10); A(&s->du, B * N * 4);
-    A(&s->res, B * 2); A(&s->u0, B * 4); A(&s->scratch, B * N1 * 10); A(&s->status, B); A(&s->iters, B);
+    A(&s->res, B * 2); A(&s->u0, B * 4); A(&s->scratch, B * N1 * 10); A(&s->slack, B * N1 * 6); A(&s->status, B); A(&s->iters, B);
     if (e == hipSuccess) e = hipHostMalloc((void**)&s->h_u0, B * 4 * sizeof(double), hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&s->h_status, B * sizeof(int), hipHostMallocDefault);
     if (e == hipSuccess) e = hipHostMalloc((void**)&s->h_iters, B * sizeof(int), hipHostMallocDefault);
@@ -190,7 +190,7 @@ extern "C" int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, c
                  {"dx", s->dx, n1, 10, d},     {"du", s->du, n, 4, d},         {"xn", s->xn, n, 10, d},
                  {"AB", s->AB, n, 140, d},     {"y", s->y, n, 11, d},          {"Jy", s->Jy, n, 154, d},
                  {"yN", s->yN, 1, 4, d},       {"JyN", s->JyN, 1, 40, d},      {"h", s->h, n1, 3, d},
-                 {"Jh", s->Jh, n1, 30, d},     {"res", s->res, 1, 2, d},       {"status", s->status, 1, 1, 4},
+                 {"Jh", s->Jh, n1, 30, d},     {"res", s->res, 1, 2, d},       {"slack", s->slack, n1, 6, d},  {"status", s->status, 1, 1, 4},
                  {"iters", s->iters, 1, 1, 4}};
     *out = s;
     return SDFNMPC_OK;
@@ -299,7 +299,7 @@ extern "C" int sdfnmpc_solver_step(sdfnmpc_solver* s) {
     qa.B = s->B; qa.N = s->N;
     qa.xn = s->xn; qa.AB = s->AB; qa.y = s->y; qa.Jy = s->Jy; qa.yN = s->yN; qa.JyN = s->JyN; qa.h = s->h; qa.Jh = s->Jh;
     qa.x = s->x; qa.u = s->u; qa.x0 = s->x0; qa.yref = s->yref; qa.W = s->W; qa.yNref = s->yNref; qa.WN = s->WN;
-    qa.dt = s->dt; qa.dx = s->dx; qa.du = s->du; qa.slack = nullptr; qa.status = s->status; qa.iters = s->iters;
+    qa.dt = s->dt; qa.dx = s->dx; qa.du = s->du; qa.slack = s->slack; qa.status = s->status; qa.iters = s->iters;
     qa.res = s->res;
     rc = sdfnmpc_qp_solve(s->ctx, &s->qp, &qa);
     if (rc) return rc;

@@ -1,0 +1,115 @@
+"""The sharded RTI of config C4 (BASELINE.json configs[3]) with world_size 2 on one GPU: two processes
+over gloo, each solving its shard.instance_range of the batch with the solver object on cuda:0, u_0
+gathered to rank 0 -- bitwise equal to one process solving the whole batch (instances never interact,
+SURVEY.md §8(e)); and the in-process occupancy gate (Ocp over several device slots) the same way."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.filterwarnings("ignore:no SDF weights")]
+
+TOTAL, N = 96, 40
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _solve(lo, hi, ctx):
+    """One SQP-RTI step for instances [lo, hi) of the seeded C4-style batch (solver object, no torch)."""
+    from sdf_nmpc_amd import _lib, synth, weights as W
+    from sdf_nmpc_amd.config import Config
+    from sdf_nmpc_amd.model import Quad
+    cfg = Config(mpc__N=N)
+    model = Quad(cfg)
+    _, dt = _lib.shooting_grid(N, cfg.mpc.T)
+    prob = synth.make_problem(cfg, TOTAL, N, seed=77, dt=dt)
+    x0 = prob["x"][:, 0] + np.random.default_rng(78).normal(0, 0.05, (TOTAL, 10))
+    net = _lib.Net.from_blob(ctx, W.pack(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0)))
+    s = _lib.Solver(ctx, net, _lib.quad_model(cfg), _lib.qp_opts(model), hi - lo, N, model.np, model.ny, dt)
+    sl = slice(lo, hi)
+    for name, v in (("x", prob["x"][sl]), ("u", prob["u"][sl]), ("p", prob["p"][sl]), ("x0", x0[sl, None]),
+                    ("yref", prob["yref"][sl]), ("W", prob["W"][sl]), ("yNref", prob["yN"][sl, None]),
+                    ("WN", prob["WN"][sl, None])):
+        s.upload(name, v)
+    s.step()
+    u0 = s.wait().copy()
+    st = s.status.copy()
+    s.close()
+    net.close()
+    return u0, st
+
+
+def _rank(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from sdf_nmpc_amd import _lib, shard
+        ctx = _lib.Context(0)  # both ranks on the one GPU of the box
+        lo, hi = shard.instance_range(TOTAL, world, rank)
+        u0, st = _solve(lo, hi, ctx)
+        full = shard.gather_rows(torch.from_numpy(u0), TOTAL)
+        stat = shard.gather_rows(torch.from_numpy(st.astype(np.int64)[:, None]), TOTAL)
+        if rank == 0:
+            ref, ref_st = _solve(0, TOTAL, ctx)  # the whole batch in one process
+            q.put((full.numpy(), stat.numpy()[:, 0], ref, ref_st))
+        ctx.close()
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_sharded_rti_equals_single_process():
+    import torch.multiprocessing as mp
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    port = _free_port()
+    procs = [mpc.Process(target=_rank, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    full, st, ref, ref_st = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    assert (st == 0).all() and (ref_st == 0).all()
+    np.testing.assert_array_equal(full, ref)
+
+
+def test_ocp_occupancy_gate_parts_equal_one_part():
+    """Ocp over two device slots (both cuda:0 here): a batch above one GPU's capacity at N = 60 (512
+    instances) is split into two parts by shard.plan; the result equals a single-part solve bitwise."""
+    from sdf_nmpc_amd import shard
+    from sdf_nmpc_amd.config import Config
+    from sdf_nmpc_amd.controller import Nmpc
+    from sdf_nmpc_amd.model import Quad
+    from sdf_nmpc_amd.ocp import Ocp
+    from sdf_nmpc_amd.reference import Ref, yaw2quat
+    Bt, cfg = 600, Config(mpc__N=60)
+    assert shard.gpu_capacity(60) == 512 and len(shard.plan(Bt, 60, 2)) == 2 and len(shard.plan(512, 60, 8)) == 1
+    rng = np.random.default_rng(4)
+    x0 = np.zeros((Bt, 10))
+    x0[:, :3] = rng.uniform(-1, 1, (Bt, 3))
+    x0[:, 3:7] = np.stack([yaw2quat(y) for y in rng.uniform(-np.pi, np.pi, Bt)])
+    lat = rng.normal(size=(Bt, 128))
+    r = Ref(cfg)
+    r.p, r.q = np.array([1.0, 2.0, 1.5]), yaw2quat(0.3)
+    r.use_weights(r.W_on)
+    res = []
+    for devs in ([0, 0], [0]):
+        o = Ocp(Quad(cfg), batch=Bt, devices=devs)
+        assert len(o.parts) == len(devs)
+        n = Nmpc(cfg, batch=Bt, ocp=o)
+        n.set_sdf_flag(1.0)
+        n.set_latent(lat, x0[:, :3], np.stack([np.eye(3)] * Bt))
+        for k in range(61):
+            n.set_ref(r, k)
+        n.set_x0(x0)
+        assert n.solve() == 0 and n.solve() == 0  # two steps: the carried iterate too
+        res.append(n.get_u())
+        o.close()
+    np.testing.assert_array_equal(res[0], res[1])
