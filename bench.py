@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--quiet", action="store_true")
     ap.add_argument("--prep-steps", type=int, default=50, help="timed preparation-only steps (0: skip)")
     ap.add_argument("--no-b1", action="store_true", help="skip the B=1 latency probe (profiling runs)")
+    ap.add_argument("--no-c2", action="store_true", help="skip the CasADi-external (libsdf_l4c.so) call leg")
     ap.add_argument("--config", choices=("c3", "c5"), default="c3",
                     help="c3: the headline 1024 x 40 RTI (default); c5: 4x-wide SDF MLP + in-loop VAE encode, "
                          "N = 60, 4096 instances over 8 GPUs (512 per GPU)")
@@ -221,6 +222,12 @@ def main():
             l1.append((time.perf_counter() - s0) * 1e3)
         lat1 = float(np.median(l1))
 
+    # config C2 as acados drives it: the CasADi external functions of libsdf_l4c.so, called per shooting
+    # node (sdf_l4c, then jac_sdf_l4c on the same input; gen_model.py:39,60), N + 1 nodes per RTI
+    c2 = None
+    if rank == 0 and not args.no_c2:
+        c2 = bench_c2(local, N, W, args.no_cpu_baseline)
+
     # traffic from the committed PMC profile of this same command (profiles/)
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -296,11 +303,74 @@ def main():
                                "frac": lin_gbs / HBM_PEAK_GBS, "bytes_per_launch": lin_b},
         "cpu_baseline": cpu,
         "prep": prep_out,
+        "c2": c2,
     }
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_c2(device, N, W, no_cpu, rtis=30):
+    """Per-call latency of the acados drop-in (include/sdf_l4c.h) through ctypes: every RTI evaluates
+    sdf_l4c and jac_sdf_l4c (1 x 131 Jacobian) at each of the N + 1 nodes, one instance, one latent.
+    Beside it: the same value + 131-gradient from the C oracle's fp32 network on one host thread."""
+    import ctypes as C
+    import tempfile
+    from sdf_nmpc_amd import _lib
+    lib = C.CDLL(_lib.l4c_path())
+    D = 131
+    with tempfile.NamedTemporaryFile(suffix=".sdfw", delete=False) as f:
+        f.write(W.pack(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed=0)))
+        wpath = f.name
+    lib.sdf_l4c_configure.argtypes = [C.c_char_p, C.c_int]
+    if lib.sdf_l4c_configure(wpath.encode(), device) != 0:
+        raise RuntimeError("sdf_l4c_configure failed")
+    os.unlink(wpath)
+    rng = np.random.default_rng(5)
+    lat = rng.normal(size=128)
+    inp = np.empty((N + 1, D))
+    inp[:, :3] = rng.uniform(-2, 2, (N + 1, 3))
+    inp[:, 3:] = lat
+    out = np.empty(N + 1)
+    jac = np.empty((N + 1, D))
+    PD = C.POINTER(C.c_double)
+    a1 = [(PD * 1)(inp[k].ctypes.data_as(PD)) for k in range(N + 1)]
+    a2 = [(PD * 2)(inp[k].ctypes.data_as(PD), out[k:k + 1].ctypes.data_as(PD)) for k in range(N + 1)]
+    r1 = [(PD * 1)(out[k:k + 1].ctypes.data_as(PD)) for k in range(N + 1)]
+    r2 = [(PD * 1)(jac[k].ctypes.data_as(PD)) for k in range(N + 1)]
+    f, jf = lib.sdf_l4c, lib.jac_sdf_l4c
+
+    def rti():
+        for k in range(N + 1):
+            if f(a1[k], r1[k], None, None, 0) or jf(a2[k], r2[k], None, None, 0):
+                raise RuntimeError("sdf_l4c call failed")
+    for _ in range(3):
+        rti()
+    ts = []
+    for _ in range(rtis):
+        t0 = time.perf_counter()
+        rti()
+        ts.append(time.perf_counter() - t0)
+    per_rti = float(np.median(ts))
+    res = {"us_per_node": per_rti / (N + 1) * 1e6, "ms_per_rti": per_rti * 1e3, "nodes_per_rti": N + 1,
+           "calls": "sdf_l4c + jac_sdf_l4c per node (ctypes, fp64 in/out, value and 1x131 Jacobian)"}
+    if not no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O
+        O.build()
+        onet = O.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed=0))
+        onet.f32(inp[:1])
+        t0 = time.perf_counter()
+        reps = 200
+        for k in range(reps):
+            onet.f32(inp[k % (N + 1):k % (N + 1) + 1], nthreads=1)
+        cpu_us = (time.perf_counter() - t0) / reps * 1e6
+        res["cpu_baseline"] = {"us_per_node": cpu_us, "cores": 1, "kind": "port",
+                               "sample": f"{reps} single-row fp32 value + 131-gradient evaluations, C oracle "
+                                         "(oracle/sdf_net.inc) on one host thread, as L4CasADi runs torch with "
+                                         "set_num_threads(1) (gen_model.py:27)"}
+    return res
 
 
 def main_c5(args):

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -77,7 +78,13 @@ struct sdfnmpc_ctx {
     int tile_rows = 32;
     bool timing = false;
     DevBuf c13, sdf4, lat, out4, glat, qpw, qpst, wws;
-    std::vector<float> h_in;  // host staging for sdf_eval_host
+    // host-pointer path (sdf_eval_host, the CasADi external): pinned staging, its own hoist buffer and
+    // the latents it was computed for (consecutive acados calls share one latent: the hoist is reused)
+    float* h_pin = nullptr;
+    size_t h_pin_bytes = 0;
+    DevBuf hin, hout, hc13;
+    std::vector<float> h_lat;
+    uint64_t h_net = 0;  // uid of the network the cached hoist belongs to
     std::map<std::string, KStat> stats;
     std::mutex mu;  // serialises the host-pointer path (CasADi externals may be called concurrently)
 };
@@ -165,6 +172,7 @@ extern "C" void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx) {
         (void)hipStreamSynchronize(ctx->aux);
         (void)hipStreamDestroy(ctx->aux);
     }
+    if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     if (ctx->own_stream) (void)hipStreamDestroy(ctx->stream);
@@ -441,11 +449,19 @@ struct sdfnmpc_net {
     HostNet host;
     void* dmem = nullptr;
     SdfArgs args{};  // weight pointers filled; per-call fields left zero
+    SdfRowArgs row{};  // the single-row path's weight pointers (deployed architecture only)
     const float4* WzT = nullptr;
     const float* bias13 = nullptr;
     uint64_t fingerprint = 0;
     bool wide = false;
     WideDev wd;
+    // process-unique id: caches keyed on a network (the host path's hoist) never confuse a freed
+    // network with a new one allocated at the same address
+    uint64_t uid = next_uid();
+    static uint64_t next_uid() {
+        static std::atomic<uint64_t> n{1};
+        return n++;
+    }
 };
 
 static void emb_table(const HostNet& h, std::vector<float>& blob) {
@@ -570,6 +586,27 @@ static int upload_net(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     while (blob.size() % 4) blob.push_back(0.0f);
     mark();
     emb_table(h, blob);
+    // plain torch-layout copies for the single-row latency path (sdf_row.hip)
+    auto plain = [&](const std::vector<float>& v) {
+        mark();
+        blob.insert(blob.end(), v.begin(), v.end());
+        while (blob.size() % 4) blob.push_back(0.0f);
+    };
+    auto padded = [&](const std::vector<float>& v, int J, int K) {  // rows padded to a multiple of 4 floats
+        const int K4 = (K + 3) / 4 * 4;
+        std::vector<float> t((size_t)J * K4, 0.0f);
+        for (int j = 0; j < J; ++j)
+            for (int k = 0; k < K; ++k) t[(size_t)j * K4 + k] = v[(size_t)j * K + k];
+        plain(t);
+    };
+    padded(h.W1, N1, c1); padded(h.W2, N2, N1); padded(h.W3, N3, c3); padded(h.W4, N4, N3);
+    auto transposed = [&](const std::vector<float>& v, int J, int K) {
+        std::vector<float> t((size_t)J * K);
+        for (int j = 0; j < J; ++j)
+            for (int k = 0; k < K; ++k) t[(size_t)k * J + j] = v[(size_t)j * K + k];
+        plain(t);
+    };
+    transposed(h.W1, N1, c1); transposed(h.W2, N2, N1); transposed(h.W3, N3, c3); transposed(h.W4, N4, N3);
     for (size_t o : off)
         if (o % 4) return fail(SDFNMPC_E_FORMAT, "internal: misaligned packed operand");
 
@@ -610,6 +647,23 @@ static int upload_net(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     a.emb_tab = (const float4*)(d + off[i++]);
     a.b5 = h.b5[0];
     a.w0 = h.w0;
+    SdfRowArgs& ra = net->row;
+    ra.W1 = d + off[i++];
+    ra.W2 = d + off[i++];
+    ra.W3 = d + off[i++];
+    ra.W4 = d + off[i++];
+    ra.W1T = d + off[i++];
+    ra.W2T = d + off[i++];
+    ra.W3T = d + off[i++];
+    ra.W4T = d + off[i++];
+    ra.b1 = net->bias13;
+    ra.b3 = net->bias13 + N1;
+    ra.b2 = a.b2;
+    ra.b4 = a.b4;
+    ra.w5 = a.w5;
+    ra.b5 = a.b5;
+    ra.w0 = a.w0;
+    ra.emb_tab = a.emb_tab;
     const uint64_t fp = net_fingerprint(h);
     net->fingerprint = fp;
     net->host = std::move(h);
@@ -779,31 +833,82 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
     std::lock_guard<std::mutex> lk(ctx->mu);
     ScopedDevice sd(ctx->device);
     const int D = 3 + L;
-    // host staging: [rows][4] pos | [rows][L] latent   (double -> float as L4CasADi does)
-    ctx->h_in.assign((size_t)rows * (4 + L), 0.0f);
-    float* hp = ctx->h_in.data();
+    // pinned staging: in [rows][4] pos | [rows][L] latent, out [rows][4] (df, d/dpos) | [rows][L] d/dlatent
+    // (double -> float as L4CasADi does); one copy each way, one synchronisation
+    const size_t nin = (size_t)rows * (4 + L), bytes = 2 * nin * sizeof(float);
+    if (bytes > ctx->h_pin_bytes) {
+        if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
+        ctx->h_pin = nullptr;
+        ctx->h_pin_bytes = 0;
+        HIPCHK(hipHostMalloc((void**)&ctx->h_pin, bytes, hipHostMallocDefault));
+        ctx->h_pin_bytes = bytes;
+    }
+    float* hp = ctx->h_pin;
     float* hl = hp + (size_t)rows * 4;
+    float* ho = ctx->h_pin + nin;
     for (int r = 0; r < rows; ++r) {
         for (int c = 0; c < 3; ++c) hp[r * 4 + c] = (float)in[(size_t)r * D + c];
+        hp[r * 4 + 3] = 0.0f;
         for (int k = 0; k < L; ++k) hl[(size_t)r * L + k] = (float)in[(size_t)r * D + 3 + k];
     }
-    HIPCHK(ctx->lat.ensure(ctx->h_in.size() * sizeof(float)));
-    HIPCHK(ctx->out4.ensure((size_t)rows * 4 * sizeof(float)));
-    if (grad) HIPCHK(ctx->glat.ensure((size_t)rows * L * sizeof(float)));
-    HIPCHK(hipMemcpyAsync(ctx->lat.p, hp, ctx->h_in.size() * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-    float* dpos = (float*)ctx->lat.p;
-    float* dlat = dpos + (size_t)rows * 4;
-    int rc = sdfnmpc_sdf_eval(ctx, net, rows, dpos, dlat, 1, (float*)ctx->out4.p, grad ? (float*)ctx->glat.p : nullptr);
-    if (rc) return rc;
-    std::vector<float> o((size_t)rows * 4), gl(grad ? (size_t)rows * L : 0);
-    HIPCHK(hipMemcpyAsync(o.data(), ctx->out4.p, o.size() * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    if (grad) HIPCHK(hipMemcpyAsync(gl.data(), ctx->glat.p, gl.size() * sizeof(float), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    const bool use_row = !net->wide && rows <= SDF_ROW_MAX;
+    if (use_row) {  // the latency path: one launch, no hoist (sdf_row.hip)
+        HIPCHK(ctx->hin.ensure(nin * sizeof(float)));
+        HIPCHK(ctx->hout.ensure(nin * sizeof(float)));
+        float* dpos = (float*)ctx->hin.p;
+        float* dout = (float*)ctx->hout.p;
+        HIPCHK(hipMemcpyAsync(dpos, hp, nin * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
+        SdfRowArgs ra = net->row;
+        ra.pos = (const float4*)dpos;
+        ra.latent = dpos + (size_t)rows * 4;
+        ra.out = (float4*)dout;
+        ra.grad_latent = grad ? dout + (size_t)rows * 4 : nullptr;
+        ra.rows = rows;
+        HIPCHK(timed(ctx, "sdf_row", [&] { return launch_sdf_row(ra, ctx->stream); }));
+        HIPCHK(hipMemcpyAsync(ho, dout, (grad ? nin : (size_t)rows * 4) * sizeof(float), hipMemcpyDeviceToHost,
+                              ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    } else {
+        HIPCHK(ctx->hin.ensure(nin * sizeof(float)));
+        HIPCHK(ctx->hout.ensure(nin * sizeof(float)));
+        float* dpos = (float*)ctx->hin.p;
+        float* dlat = dpos + (size_t)rows * 4;
+        float* dout = (float*)ctx->hout.p;
+        float* dglat = dout + (size_t)rows * 4;
+        // the latent hoist depends on the latents only: reuse it while they repeat (the same image's
+        // latent at every shooting node of an RTI); the positions go up every call
+        const bool same_lat = !net->wide && ctx->h_net == net->uid && ctx->h_lat.size() == (size_t)rows * L &&
+                              !memcmp(ctx->h_lat.data(), hl, (size_t)rows * L * sizeof(float));
+        HIPCHK(hipMemcpyAsync(dpos, hp, (same_lat ? (size_t)rows * 4 : nin) * sizeof(float), hipMemcpyHostToDevice,
+                              ctx->stream));
+        int rc = SDFNMPC_OK;
+        if (net->wide) {
+            rc = sdfnmpc_sdf_eval(ctx, net, rows, dpos, dlat, 1, dout, grad ? dglat : nullptr);
+        } else {
+            if (!same_lat) {
+                HIPCHK(ctx->hc13.ensure((size_t)rows * C13_STRIDE * sizeof(float)));
+                rc = run_hoist<float>(ctx, net, dlat, L, rows, (float*)ctx->hc13.p);
+                if (rc) return rc;
+                ctx->h_lat.assign(hl, hl + (size_t)rows * L);
+                ctx->h_net = net->uid;
+            }
+            rc = run_sdf(ctx, net, rows, (const float4*)dpos, (const float*)ctx->hc13.p, 1, (float4*)dout,
+                         grad ? dglat : nullptr, grad ? 32 : ctx->tile_rows);
+        }
+        if (rc) {
+            ctx->h_net = 0;
+            return rc;
+        }
+        HIPCHK(hipMemcpyAsync(ho, dout, (grad ? nin : (size_t)rows * 4) * sizeof(float), hipMemcpyDeviceToHost,
+                              ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
+    const float* go = ho + (size_t)rows * 4;
     for (int r = 0; r < rows; ++r) {
-        df[r] = o[(size_t)r * 4];
+        df[r] = ho[(size_t)r * 4];
         if (grad) {
-            for (int c = 0; c < 3; ++c) grad[(size_t)r * D + c] = o[(size_t)r * 4 + 1 + c];
-            for (int k = 0; k < L; ++k) grad[(size_t)r * D + 3 + k] = gl[(size_t)r * L + k];
+            for (int c = 0; c < 3; ++c) grad[(size_t)r * D + c] = ho[(size_t)r * 4 + 1 + c];
+            for (int k = 0; k < L; ++k) grad[(size_t)r * D + 3 + k] = go[(size_t)r * L + k];
         }
     }
     return SDFNMPC_OK;

@@ -6,6 +6,7 @@
 // served from a per-thread cache keyed on the exact input bits.
 #include <dlfcn.h>
 
+#include <atomic>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -21,11 +22,15 @@ constexpr int D = 131;  // 3 + latent 128
 std::mutex g_mu;
 sdfnmpc_ctx* g_ctx = nullptr;
 sdfnmpc_net* g_net = nullptr;
-std::string g_err;
+std::string g_err;                    // guarded by g_mu
+std::atomic<unsigned long long> g_gen{1};  // bumped by every sdf_l4c_configure: invalidates all caches
 
+// per-thread cache of the last input (acados calls sdf_l4c then jac_sdf_l4c on the same input); an
+// entry is valid only for the configuration generation it was computed under
 thread_local double t_in[D];
 thread_local double t_df = 0.0, t_grad[D];
-thread_local bool t_valid = false;
+thread_local unsigned long long t_gen = 0;
+thread_local std::string t_err;
 
 std::string lib_dir() {
     Dl_info info;
@@ -68,16 +73,17 @@ int init_locked(const char* path, int device) {
 // value + gradient for one input, cached per thread
 int eval(const double* in) {
     if (!in) return 1;
-    if (t_valid && memcmp(in, t_in, sizeof t_in) == 0) return 0;
+    if (t_gen == g_gen.load() && memcmp(in, t_in, sizeof t_in) == 0) return 0;
     std::lock_guard<std::mutex> lk(g_mu);
     if (init_locked(nullptr, -1)) return 1;
+    const unsigned long long gen = g_gen.load();
     if (sdfnmpc_sdf_eval_host(g_ctx, g_net, 1, in, &t_df, t_grad) != SDFNMPC_OK) {
         g_err = std::string("sdf_l4c: ") + sdfnmpc_last_error();
-        t_valid = false;
+        t_gen = 0;
         return 1;
     }
     memcpy(t_in, in, sizeof t_in);
-    t_valid = true;
+    t_gen = gen;
     return 0;
 }
 
@@ -104,6 +110,7 @@ extern "C" {
 
 int sdf_l4c_configure(const char* weights_path, int device) {
     std::lock_guard<std::mutex> lk(g_mu);
+    g_gen++;  // every thread's cached value / gradient belongs to the previous network
     if (g_net) {
         sdfnmpc_net_free(g_net);
         g_net = nullptr;
@@ -112,10 +119,13 @@ int sdf_l4c_configure(const char* weights_path, int device) {
         sdfnmpc_ctx_destroy(g_ctx);
         g_ctx = nullptr;
     }
-    t_valid = false;
     return init_locked(weights_path, device) ? 1 : 0;
 }
-const char* sdf_l4c_last_error(void) { return g_err.c_str(); }
+const char* sdf_l4c_last_error(void) {  // a per-thread copy taken under the lock
+    std::lock_guard<std::mutex> lk(g_mu);
+    t_err = g_err;
+    return t_err.c_str();
+}
 
 // ---- f
 int sdf_l4c(const double** arg, double** res, long long*, double*, int) {

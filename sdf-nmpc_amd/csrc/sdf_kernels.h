@@ -59,6 +59,24 @@ struct SdfArgs {
     int rows_per_inst;      // row r uses c13[r / rows_per_inst]
 };
 
+// single-row latency path (sdf_row.hip): plain row-major torch-layout weights, value + full input gradient
+struct SdfRowArgs {
+    const float *W1, *b1;   // [N1][E + L], [N1]     (rows padded to a multiple of 4 floats)
+    const float *W2, *b2;   // [N2][N1]
+    const float *W3, *b3;   // [N3][N2 + E + L]
+    const float *W4, *b4;   // [N4][N3]
+    const float *W1T, *W2T, *W3T, *W4T;  // the same, transposed ([K][J]): the forward's coalesced operand
+    const float* w5;        // [N4]
+    float b5, w0;
+    const float4* emb_tab;  // [NE]
+    const float4* pos;      // [rows] (Co_p_B, pad)
+    const float* latent;    // [rows][L]
+    float4* out;            // [rows] (df, d df / d pos)
+    float* grad_latent;     // [rows][L] or NULL
+    int rows;
+};
+constexpr int SDF_ROW_MAX = 16;  // host-path calls with at most this many rows use sdf_row_kernel
+
 template <typename T>
 struct HoistArgs {
     const T* latent;     // latent of instance i at latent[i * stride + k]
@@ -112,6 +130,7 @@ hipError_t launch_wide_final(const WideSdfArgs& a, hipStream_t s);
 size_t sdf_lds_bytes(int M);
 hipError_t sdf_set_lds_limits();
 hipError_t launch_sdf_mlp(const SdfArgs& a, int M, bool latent_grad, hipStream_t s);
+hipError_t launch_sdf_row(const SdfRowArgs& a, hipStream_t s);
 template <typename T>
 hipError_t launch_hoist(const HoistArgs<T>& a, hipStream_t s);
 

@@ -1,0 +1,224 @@
+// NeuralDF value + full 1x131 input gradient for a handful of rows: the latency path of the CasADi
+// external (config C2: acados calls sdf_l4c / jac_sdf_l4c one shooting node at a time, gen_model.py:
+// 39,60).  The batched kernel (sdf_mlp.hip) tiles 32 rows per workgroup and hoists the latent per
+// instance -- at one row it is a single workgroup walking ~1.5 MB of weights through a 3-deep register
+// ring, latency-bound at ~60 us.  Here one 512-thread workgroup per row keeps each layer's weights in
+// flight at once:
+//   forward  a = W in + b   threads own outputs and K-slices of the transposed weights W^T: coalesced
+//                           loads, no cross-lane reduction;  h = sin(w0 a), cos(w0 a) kept in LDS
+//   backward d_in = W^T d   waves own input rows j, lanes own columns k and accumulate over j, one LDS
+//                           reduction over the 8 waves -- W read row-major (coalesced across lanes)
+// At one row the kernel is a chain of 8 dependent layers, each a few L2 / MALL round trips: ~23 us on
+// MI355X, against ~60 us for the batched kernel at one row.
+// Reference semantics: PositionEmbedding (embeddings.py:106-111), NeuralDF.forward (neural_df.py:
+// 91-103), Sine (activation.py:12-13) and the reverse-mode input gradient L4CasADi's jac_sdf_l4c
+// returns; the arithmetic of the embedding and its derivative is sdf_mlp.hip's / sdf_wide.hip's.
+#include <hip/hip_runtime.h>
+
+#include "sdf_kernels.h"
+#include "sincos.h"
+
+namespace sdfn {
+
+namespace {
+
+constexpr int RW = 8;             // waves per row workgroup
+constexpr int C1 = E + L;         // W1 row length (211)
+constexpr int C3 = N2 + E + L;    // W3 row length (467)
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// out[j] = bias[j] + W[j][:K] . in  for j < J, from the transposed copy WT [K][J] (column j of WT is
+// row j of W): thread t owns output j = t % J over the K-slice t / J, so every weight load is one
+// coalesced 256-B wave access and no cross-lane reduction is needed; the S = 512 / J partial sums of
+// an output meet in LDS (`part`)
+template <int J, int K>
+__device__ __forceinline__ void fwd(const float* __restrict__ WT, const float* __restrict__ bias, const float* in,
+                                    float* part, float* out) {
+    constexpr int S = 64 * RW / J, KS = (K + S - 1) / S;
+    static_assert(S >= 1 && S * J == 64 * RW, "J must divide the workgroup");
+    const int t = threadIdx.x, j = t % J, s = t / J;
+    const int k0 = s * KS, k1 = (k0 + KS < K) ? k0 + KS : K;
+    float a0 = 0.0f, a1 = 0.0f;
+    int k = k0;
+#pragma unroll 8
+    for (; k + 1 < k1; k += 2) {
+        a0 = fmaf(WT[(size_t)k * J + j], in[k], a0);
+        a1 = fmaf(WT[(size_t)(k + 1) * J + j], in[k + 1], a1);
+    }
+    if (k < k1) a0 = fmaf(WT[(size_t)k * J + j], in[k], a0);
+    part[s * J + j] = a0 + a1;
+    __syncthreads();
+    if (t < J) {
+        float v = 0.0f;
+#pragma unroll
+        for (int q = 0; q < S; ++q) v += part[q * J + t];
+        out[t] = v + bias[t];
+    }
+}
+
+// out[k] = sum_j W[j][k] d[j]  for k < K (W row-major [J][K4], rows padded to K4 = 4 ceil(K / 4)); waves
+// own rows j (4 at a time), lanes own columns k and accumulate over j; partial sums reduced over the
+// waves through `part` [RW][K]
+template <int J, int K>
+__device__ __forceinline__ void bwd(const float* __restrict__ W, const float* d, float* part, float* out, int wave,
+                                    int lane) {
+    constexpr int T = (K + 63) / 64, K4 = (K + 3) / 4 * 4;
+    float acc[T];
+#pragma unroll
+    for (int t = 0; t < T; ++t) acc[t] = 0.0f;
+    for (int j0 = 4 * wave; j0 < J; j0 += 4 * RW) {
+        float w[4][T], dj[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            dj[r] = (j0 + r < J) ? d[j0 + r] : 0.0f;
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const int k = lane + 64 * t;
+                w[r][t] = (j0 + r < J && k < K) ? W[(size_t)(j0 + r) * K4 + k] : 0.0f;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+#pragma unroll
+            for (int t = 0; t < T; ++t) acc[t] = fmaf(w[r][t], dj[r], acc[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < T; ++t)
+        if (lane + 64 * t < K) part[wave * K + lane + 64 * t] = acc[t];
+    __syncthreads();
+    for (int k = threadIdx.x; k < K; k += 64 * RW) {
+        float s = 0.0f;
+#pragma unroll
+        for (int w = 0; w < RW; ++w) s += part[w * K + k];
+        out[k] = s;
+    }
+    __syncthreads();
+}
+
+}  // namespace
+
+__global__ __launch_bounds__(64 * RW) void sdf_row_kernel(SdfRowArgs A) {
+    const int r = blockIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    __shared__ float in1[C1], in3[C3], gm[NE];             // [e | z], [h2 | e | z], d e / d xb
+    __shared__ float a1[N1], c1[N1], a2[N2], c2[N2], a3[N3], c3[N3], a4[N4], c4[N4], h3[N3], h4[N4];
+    __shared__ float g1[C1], g3[C3];
+    __shared__ __align__(16) float part[RW * (C3 + 1)];
+    __shared__ float red[4];
+    const float w0 = A.w0;
+    const float4 p = A.pos[r];
+    // ---- embedding (e = [x, sin(xb), sin(xb + pi/2)], sdf_wide.hip's arithmetic) and the latent
+    for (int m = threadIdx.x; m < NE; m += 64 * RW) {
+        float e = 0.0f, g = 0.0f;
+        if (m < 3) {
+            e = m == 0 ? p.x : (m == 1 ? p.y : p.z);
+            g = 1.0f;
+        } else if (m < E) {
+            const float4 t = A.emb_tab[m];
+            float xb = p.x * t.x + p.y * t.y + p.z * t.z;
+            if (m >= 3 + EMB_NB) xb = xb + 1.57079637050628662109375f;
+            sdfn_sincosf(xb, &e, &g);
+        }
+        gm[m] = g;
+        if (m < E) {
+            in1[m] = e;
+            in3[N2 + m] = e;
+        }
+    }
+    for (int k = threadIdx.x; k < L; k += 64 * RW) {
+        const float z = A.latent[(size_t)r * L + k];
+        in1[E + k] = z;
+        in3[N2 + E + k] = z;
+    }
+    __syncthreads();
+    // ---- forward
+    fwd<N1, C1>(A.W1T, A.b1, in1, part, a1);
+    __syncthreads();
+    for (int j = threadIdx.x; j < N1; j += 64 * RW) {
+        float s, c;
+        sdfn_sincosf(w0 * a1[j], &s, &c);
+        a1[j] = s;  // h1
+        c1[j] = c;
+    }
+    __syncthreads();
+    fwd<N2, N1>(A.W2T, A.b2, a1, part, a2);
+    __syncthreads();
+    for (int j = threadIdx.x; j < N2; j += 64 * RW) {
+        float s, c;
+        sdfn_sincosf(w0 * a2[j], &s, &c);
+        in3[j] = s;  // h2
+        c2[j] = c;
+    }
+    __syncthreads();
+    fwd<N3, C3>(A.W3T, A.b3, in3, part, a3);
+    __syncthreads();
+    for (int j = threadIdx.x; j < N3; j += 64 * RW) {
+        float s, c;
+        sdfn_sincosf(w0 * a3[j], &s, &c);
+        h3[j] = s;
+        c3[j] = c;
+    }
+    __syncthreads();
+    fwd<N4, N3>(A.W4T, A.b4, h3, part, a4);
+    __syncthreads();
+    for (int j = threadIdx.x; j < N4; j += 64 * RW) {
+        float s, c;
+        sdfn_sincosf(w0 * a4[j], &s, &c);
+        h4[j] = s;
+        c4[j] = c;
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const float v = wave_sum(lane < N4 ? A.w5[lane] * h4[lane] : 0.0f);
+        if (lane == 0) red[0] = v + A.b5;
+    }
+    // ---- backward: delta_a = (delta_h * cos(w0 a)) * w0 (torch SinBackward then MulBackward)
+    for (int j = threadIdx.x; j < N4; j += 64 * RW) a4[j] = (A.w5[j] * c4[j]) * w0;
+    __syncthreads();
+    bwd<N4, N3>(A.W4, a4, part, h3, wave, lane);             // d h3
+    for (int j = threadIdx.x; j < N3; j += 64 * RW) a3[j] = (h3[j] * c3[j]) * w0;
+    __syncthreads();
+    bwd<N3, C3>(A.W3, a3, part, g3, wave, lane);             // [d h2 | d e | d z]
+    for (int j = threadIdx.x; j < N2; j += 64 * RW) a2[j] = (g3[j] * c2[j]) * w0;
+    __syncthreads();
+    bwd<N2, N1>(A.W2, a2, part, a1, wave, lane);             // d h1
+    for (int j = threadIdx.x; j < N1; j += 64 * RW) a1[j] = (a1[j] * c1[j]) * w0;
+    __syncthreads();
+    bwd<N1, C1>(A.W1, a1, part, g1, wave, lane);             // [d e | d z]
+    // ---- outputs: df, d df / d pos (through the embedding), d df / d latent
+    if (A.grad_latent)
+        for (int k = threadIdx.x; k < L; k += 64 * RW) A.grad_latent[(size_t)r * L + k] = g3[N2 + E + k] + g1[E + k];
+    if (wave == 0) {
+        float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f;
+        for (int m = lane; m < E; m += 64) {
+            const float u = (g3[N2 + m] + g1[m]) * gm[m];
+            if (m < 3) {
+                s0 += m == 0 ? u : 0.0f;
+                s1 += m == 1 ? u : 0.0f;
+                s2 += m == 2 ? u : 0.0f;
+            } else {
+                const float4 t = A.emb_tab[m];
+                s0 = fmaf(u, t.x, s0);
+                s1 = fmaf(u, t.y, s1);
+                s2 = fmaf(u, t.z, s2);
+            }
+        }
+        s0 = wave_sum(s0);
+        s1 = wave_sum(s1);
+        s2 = wave_sum(s2);
+        if (lane == 0) A.out[r] = make_float4(red[0], s0, s1, s2);
+    }
+}
+
+hipError_t launch_sdf_row(const SdfRowArgs& a, hipStream_t s) {
+    if (a.rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(sdf_row_kernel, dim3((unsigned)a.rows), dim3(64 * RW), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace sdfn

@@ -137,3 +137,58 @@ def test_l4c_shim_casadi_calls(golden, tmp_path):
         np.testing.assert_array_equal(adj, 0.5 * jac)
     # bad weights path -> non-zero status, never an exception across the ABI
     assert lib.sdf_l4c_configure(str(tmp_path / "missing.sdfw").encode(), 0) != 0
+
+
+def test_host_path_hoist_reuse_across_calls(golden, gpu_ctx, oracle_lib):
+    """sdfnmpc_sdf_eval_host keeps the latent hoist while consecutive calls repeat the latent (acados:
+    one latent for all N + 1 nodes) and recomputes it when the latent or the network changes."""
+    g = golden["sdf"]
+    net0, net1 = _lib.Net.siren(gpu_ctx, 0), _lib.Net.siren(gpu_ctx, 1)
+    onet = {0: oracle_lib.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0)),
+            1: oracle_lib.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 1))}
+    rng = np.random.default_rng(2)
+    lat_a, lat_b = g["input"][0, 3:], g["input"][1, 3:]
+    seq = [(0, lat_a), (0, lat_a), (0, lat_a), (0, lat_b), (0, lat_b), (1, lat_b), (0, lat_b), (0, lat_a)]
+    for s, lat in seq:
+        x = np.concatenate([rng.uniform(-2, 2, 3), lat])[None].astype(np.float64)
+        df, gr = (net0 if s == 0 else net1).eval_host(x)
+        df64, _, g64 = onet[s].f64(x)
+        assert sdf_df_ok(df, df64), (s, sdf_df_err(df, df64))
+        assert np.abs(gr - g64).max() <= 1e-5 * max(1.0, np.abs(g64).max())
+
+
+def test_l4c_shim_reconfigure_invalidates_every_thread(tmp_path):
+    """sdf_l4c_configure must invalidate the cached value / gradient of every thread, not only
+    the caller's (acados with OpenMP calls the externals from several threads)."""
+    import threading
+    lib = ctypes.CDLL(_lib.L4C_PATH)
+    lib.sdf_l4c_configure.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    D = ctypes.POINTER(ctypes.c_double)
+    lib.sdf_l4c.argtypes = [ctypes.POINTER(D), ctypes.POINTER(D), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    paths = []
+    for seed in (0, 1):
+        p = tmp_path / f"w{seed}.sdfw"
+        W.save(str(p), W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed))
+        paths.append(str(p).encode())
+    x = np.concatenate([[0.3, -0.2, 1.1], np.random.default_rng(0).normal(size=128)])
+    results, go, done = {}, threading.Event(), threading.Event()
+
+    def worker():
+        out = np.zeros(1)
+        args = (D * 1)(x.ctypes.data_as(D))
+        lib.sdf_l4c(args, (D * 1)(out.ctypes.data_as(D)), None, None, 0)
+        results["before"] = out[0]
+        done.set()
+        go.wait(60)
+        lib.sdf_l4c(args, (D * 1)(out.ctypes.data_as(D)), None, None, 0)  # same input, new weights
+        results["after"] = out[0]
+    assert lib.sdf_l4c_configure(paths[0], 0) == 0
+    t = threading.Thread(target=worker)
+    t.start()
+    assert done.wait(60)
+    assert lib.sdf_l4c_configure(paths[1], 0) == 0  # from another thread
+    go.set()
+    t.join(60)
+    out = np.zeros(1)
+    lib.sdf_l4c((D * 1)(x.ctypes.data_as(D)), (D * 1)(out.ctypes.data_as(D)), None, None, 0)
+    assert results["after"] == out[0] and results["after"] != results["before"]
