@@ -189,6 +189,54 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubl
     return s;
 }
 
+// Lane constants of the backward factor stage: window indices (R_Z: a zero slot) and record-store byte
+// offsets (F_J: a junk slot).  Built once per factor sweep; every field goes through opaque(), so the
+// compiler keeps them in registers instead of rematerialising the index arithmetic (with its
+// divergent branches) at every stage.
+struct FConst {
+    int g, c, og01, og2, cgi, gj, ab01, ab2, bmi, hxu_i, huu_i, v0_i;
+    int h_i[4];
+    unsigned spc[3], sab[3], sk_;
+};
+
+__device__ __forceinline__ FConst fconst(int lane) {
+    FConst f;
+    const int g = lane >> 4, c = lane & 15;
+    f.g = g;
+    f.c = c;
+    // G = [A B c] (column 14 is c at R_C + k): G[4 st + g][c] at og01 + 4 st (st = 0, 1), og2
+    f.og01 = opaque(c < 15 ? c * 10 + g : R_Z);
+    f.og2 = opaque((c < 15 && g < 2) ? c * 10 + g + 8 : R_Z);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
+        f.h_i[r] = opaque((a < 14 && c < 14) ? R_H + tri14(lo, hi) : (a < 14 && c == 14) ? R_G + a : R_Z);
+    }
+    // fold operands: A = C[c][g] (g < 3), B = w_g C[c][g] (c < 10) | gamma_g (c = 14)
+    f.cgi = opaque((c < NX && g < NS) ? R_CT + g * 10 + c : R_Z);
+    f.gj = g < NS ? g : 0;
+    // closed loop: [A | c][a][c] at ab01 + 4 r (r = 0, 1), ab2; A operand B[a = c][g] at bmi
+    const bool xcol = c < NX || c == 14;  // columns of [P | p], [A | c], [K | k_ff]
+    const int xo = c < NX ? c : 10;       // their column in the 11-wide factor-record rows
+    f.ab01 = opaque(xcol ? (c < NX ? c : 14) * 10 + g : R_Z);
+    f.ab2 = opaque((xcol && g < 2) ? (c < NX ? c : 14) * 10 + g + 8 : R_Z);
+    f.bmi = opaque(c < NX ? (NX + g) * 10 + c : R_Z);
+    // factor-record store offsets in bytes (F_J: junk)
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const int a = g + 4 * r;
+        f.spc[r] = (unsigned)opaque(8 * ((c == 14 && a < NX) ? F_PC + a : F_J));
+        f.sab[r] = (unsigned)opaque(8 * ((xcol && a < NX) ? F_AB + a * 11 + xo : F_J));
+    }
+    f.sk_ = (unsigned)opaque(8 * (xcol ? F_K + g * 11 + xo : F_J));
+    // Joseph form operands (window indices; R_Z reads 0):  A operand H^_xu[c][g] (c < 10);
+    // A operand R^0[c][g] = H_uu[c][g] (+ box diagonal, c < 4); C init H^[10 + g][c] of V's row g
+    f.hxu_i = opaque(c < NX ? R_H + tri14(c, NX + g) : R_Z);
+    f.huu_i = opaque(c < NU ? R_H + tri14(NX + (c < g ? c : g), NX + (c < g ? g : c)) : R_Z);
+    f.v0_i = opaque(c < 14 ? R_H + tri14(c < NX + g ? c : NX + g, c < NX + g ? NX + g : c) : c == 14 ? R_G + NX + g : R_Z);
+    return f;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------------------------------------------
@@ -438,32 +486,23 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     auto fs_at = [&](int k, int e) -> ldsd* { return e < F_FW ? s.fsave + k * F_FW + e : s.junk; };
 
     d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
-    auto bf_stage = [&](auto Fc, int q, const int lane) {
+    auto bf_stage = [&](auto Fc, int q, const FConst& f) {
         constexpr bool FIRST = decltype(Fc)::value;  // q == 0: the terminal node
-        const int g = lane >> 4, c = lane & 15;
-        // Index bases with immediate offsets: a base is R_Z for an inactive lane, and the window is 0 from
-        // R_Z up to 384 in the factor sweep, so base + offset stays 0 there.  Accumulator entries outside
-        // the 10 x 10 (+ column 14) blocks are finite garbage that only ever meets zero operands, so no
-        // operand is masked.
-        // G = [A B c] (column 14 is c at R_C + k): G[4 st + g][c] at og01 + 4 st (st = 0, 1), og2
-        const int og01 = c < 15 ? c * 10 + g : R_Z, og2 = (c < 15 && g < 2) ? c * 10 + g + 8 : R_Z;
-        int h_i[4];
+        const int g = f.g, c = f.c;
+        const int og01 = f.og01, og2 = f.og2, cgi = f.cgi, gj = f.gj, gj4 = f.g, ab01 = f.ab01, ab2 = f.ab2;
+        const int bmi = f.bmi, hxu_i = f.hxu_i, huu_i = f.huu_i, v0_i = f.v0_i;
+        int h_i[4], bi[2];
+        unsigned spc[3], sab[3];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
-            h_i[r] = (a < 14 && c < 14) ? R_H + tri14(lo, hi) : (a < 14 && c == 14) ? R_G + a : R_Z;
+        for (int r = 0; r < 4; ++r) h_i[r] = f.h_i[r];
+#pragma unroll
+        for (int r = 0; r < 3; ++r) {
+            spc[r] = f.spc[r];
+            sab[r] = f.sab[r];
         }
-        // fold operands: A = C[c][g] (g < 3), B = w_g C[c][g] (c < 10) | gamma_g (c = 14)
-        const int cgi = (c < NX && g < NS) ? R_CT + g * 10 + c : R_Z, gj = g < NS ? g : 0, gj4 = g;
+        const unsigned sk_ = f.sk_;
         const double m14 = c == 14 ? 1.0 : 0.0, mg3 = g < NS ? 1.0 : 0.0;
-        // closed loop: [A | c][a][c] at ab01 + 4 r (r = 0, 1), ab2; A operand B[a = c][g] at bmi
-        const bool xcol = c < NX || c == 14;           // columns of [P | p], [A | c], [K | k_ff]
-        const int xo = c < NX ? c : 10;                // their column in the 11-wide factor-record rows
-        const int ab01 = xcol ? (c < NX ? c : 14) * 10 + g : R_Z, ab2 = (xcol && g < 2) ? (c < NX ? c : 14) * 10 + g + 8 : R_Z;
-        const int bmi = c < NX ? (NX + g) * 10 + c : R_Z;
-        // box terms: rows 10..13 of M' live in r = 2 (groups 2, 3) and r = 3 (groups 0, 1)
-        int bi[2];
-        double bxm[2], bvm[2];
+        double bxm[2], bvm[2], mg[4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int a = g + 4 * (2 + h);
@@ -472,24 +511,9 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             bxm[h] = (in && c == a) ? 1.0 : 0.0;
             bvm[h] = (in && c == 14) ? 1.0 : 0.0;
         }
-        double mg[4];
 #pragma unroll
         for (int i = 0; i < 4; ++i) mg[i] = g == i ? 1.0 : 0.0;
-        // factor-record store offsets in bytes (F_J: junk)
-        unsigned spc[3], sab[3];
-#pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int a = g + 4 * r;
-            spc[r] = 8u * ((c == 14 && a < NX) ? F_PC + a : F_J);
-            sab[r] = 8u * ((xcol && a < NX) ? F_AB + a * 11 + xo : F_J);
-        }
-        const unsigned sk_ = 8u * (xcol ? F_K + g * 11 + xo : F_J);
-        // Joseph form operands (window indices; R_Z reads 0):  A operand H^_xu[c][g] (c < 10);
-        // A operand R^0[c][g] = H_uu[c][g] (+ box diagonal, c < 4); C init H^[10 + g][c] of V's row g
-        const int hxu_i = c < NX ? R_H + tri14(c, NX + g) : R_Z;
-        const int huu_i = c < NU ? R_H + tri14(NX + (c < g ? c : g), NX + (c < g ? g : c)) : R_Z;
         const double huu_b = c == g ? 1.0 : 0.0;  // box diagonal of R^0 (c == g < 4)
-        const int v0_i = c < 14 ? R_H + tri14(c < NX + g ? c : NX + g, c < NX + g ? NX + g : c) : c == 14 ? R_G + NX + g : R_Z;
         const double v0_bd = c == NX + g ? 1.0 : 0.0, v0_bv = c == 14 ? 1.0 : 0.0;
 
         const int k = N - q;
@@ -934,8 +958,12 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     auto sweep = [&](auto Kc) {
         constexpr int K = decltype(Kc)::value, KN = K == 4 ? 1 : K + 1;
         // the stages' lane constants derive from an opaque copy of the lane id, so they are hoisted
-        // to this sweep's preheader and live only during the sweep (not across the whole solve)
-        const int ln = opaque(lane);
+        // to this sweep's preheader and live only during the sweep (not across the whole solve); the
+        // factor sweep's are built up front (fconst) and pinned in registers
+        const auto ln = [&] {
+            if constexpr (K == 1) return fconst(opaque(lane));
+            else return opaque(lane);
+        }();
         using T_ = IC<1>;
         using F_ = IC<0>;
         if (NP > PD) {
