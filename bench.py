@@ -511,6 +511,34 @@ def main_c5(args):
         "vae_ms": vae_ms, "wide_sdf_ms": wide_ms,
         "cpu_baseline": None,
     }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # the same per-instance work on the host: fp64 C encoder (oracle/vae.c) of the instance's image,
+        # the wide network's preparation phase (oracle/oracle.c) and the structured C IPM, a bounded sample
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # CPU baseline leg only (the "port")
+        O.build()
+        S = 4
+        threads = min(16, os.cpu_count() or 1)
+        spec = V.DEFAULT_ENCODER
+        flat = np.concatenate([V.synthetic_encoder(spec, 0)[n].ravel() for n, _ in spec.param_shapes()])
+        yzh = V.depth2range_table(cfg.sensor.shape_imgs, cfg.sensor.hfov, cfg.sensor.vfov)
+        img_h = synth.depth_images(S, 270, 480, seed=rank)
+        onet = O.Net(W.WIDE_SPEC, W.siren_weights(W.WIDE_SPEC, seed=0))
+        om = O.quad_model(cfg)
+        sub = {k: np.ascontiguousarray(prob[k][:S]) for k in ("x", "u", "p", "yref", "W", "yN", "WN")}
+        sub["dt"] = prob["dt"]
+        c0 = time.perf_counter()
+        pre = np.stack([O.vae_preprocess(im, (270, 480), V.clip_scale(cfg), yzh) for im in img_h])
+        lat = O.vae_encode(pre, flat)
+        sub["p"][:, :, 17:] = lat[:, None, :]
+        lin = O.linearize_batch(om, onet, sub["x"], sub["u"], sub["p"], sub["dt"], nthreads=threads)
+        O.qp_ipm_batch(lin, sub, x0[:S], quad, nthreads=threads)
+        cpu_s = time.perf_counter() - c0
+        out["cpu_baseline"] = {"value": S / cpu_s, "unit": "instance-RTI-solves/s (incl. VAE encode)",
+                               "cores": threads, "kind": "port",
+                               "sample": f"{S} instances: fp64 C encoder (oracle/vae.c, OpenMP) of one 270x480 image "
+                                         f"each, the wide network's preparation phase at N={N} and the structured "
+                                         "C IPM (oracle/oracle.c, oracle/qp_ipm.c)"}
     if rank == 0:
         print(json.dumps(out))
     if world > 1:

@@ -18,7 +18,7 @@
  *   sdfnmpc_linearize                  the per-node evaluations acados performs in the SQP-RTI
  *                                      preparation phase of Ocp.solve (ocp.py:159-170, rti_phase 0):
  *                                      ERK4 + forward sensitivities (ocp.py:106), NONLINEAR_LS residual
- *                                      and Jacobian (model/quad_rollpitchyawrate.py:370-377), and the
+ *                                      and Jacobian (model/quad_rollpitchyawrate.py:48-55), and the
  *                                      constraint vector h = [hfov, vfov, sdf] with its Jacobian
  *                                      (model/cost_const_helpers.py:48-75, gen_model.py:46-70)
  *   sdfnmpc_qp_solve                   the feedback phase of the same SQP-RTI step: the QP acados
@@ -68,7 +68,7 @@ typedef struct {
     double g;                      /* gravity, 9.81 (model/base_model.py:10) */
     double B_p_C[3];               /* sensor.B_p_C (utils/config.py:43) */
     double B_R_C[9];               /* sensor.B_R_C, row-major (utils/config.py:44) */
-    double fov_const_offset;       /* mpc.fov_const_offset (cost_const_helpers.py:452) */
+    double fov_const_offset;       /* mpc.fov_const_offset (cost_const_helpers.py:65) */
 } sdfnmpc_quad_model;
 
 /* Batched preparation phase: B instances x (N+1) shooting nodes, fp64, row-major C arrays.
@@ -95,7 +95,7 @@ typedef struct {
 
 /* QP model data and solver options (defaults in sdf-nmpc_amd/model.py / ocp.py) */
 typedef struct {
-    double lbu[4], ubu[4]; /* input box (model/quad_rollpitchyawrate.py:380-381) */
+    double lbu[4], ubu[4]; /* input box (model/quad_rollpitchyawrate.py:58-59) */
     double lh[3], uh[3];   /* h bounds: +-fov_ratio*fov, [size.xy+bound_margin, max_df+0.2] */
     double zl[3], Zl[3];   /* L1 / L2 slack penalties of the soft h rows, lower == upper (ocp.py:85-92) */
     double lm;             /* levenberg_marquardt (ocp.py:120, mpc.lm_reg) */

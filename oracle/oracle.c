@@ -13,7 +13,7 @@
  *   dynamics ........... sdf_nmpc/model/quad_rollpitchyawrate.py:19-42, utils/math.py:7-54,177-192
  *   ERK4 + sensitivities acados ERK (ocp.py:106: integrator 'ERK', defaults RK4 / 1 step /
  *                        forward sensitivities) == exact derivative of the RK4 map
- *   NLS residual ....... quad_rollpitchyawrate.py:370-377, utils/math.py:169-174
+ *   NLS residual ....... quad_rollpitchyawrate.py:48-55, utils/math.py:169-174
  *   constraints h ...... cost_const_helpers.py:48-75 (add_fov_const_trigo) + gen_model.py:46-70
  *   shooting grid ...... ocp.py:18-27 (numpy linspace / hstack / diff semantics)
  */

@@ -396,7 +396,7 @@ void siren_host(HostNet& h, uint64_t seed, float wg, float bg) {
     h.nb_states = 3; h.L = L; h.n1 = N1; h.n2 = N2; h.n3 = N3; h.n4 = N4; h.nf = EMB_NF; h.nd = EMB_ND;
     h.w0 = 20.0f;
     h.max_df = 1.0f;
-    // 'oct' dirs exactly as torch builds them (embeddings.py:140-154): +-1 / fp32 sqrt(3)
+    // 'oct' dirs exactly as torch builds them (embeddings.py:37-51): +-1 / fp32 sqrt(3)
     static const int sg[8][3] = {{-1, -1, -1}, {-1, -1, 1}, {-1, 1, -1}, {-1, 1, 1},
                                  {1, -1, -1},  {1, -1, 1},  {1, 1, -1},  {1, 1, 1}};
     const float nrm = sqrtf(3.0f);

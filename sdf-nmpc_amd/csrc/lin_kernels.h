@@ -8,7 +8,7 @@ namespace sdfn {
 struct QuadModel {
     double gamma, roll, pitch, wz;  // input scalings u -> (thrust/m, roll, pitch, yaw rate)
     double g;                       // 9.81 (base_model.py:10)
-    double fov_off[3];              // B_R_C^T B_p_C + [fov_const_offset, 0, 0] (cost_const_helpers.py:451-452)
+    double fov_off[3];              // B_R_C^T B_p_C + [fov_const_offset, 0, 0] (cost_const_helpers.py:64-65)
     double max_df;                  // NeuralDF.max_df: h_sdf when flag = 0 (gen_model.py:61)
 };
 

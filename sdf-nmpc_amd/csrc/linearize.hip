@@ -81,7 +81,7 @@ __device__ __forceinline__ void quad_f(const QuadModel& m, const dd* x, dd gamma
     f[9] = r33 * b2 - C(m.g);
 }
 
-// (q_d (x) invert(q))[3] with q = x[3:7]/|x[3:7]| (|q| = 1 up to rounding): quad_rollpitchyawrate.py:372
+// (q_d (x) invert(q))[3] with q = x[3:7]/|x[3:7]| (|q| = 1 up to rounding): quad_rollpitchyawrate.py:48-51
 __device__ __forceinline__ dd qerr3(const dd* x, const double* qd) {
     const dd inv = drsqrt(x[3] * x[3] + x[4] * x[4] + (x[5] * x[5] + x[6] * x[6]));
     return (((x[3] * qd[3] + x[4] * qd[2]) - x[5] * qd[1]) - x[6] * qd[0]) * inv;
@@ -137,7 +137,7 @@ __global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
             if (t < 14) ABc[i] = xo[i].t;
             if (t == i) A.xn[s * 10 + i] = xo[i].v;
         }
-        // ---- NONLINEAR_LS residual (quad_rollpitchyawrate.py:370-377)
+        // ---- NONLINEAR_LS residual (quad_rollpitchyawrate.py:48-55)
         const double* pr = A.p + r * A.np;
         const dd qe3 = qerr3(X, pr + 13);  // p_idx.q_d
         dd Y[11] = {X[0], X[1], X[2], qe3, X[7], X[8], X[9], roll, pitch, wz, W_a2};
@@ -160,7 +160,7 @@ __global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
         if (t < 4) A.yN[b * 4 + t] = Y[t].v;
     }
 
-    // ---- constraints h = [hfov, vfov, sdf] (cost_const_helpers.py:443-452, gen_model.py:46-61)
+    // ---- constraints h = [hfov, vfov, sdf] (cost_const_helpers.py:48-75, gen_model.py:46-61)
     const double* pr = A.p + r * A.np;
     const double flag = pr[0];
     const double Wp0 = pr[1], Wp1 = pr[2], Wp2 = pr[3];

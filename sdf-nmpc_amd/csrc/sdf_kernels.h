@@ -9,7 +9,7 @@ namespace sdfn {
 
 constexpr int EMB_ND = 8, EMB_NF = 5;
 constexpr int EMB_NB = EMB_ND * EMB_NF;  // 40 projected frequencies
-constexpr int E = 3 + 2 * EMB_NB;        // 83 embedding features (embeddings.py:207)
+constexpr int E = 3 + 2 * EMB_NB;        // 83 embedding features (embeddings.py:104)
 constexpr int KE = 88;                   // E padded to a multiple of 8 (MFMA k-grouping)
 constexpr int NE = 96;                   // E padded to 3 column blocks of 32 (d e GEMM)
 constexpr int L = 128;                   // latent size (default.yaml nn.size_latent)

@@ -3,9 +3,9 @@
 Host-side description only -- the arithmetic (dynamics, residuals, constraints and their Jacobians)
 runs in csrc/linearize.hip and csrc/sdf_mlp.hip.  Mirrors (paths relative to the reference checkout):
   * dimensions / bounds / hover input ... sdf_nmpc/model/quad_rollpitchyawrate.py:12-17, 366, 380-381
-  * formate_ref ........................ sdf_nmpc/model/quad_rollpitchyawrate.py:384-387
-  * constraint set (default flags) ..... sdf_nmpc/gen_model.py:35,41-70, model/cost_const_helpers.py:435-462
-  * slack weights ...................... model/base_model.py:296-322, ocp.py:85-92
+  * formate_ref ........................ sdf_nmpc/model/quad_rollpitchyawrate.py:62-65
+  * constraint set (default flags) ..... sdf_nmpc/gen_model.py:35,41-70, model/cost_const_helpers.py:48-75
+  * slack weights ...................... model/base_model.py:63-71,142-168, ocp.py:85-92
 """
 from __future__ import annotations
 
@@ -67,7 +67,7 @@ class Quad:
         self.lbu = np.array([0.0, -1.0, -1.0, -1.0])
         self.ubu = np.array([1.0, 1.0, 1.0, 1.0])
         self.u_hover = np.array([G / lim.gamma, 0.0, 0.0, 0.0])
-        # h = [hfov, vfov, sdf]; bounds (cost_const_helpers.py:454-462, gen_model.py:35)
+        # h = [hfov, vfov, sdf]; bounds (cost_const_helpers.py:66-75, gen_model.py:35)
         hfov_lim = cfg.sensor.hfov * cfg.mpc.fov_ratio
         vfov_lim = cfg.sensor.vfov * cfg.mpc.fov_ratio
         self.lh = np.array([-hfov_lim, -vfov_lim, cfg.robot.size.xy + cfg.mpc.bound_margin])

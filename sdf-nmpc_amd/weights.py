@@ -6,14 +6,14 @@ HIP kernels (``csrc/sdf_mlp.hip``) consume through the C ABI (``include/sdfnmpc.
 Reference anchors (``/root/reference``):
   * architecture / parameter order ... ``sdf_nmpc/network/neural_df.py:61-89`` (``layers`` ModuleDict)
   * forward semantics ................ ``sdf_nmpc/network/neural_df.py:91-103``
-  * positional embedding ............. ``sdf_nmpc/utils/embeddings.py:115-214`` ('oct' dirs :140-154)
+  * positional embedding ............. ``sdf_nmpc/utils/embeddings.py:12-111`` ('octohedron' dirs :37-51)
   * SIREN init ....................... ``sdf_nmpc/utils/layer_init.py:15-25``
   * deployed hyper-parameters ........ ``scripts/neural_nets/df_train.py:98-102``
     (``layer_sizes=[256,256,128,64]``, ``embed='oct'``, ``nb_freqs=5``, ``w0=20``, ``res='full'``)
 
 The real trained weights (``sdf_nmpc/data/sdf_90_25664.pt``) are git-LFS pointers that are absent
 from the reference checkout, so every test and benchmark uses weights regenerated from a seed by
-the counter-based PRNG below. The same PRNG is implemented in C (``csrc/sdfnmpc_prng.h``) and in the
+the counter-based PRNG below. The same PRNG is implemented in C (``csrc/engine.cpp:prng_fill``) and in the
 oracle, so weights never need to be committed.
 """
 from __future__ import annotations
@@ -28,21 +28,21 @@ MAGIC = b"SDFNMPCW"
 VERSION = 1
 _HDR = struct.Struct("<8s10I2f")  # magic, version, nb_states, L, n1..n4, nb_freqs, n_dirs, res, w0, max_df
 
-# embedding projection directions, one row per direction (embeddings.py:127-201)
+# embedding projection directions, one row per direction (embeddings.py:20-100)
 _OCT = [(-1, -1, -1), (-1, -1, +1), (-1, +1, -1), (-1, +1, +1),
         (+1, -1, -1), (+1, -1, +1), (+1, +1, -1), (+1, +1, +1)]
 _CUBE = [(-1, 0, 0), (+1, 0, 0), (0, -1, 0), (0, +1, 0), (0, 0, -1), (0, 0, +1)]
 
 
 def embedding_dirs(embed: str) -> np.ndarray:
-    """fp32 [3, n_dirs] projection matrix exactly as torch builds it (embeddings.py:127-154).
+    """fp32 [3, n_dirs] projection matrix exactly as torch builds it (embeddings.py:20-51).
 
     torch normalises each column with ``vector_norm`` in fp32: sqrt of a fp32 sum, then a
     correctly-rounded fp32 division, which numpy reproduces bit for bit.
     """
     if embed == "pos":
         return np.eye(3, dtype=np.float32)
-    if embed == "cube":  # not normalised in the reference (embeddings.py:129-139)
+    if embed == "cube":  # not normalised in the reference (embeddings.py:26-36)
         return np.array(_CUBE, dtype=np.float32).T.copy()
     if embed == "oct":
         d = np.array(_OCT, dtype=np.float32).T.copy()
@@ -67,7 +67,7 @@ class NetSpec:
         return embedding_dirs(self.embed).shape[1]
 
     @property
-    def n_embed(self) -> int:  # embeddings.py:207
+    def n_embed(self) -> int:  # embeddings.py:104
         return self.nb_freqs * self.n_dirs * 2 + 3
 
     def param_shapes(self) -> List[Tuple[str, Tuple[int, ...]]]:
@@ -91,7 +91,7 @@ WIDE_SPEC = NetSpec(layer_sizes=(1024, 1024, 512, 256))  # BASELINE config 5
 
 
 # ---------------------------------------------------------------------------------------------
-# counter-based PRNG (splitmix64 finaliser); mirrored in csrc/sdfnmpc_prng.h and oracle/oracle.c
+# counter-based PRNG (splitmix64 finaliser); mirrored in csrc/engine.cpp (prng_fill) and oracle/oracle.c
 # ---------------------------------------------------------------------------------------------
 _M64 = (1 << 64) - 1
 _GOLD = 0x9E3779B97F4A7C15

@@ -15,7 +15,7 @@ What is pinned to what:
   * lin_golden.npz     -- dynamics / cost / constraint values computed with the reference's own numpy
                           helpers (utils/math.py: quat2rot :7, euler2rot :26, hamilton_prod :177,
                           invert :169) assembled as in model/quad_rollpitchyawrate.py:19-55 and
-                          model/cost_const_helpers.py:443-452 / gen_model.py:46-61; RK4 (acados ERK,
+                          model/cost_const_helpers.py:48-75 / gen_model.py:46-61; RK4 (acados ERK,
                           ocp.py:106) on top; Jacobians by torch autograd of an fp64 restatement that
                           is asserted equal (values) to the helper-based version and to central
                           finite differences of it (derivatives).  CasADi/acados are not installed,
@@ -172,7 +172,7 @@ def f_expl_np(x, u):
 
 
 def y_np(x, u, p):
-    """quad_rollpitchyawrate.py:371-377 (stage/terminal NONLINEAR_LS residual)."""
+    """quad_rollpitchyawrate.py:48-55 (stage/terminal NONLINEAR_LS residual)."""
     q = x[3:7] / np.linalg.norm(x[3:7])
     q_d = p[P_IDX.q_d]
     q_e = rmath.hamilton_prod(q_d, rmath.invert(q))
@@ -182,7 +182,7 @@ def y_np(x, u, p):
 
 
 def h_np(x, p, df, max_df=1.0):
-    """cost_const_helpers.py:443-452 (FOV, trigo form) + gen_model.py:46-61 (sdf, flag)."""
+    """cost_const_helpers.py:48-75 (FOV, trigo form) + gen_model.py:46-61 (sdf, flag)."""
     W_R_Co = p[P_IDX.W_R_Co].reshape(3, 3)  # == casadi reshape((3,3)).T
     W_p_Co = p[P_IDX.W_p_Co]
     flag = p[P_IDX.flag]

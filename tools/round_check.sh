@@ -1,12 +1,15 @@
 #!/bin/bash
-# Full round check on the GPU box: GPU tests, smoke, default bench, C5 bench, rocprofv3 kernel stats of both.
+# Round check on a fresh GPU box: the -m gpu suite, smoke, the default bench (C3 + c2 leg + CPU baseline),
+# the C5 bench, rocprofv3 kernel-trace stats of both, FETCH_SIZE / WRITE_SIZE passes of the default bench
+# (separate runs, MI355X_MICROARCH.md), and the QP per-phase cycle stamps.  Everything under
+# gpurun_out/rc/; the summaries worth keeping are copied to profiles/<round>/ afterwards.
 set -euo pipefail
 cd /tmp && export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/rc
 mkdir -p $O
 cd $R
-timeout -k 10 600 python -u -m pytest tests -v -m gpu -x --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 2; }
+timeout -k 10 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 2; }
 tail -2 $O/pytest_gpu.log
 cd /tmp
 timeout -k 10 300 python -c "import sys; sys.path.insert(0, '$R'); import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
@@ -16,7 +19,12 @@ cat $O/bench.json
 timeout -k 10 400 python $R/bench.py --config c5 > $O/bench_c5.json 2> $O/bench_c5.err
 cat $O/bench_c5.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- \
-    python $R/bench.py --no-cpu-baseline --no-b1 > $O/bench_traced.json 2> $O/trace.err
+    python3 $R/bench.py --no-cpu-baseline --no-b1 --no-c2 > $O/bench_traced.json 2> $O/trace.err
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c5 -o bench -- \
-    python $R/bench.py --config c5 --no-cpu-baseline > $O/bench_c5_traced.json 2> $O/trace_c5.err
+    python3 $R/bench.py --config c5 --no-cpu-baseline > $O/bench_c5_traced.json 2> $O/trace_c5.err
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch -o p -- \
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 --prep-steps 2 --no-b1 --no-c2 > /dev/null 2> $O/fetch.err
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o p -- \
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 --prep-steps 2 --no-b1 --no-c2 > /dev/null 2> $O/write.err
+timeout -k 10 200 python3 $R/tools/qp_stamps.py > $O/qp_stamps.txt 2>&1
 echo done
