@@ -122,6 +122,12 @@ __device__ __forceinline__ double rdlane(double v, int l) {
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
+// f64 4x4x4, four blocks: with the A block replicated over the blocks (lane (g, c) holds A[c & 3][g]) it is
+// rows 0..3 of the 16x16x4 product in one accumulator register (lane (g, c): D[g][c]) at a quarter of
+// the matrix-pipe time (16 cycles against 64, dependent latency ~21 against ~67 on gfx950)
+__device__ __forceinline__ double mfma4(double a, double b, double c) {
+    return __builtin_amdgcn_mfma_f64_4x4x4f64(a, b, c, 0, 0, 0);
+}
 // 1/x: hardware estimate + two Newton steps (the IPM's row updates; replaces IEEE division)
 __device__ __forceinline__ double rcp_nr(double x) {
     double y = __builtin_amdgcn_rcp(x);
@@ -193,9 +199,10 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubl
 // offsets (F_J: a junk slot).  Built once per factor sweep; every field goes through opaque(), so the
 // compiler keeps them in registers instead of rematerialising the index arithmetic (with its
 // divergent branches) at every stage.
+constexpr int FJB = 8 * F_J;
 struct FConst {
     int g, c, og01, og2, cgi, gj, ab01, ab2, bmi, hxu_i, huu_i, v0_i;
-    int h_i[4];
+    int h_i[4], bq[3];
     unsigned spc[3], sab[3], sk_;
 };
 
@@ -225,14 +232,19 @@ __device__ __forceinline__ FConst fconst(int lane) {
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const int a = g + 4 * r;
-        f.spc[r] = (unsigned)opaque(8 * ((c == 14 && a < NX) ? F_PC + a : F_J));
-        f.sab[r] = (unsigned)opaque(8 * ((xcol && a < NX) ? F_AB + a * 11 + xo : F_J));
+        f.spc[r] = (unsigned)opaque((c == 14 && a < NX) ? 8 * (F_PC + a) : FJB);
+        f.sab[r] = (unsigned)opaque((xcol && a < NX) ? 8 * (F_AB + a * 11 + xo) : FJB);
     }
-    f.sk_ = (unsigned)opaque(8 * (xcol ? F_K + g * 11 + xo : F_J));
+    f.sk_ = (unsigned)opaque(xcol ? 8 * (F_K + g * 11 + xo) : FJB);
     // Joseph form operands (window indices; R_Z reads 0):  A operand H^_xu[c][g] (c < 10);
     // A operand R^0[c][g] = H_uu[c][g] (+ box diagonal, c < 4); C init H^[10 + g][c] of V's row g
     f.hxu_i = opaque(c < NX ? R_H + tri14(c, NX + g) : R_Z);
-    f.huu_i = opaque(c < NU ? R_H + tri14(NX + (c < g ? c : g), NX + (c < g ? g : c)) : R_Z);
+    // 4x4x4 A operands (one 4 x 4 block, replicated over the instruction's four column blocks: lane
+    // (g, c) holds A[c & 3][g]):  R^0[i][g] = H_uu[i][g];  B^T of k-step st: B[4 st + g][i] = G[4 st + g][10 + i]
+    const int c3 = c & 3;
+    f.huu_i = opaque(R_H + tri14(NX + (c3 < g ? c3 : g), NX + (c3 < g ? g : c3)));
+#pragma unroll
+    for (int st = 0; st < 3; ++st) f.bq[st] = opaque(4 * st + g < NX ? (NX + c3) * 10 + 4 * st + g : R_Z);
     f.v0_i = opaque(c < 14 ? R_H + tri14(c < NX + g ? c : NX + g, c < NX + g ? NX + g : c) : c == 14 ? R_G + NX + g : R_Z);
     return f;
 }
@@ -359,10 +371,16 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
 #define STAMP_DECL long long st_t0 = clock64(), st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
 #define STAMP(i) do { const long long t1_ = clock64(); st_acc[i] += t1_ - st_t0; st_t0 = t1_; } while (0)
 #define STAMP_OUT if (lane == 0 && A.stamps) for (int i_ = 0; i_ < 16; ++i_) A.stamps[(size_t)b * 16 + i_] = (double)st_acc[i_];
+#ifdef QP_FSTAMPS  // finer: slices of the backward factor stage, each ending when value v is available
+#define FSTAMP(i, v) do { long long t1_; asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1_) : "v"(v)); st_acc[i] += t1_ - st_t0; st_t0 = t1_; } while (0)
+#endif
 #else
 #define STAMP_DECL
 #define STAMP(i)
 #define STAMP_OUT
+#endif
+#ifndef FSTAMP
+#define FSTAMP(i, v)
 #endif
 
 __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
@@ -485,6 +503,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // every store of an inactive lane goes to a junk slot.
     auto fs_at = [&](int k, int e) -> ldsd* { return e < F_FW ? s.fsave + k * F_FW + e : s.junk; };
 
+#define FBST(v, off) bst(v, rsF, off, sko)
     d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
     auto bf_stage = [&](auto Fc, int q, const FConst& f) {
         constexpr bool FIRST = decltype(Fc)::value;  // q == 0: the terminal node
@@ -513,7 +532,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i) mg[i] = g == i ? 1.0 : 0.0;
-        const double huu_b = c == g ? 1.0 : 0.0;  // box diagonal of R^0 (c == g < 4)
+        const double huu_b = (c & 3) == g ? 1.0 : 0.0;  // box diagonal of R^0 (replicated 4x4x4 A block)
         const double v0_bd = c == NX + g ? 1.0 : 0.0, v0_bv = c == 14 ? 1.0 : 0.0;
 
         const int k = N - q;
@@ -530,20 +549,38 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             return;
         }
         const unsigned sko = (unsigned)k * (FREC * 8u);
+        FSTAMP(8, Pa[0]);
         // ---- W = P G (K = 10: k-steps 0..2); column 14 -> P c, then + p
         const double og0 = win[og01], og1 = win[og01 + 4], og2v = win[og2];
+        const double bq0 = win[f.bq[0]], bq1 = win[f.bq[1]], bq2 = win[f.bq[2]];
+        const double hv0 = win[v0_i] + v0_bd * s.bd[k * NU + gj4] + v0_bv * s.bv[k * NU + gj4];
+        FSTAMP(13, og0 + og1 + og2v);
         d4 W = {0.0, 0.0, 0.0, 0.0};
         W = mfma(Pa[0], og0, W);
         W = mfma(Pa[1], og1, W);
         W = mfma(Pa[2], og2v, W);
         __builtin_amdgcn_sched_barrier(0);  // the W chain goes first; the rest fills its latency
-        // ---- M' = G_ab^T W + [H | g] + C^T diag(w) [C | gamma] + box terms
-        d4 M;
+        FSTAMP(14, W[3]);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) M[r] = win[h_i[r]];
+        for (int r = 0; r < 3; ++r) FBST(W[r], spc[r]);
+#pragma unroll
+        for (int r = 0; r < 3; ++r) W[r] = fma(m14, Pa[r], W[r]);
+        // ---- rows 10..13 of M' ([S | R^ | m_u] = [H_u | g_u] + box terms + B^T W), lane (i, c): M'[10 + i][c]
+        double Mu = mfma4(bq0, W[0], hv0);
+        Mu = mfma4(bq1, W[1], Mu);
+        Mu = mfma4(bq2, W[2], Mu);
+        __builtin_amdgcn_sched_barrier(0);  // M_u ahead of everything else on the matrix pipe
+        // B^T P (lane (g, c): (P B)[c][g], the A operand of P B [K | k_ff] below)
+        double Ub = mfma4(bq0, Pa[0], 0.0);
+        Ub = mfma4(bq1, Pa[1], Ub);
+        Ub = mfma4(bq2, Pa[2], Ub);
+        // H^ = [H | g] + C^T diag(w) [C | gamma] + box terms (the Joseph form's stage term)
+        d4 Hh;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) Hh[r] = win[h_i[r]];
 #pragma unroll
         for (int h = 0; h < 2; ++h)
-            M[2 + h] += bxm[h] * s.bd[k * NU + bi[h]] + bvm[h] * s.bv[k * NU + bi[h]];
+            Hh[2 + h] += bxm[h] * s.bd[k * NU + bi[h]] + bvm[h] * s.bv[k * NU + bi[h]];
         d4 Ab;  // closed-loop init [A | c] (rows 12..15: don't care)
         Ab[0] = win[ab01];
         Ab[1] = win[ab01 + 4];
@@ -552,23 +589,14 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double bm = win[bmi];
         const double hxa = win[hxu_i];
         const double hua = win[huu_i] + huu_b * s.bd[k * NU + gj4];
-        const double hv0 = win[v0_i] + v0_bd * s.bd[k * NU + gj4] + v0_bv * s.bv[k * NU + gj4];
-        M = mfma(cg, fb, M);
-        d4 Hh = M;  // H^ = [H | g] + fold + box terms (the Joseph form's stage term)
-#pragma unroll
-        for (int r = 0; r < 3; ++r) bst(W[r], rsF, spc[r], sko);
-#pragma unroll
-        for (int r = 0; r < 4; ++r) W[r] = fma(m14, Pa[r], W[r]);
-        M = mfma(og0, W[0], M);
-        M = mfma(og1, W[1], M);
-        M = mfma(og2v, W[2], M);
-        // ---- L = chol(R^): R^[i][j] = M'[10+i][10+j], read straight from the accumulator lanes
-        const double r00 = rdlane(M[2], 42), r10 = rdlane(M[2], 58), r20 = rdlane(M[3], 10), r30 = rdlane(M[3], 26);
-        const double r11 = rdlane(M[2], 59), r21 = rdlane(M[3], 11), r31 = rdlane(M[3], 27);
-        const double r22 = rdlane(M[3], 12), r32 = rdlane(M[3], 28), r33 = rdlane(M[3], 29);
-        // rows 10..13 of M' ([S | R^ | m_u]) of column c into every lane of that column
-        const double s0 = __shfl(M[2], 32 + c), s1 = __shfl(M[2], 48 + c);
-        const double s2 = __shfl(M[3], c), s3 = __shfl(M[3], 16 + c);
+        Hh = mfma(cg, fb, Hh);
+        FSTAMP(9, Mu);
+        // ---- L = chol(R^): R^[i][j] = M'[10+i][10+j] at lane 16 i + 10 + j
+        const double r00 = rdlane(Mu, 10), r10 = rdlane(Mu, 26), r20 = rdlane(Mu, 42), r30 = rdlane(Mu, 58);
+        const double r11 = rdlane(Mu, 27), r21 = rdlane(Mu, 43), r31 = rdlane(Mu, 59);
+        const double r22 = rdlane(Mu, 44), r32 = rdlane(Mu, 60), r33 = rdlane(Mu, 61);
+        // rows 10..13 of M' of column c into every lane of that column
+        const double s0 = __shfl(Mu, c), s1 = __shfl(Mu, 16 + c), s2 = __shfl(Mu, 32 + c), s3 = __shfl(Mu, 48 + c);
         const double i0 = rsqrt_nr(r00);
         const double l10 = r10 * i0, l20 = r20 * i0, l30 = r30 * i0;
         const double i1 = rsqrt_nr(r11 - l10 * l10);
@@ -586,37 +614,35 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double k1 = (-y1 - l21 * k2 - l31 * k3) * i1;
         const double k0 = (-y0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
         const double kg = mg[0] * k0 + mg[1] * k1 + mg[2] * k2 + mg[3] * k3;
+        FSTAMP(10, kg);
         // ---- Joseph form: [P | p] <- T^T H^ T + A~^T [P A~ | P b~ + p],  T = [I 0; K k_ff; 0 1]
         // (a sum of PSD terms: no cancellation of M'_xx - Y^T Y when a hard state row puts a huge fold
         // into P; that cancellation costs ~1e-6 absolute accuracy and the IPM its worst-case iterations)
+        // with [P A~ | P b~ + p] = [P A | P c + p] + (P B) [K | k_ff]: one product after K, from W
+        const double V = mfma4(hua, kg, hv0);                       // rows 10..13 of H^ T
         Ab = mfma(bm, kg, Ab);                                      // [A~ | b~] = [A | c] + B [K | k_ff]
-        d4 V = {hv0, 0.0, 0.0, 0.0};
-        V = mfma(hua, kg, V);                                       // rows 10..13 of H^ T, in rows 0..3
-        d4 W2 = {0.0, 0.0, 0.0, 0.0};
-        W2 = mfma(Pa[0], Ab[0], W2);
-        W2 = mfma(Pa[1], Ab[1], W2);
-        W2 = mfma(Pa[2], Ab[2], W2);
+        const d4 W2 = mfma(Ub, kg, W);                              // [P A~ | P b~ + p]
         Hh = mfma(hxa, kg, Hh);                                     // H^_x T
-        Hh = mfma(kg, V[0], Hh);                                    // + K^T (H^_u T)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) W2[r] = fma(m14, Pa[r], W2[r]);  // column 14: P b~ + p
+        Hh = mfma(kg, V, Hh);                                       // + K^T (H^_u T)
         Pa = mfma(Ab[0], W2[0], Hh);
         Pa = mfma(Ab[1], W2[1], Pa);
         Pa = mfma(Ab[2], W2[2], Pa);
+        FSTAMP(11, Pa[2]);
         __builtin_amdgcn_sched_barrier(0);  // hand P to the next stage before the record stores
         // ---- factor record (and its LDS copy for the first forward stages)
-        bst(kg, rsF, sk_, sko);
+        FBST(kg, sk_);
         {  // the (uniform) Cholesky factor: every lane stores the same 16 bytes, no lane selection
             d2* Lp = (d2*)(F + (size_t)k * FREC + F_L);
             Lp[0] = d2{i0, l10}; Lp[1] = d2{i1, l20}; Lp[2] = d2{l21, i2}; Lp[3] = d2{l30, l31}; Lp[4] = d2{l32, i3};
         }
 #pragma unroll
-        for (int r = 0; r < 3; ++r) bst(Ab[r], rsF, sab[r], sko);
+        for (int r = 0; r < 3; ++r) FBST(Ab[r], sab[r]);
         if (k < PD) {
 #pragma unroll
             for (int r = 0; r < 3; ++r) *fs_at(k, sab[r] / 8) = Ab[r];
             *fs_at(k, sk_ / 8) = kg;
         }
+        FSTAMP(12, kg);
     };
 
     // ------------------------------------------------------------ backward stage, corrector
