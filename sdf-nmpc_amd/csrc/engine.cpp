@@ -75,6 +75,7 @@ struct sdfnmpc_ctx {
     hipStream_t aux = nullptr;                       // low-priority side stream (fork/join per call)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool lin_first = false;
+    bool serial_prep = false;  // diagnostic (SDFNMPC_SERIAL_PREP=1): linearize after the SDF kernel, same stream
     int tile_rows = 32;
     bool timing = false;
     DevBuf c13, sdf4, lat, out4, glat, qpw, qpst, wws;
@@ -155,6 +156,8 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
     }
     const char* lf = getenv("SDFNMPC_LIN_FIRST");
     c->lin_first = lf && *lf == '1';
+    const char* sp = getenv("SDFNMPC_SERIAL_PREP");
+    c->serial_prep = sp && *sp == '1';
     *out = c;
     return SDFNMPC_OK;
 }
@@ -947,6 +950,7 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
                           mdl->B_R_C[2 * 3 + i] * mdl->B_p_C[2] + (i == 0 ? mdl->fov_const_offset : 0.0);
     la.m.max_df = net->host.max_df;
     auto fork_lin = [&]() -> int {
+        if (ctx->serial_prep) return SDFNMPC_OK;
         HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
         HIPCHK(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
         HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->aux); }, ctx->aux));
@@ -969,6 +973,10 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
         rc = run_wide(ctx, net, rows, nullptr, nullptr, a->p + 17, stride, n_inst, a->latent_mode == 0 ? a->N + 1 : 1,
                       sdf4, &cons);
         if (rc) return rc;
+        if (ctx->serial_prep) {
+            HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }, ctx->stream));
+            return SDFNMPC_OK;
+        }
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
         return SDFNMPC_OK;
     }
@@ -979,6 +987,10 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
     rc = run_sdf(ctx, net, rows, nullptr, (const float*)ctx->c13.p,
                  a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows, &cons);
     if (rc) return rc;
+    if (ctx->serial_prep) {
+        HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }, ctx->stream));
+        return SDFNMPC_OK;
+    }
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
     return SDFNMPC_OK;
 }

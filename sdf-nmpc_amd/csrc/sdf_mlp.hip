@@ -36,6 +36,11 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 #endif
 }
 
+// weight prefetch depth of the GEMM loop, in groups of 4 k-steps
+#ifndef SDF_PF
+#define SDF_PF 3
+#endif
+
 // Row held by accumulator register `reg` of lane half `h` (32x32 f32 MFMA C/D layout, gfx950).
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
@@ -49,7 +54,7 @@ __device__ __forceinline__ void gemm(f32x16 (&acc)[RB][NCB], const float* lds, i
                                      const float4* __restrict__ wpk, int cb0, int lane) {
     constexpr int G = K / 8;
     constexpr int NG = G1 - G0;
-    constexpr int PF = (NG < 3) ? NG : 3;
+    constexpr int PF = (NG < SDF_PF) ? NG : SDF_PF;
     static_assert(0 <= G0 && G0 < G1 && G1 <= G, "group range");
     static_assert(K % 8 == 0, "K must be a multiple of 8");
     const int r = lane & 31, h = lane >> 5;
@@ -135,6 +140,12 @@ __device__ __forceinline__ void init_hoisted(f32x16 (&acc)[RB][NCB], const float
         }
 }
 
+#ifdef SDF_CHEAP_SIN  // diagnostic build (tools/build_variant.sh): the kernel's time without its sine epilogues
+__device__ __forceinline__ void act_sincos(float x, float* s, float* c) { *s = x * 0.01f; *c = 1.0f - x; }
+#else
+__device__ __forceinline__ void act_sincos(float x, float* s, float* c) { sdfn_sincosf(x, s, c); }
+#endif
+
 // sine activation epilogue: t = w0*acc, h = sin(t) -> LDS, keep cos(t) in `d`
 template <int RB, int NCB>
 __device__ __forceinline__ void act_fwd(f32x16 (&acc)[RB][NCB], f32x16 (&d)[RB][NCB], float* out, int stride,
@@ -147,7 +158,7 @@ __device__ __forceinline__ void act_fwd(f32x16 (&acc)[RB][NCB], f32x16 (&d)[RB][
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 float s, co;
-                sdfn_sincosf(w0 * acc[rb][c][i], &s, &co);
+                act_sincos(w0 * acc[rb][c][i], &s, &co);
                 d[rb][c][i] = co;
                 out[(rb * 32 + acc_row(i, h)) * stride + (cb0 + 4 * c) * 32 + col] = s;
             }
@@ -269,7 +280,7 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 float s, co;
-                sdfn_sincosf(w0 * acc1[rb][0][i], &s, &co);
+                act_sincos(w0 * acc1[rb][0][i], &s, &co);
                 const int row = rb * 32 + acc_row(i, hh);
                 Ebuf[row * SE + cb4 * 32 + col] = s;
                 Bbuf[row * SA + cb4 * 32 + col] = (w5 * co) * w0;

@@ -17,6 +17,7 @@
 #endif
 
 SDFN_HD void sdfn_sincosf(float x, float* s_out, float* c_out) {
+#ifndef SDF_FAST_SIN_ONLY  // diagnostic build: no large-argument path (wrong beyond |x| = 2^17)
     if (!(fabsf(x) < 131072.0f)) {  // also NaN / inf
 #if defined(__HIP_DEVICE_COMPILE__)
         sincosf(x, s_out, c_out);
@@ -26,6 +27,7 @@ SDFN_HD void sdfn_sincosf(float x, float* s_out, float* c_out) {
 #endif
         return;
     }
+#endif
     const float q = rintf(x * 0.636619772367581343f);  // x * 2/pi
     // pi/2 = C1 + C2 + C3, C1/C2 exact fp32
     float r = fmaf(q, -1.57079637050628662109375f, x);
