@@ -554,13 +554,13 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double og0 = win[og01], og1 = win[og01 + 4], og2v = win[og2];
         const double bq0 = win[f.bq[0]], bq1 = win[f.bq[1]], bq2 = win[f.bq[2]];
         const double hv0 = win[v0_i] + v0_bd * s.bd[k * NU + gj4] + v0_bv * s.bv[k * NU + gj4];
-        FSTAMP(13, og0 + og1 + og2v);
+        FSTAMP(8, og0 + og1 + og2v);
         d4 W = {0.0, 0.0, 0.0, 0.0};
         W = mfma(Pa[0], og0, W);
         W = mfma(Pa[1], og1, W);
         W = mfma(Pa[2], og2v, W);
         __builtin_amdgcn_sched_barrier(0);  // the W chain goes first; the rest fills its latency
-        FSTAMP(14, W[3]);
+        FSTAMP(8, W[3]);
 #pragma unroll
         for (int r = 0; r < 3; ++r) FBST(W[r], spc[r]);
 #pragma unroll
@@ -665,6 +665,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const unsigned bc_st = lane < 14 ? lane * 11 + 10 : F_J;  // b~ rows (lanes < 10), k_ff rows (lanes 10..13)
         ldsd* const bc_p = fx ? s.p + lane : s.junk;
         const int k = N - q;
+        FSTAMP(7, mfx);
         double off = *bc_g;
 #pragma unroll
         for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * bc_ct[10 * j];
@@ -697,6 +698,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) pv[l] = pp[l];
         __builtin_amdgcn_sched_barrier(0);
+        FSTAMP(13, pv[4].y + B3 + row[9] + Lv[4].y + pcv[4].y + kk[3]);
         // g~_u (uniform) and the per-lane offset of the chain
 #pragma unroll
         for (int i = 0; i < NU; ++i) off += kk[i] * (guw[i] + bvv[i]) + mu_[i] * bvv[i];
@@ -708,6 +710,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
         const double z = a0 + a1;
         *bc_p = z;
+        FSTAMP(14, z);
         // off the chain: k_ff, b~
         const double z0 = rdlane(z, 10), z1 = rdlane(z, 11), z2 = rdlane(z, 12), z3 = rdlane(z, 13);
         const double i0 = Lv[0].x, l10 = Lv[0].y, i1 = Lv[1].x, l20 = Lv[1].y, l21 = Lv[2].x;
@@ -724,6 +727,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         const double fv = mfx * bb + mu_[0] * k0 + mu_[1] * k1 + mu_[2] * k2 + mu_[3] * k3;
         bst(fv, rsF, 8u * bc_st, (unsigned)k * (FREC * 8u));
         if (k < PD) *fs_at(k, bc_st) = fv;
+        FSTAMP(15, fv);
     };
 
     // ------------------------------------------------------------ initial iterate (dynamics-feasible):
