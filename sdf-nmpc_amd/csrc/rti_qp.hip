@@ -56,9 +56,11 @@ using IC = std::integral_constant<int, V>;
 constexpr int NX = 10, NU = 4, NS = 3;
 // stage record: [AB 140 (column j = d xn / d (x,u)_j) | c 10 | g 14 | C^T 30 (row j = d h_j / d x) | H 105 upper | 0]
 constexpr int R_AB = 0, R_C = 140, R_G = 150, R_CT = 164, R_H = 194, R_Z = 299, REC = QP_REC;
-// factor record: [A~|b~ 10 x 11 | K|k_ff 4 x 11 | (unused 4 x 10) | L 10 (lower packed, diagonal 1/L_ii) | P c 10 | junk 2]
-constexpr int F_AB = 0, F_K = 110, F_L = 194, F_PC = 204, F_J = 214, FREC = QP_FREC;
-constexpr int F_FW = 154;  // forward sweeps read [0, F_FW)
+// factor record: [A~|b~ 10 x 12 | K|k_ff 4 x 12 | L 10 (lower packed, diagonal 1/L_ii) | P c 10 | junk 2]; rows are
+// 12 doubles (11 used) so that a forward stage reads its row with five 16-byte LDS reads
+constexpr int FR = 12;  // factor-record row stride
+constexpr int F_AB = 0, F_K = 10 * FR, F_L = 14 * FR, F_PC = F_L + 10, F_J = F_PC + 10, FREC = QP_FREC;
+constexpr int F_FW = 14 * FR;  // forward sweeps read [0, F_FW)
 constexpr int SLOT = QP_SLOT, PD = QP_RING;
 // Window of one stream position per sweep kind: n_loads(K) loads of 64 consecutive doubles (lanes
 // clamped to the record), load j landing at window offset 64 j:
@@ -72,7 +74,7 @@ __host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K ==
 __host__ __device__ constexpr int load_at(int K, int j) {
     return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 4 ? 64 * j : 100 + 64 * (j - 4));
 }
-static_assert(FREC == 216 && PD == 3 && SLOT == 6, "record layout");
+static_assert(FREC == F_J + 2 && FREC % 2 == 0 && F_FW <= WF_CT && PD == 3 && SLOT == 6, "record layout");
 static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT, "window layout");
 // IPM starting point and step fraction (the kernel waits for its slowest instance, so these were
 // chosen on the worst case over seeds / x0 spreads with the C restatement, oracle/qp_ipm.c):
@@ -233,9 +235,9 @@ __device__ __forceinline__ FConst fconst(int lane) {
     for (int r = 0; r < 3; ++r) {
         const int a = g + 4 * r;
         f.spc[r] = (unsigned)opaque((c == 14 && a < NX) ? 8 * (F_PC + a) : FJB);
-        f.sab[r] = (unsigned)opaque((xcol && a < NX) ? 8 * (F_AB + a * 11 + xo) : FJB);
+        f.sab[r] = (unsigned)opaque((xcol && a < NX) ? 8 * (F_AB + a * FR + xo) : FJB);
     }
-    f.sk_ = (unsigned)opaque(xcol ? 8 * (F_K + g * 11 + xo) : FJB);
+    f.sk_ = (unsigned)opaque(xcol ? 8 * (F_K + g * FR + xo) : FJB);
     // Joseph form operands (window indices; R_Z reads 0):  A operand H^_xu[c][g] (c < 10);
     // A operand R^0[c][g] = H_uu[c][g] (+ box diagonal, c < 4); C init H^[10 + g][c] of V's row g
     f.hxu_i = opaque(c < NX ? R_H + tri14(c, NX + g) : R_Z);
@@ -476,10 +478,15 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             off = *(fx ? win + R_C + lane : s.zero);
         } else {
             const ldsd* fk = k < PD ? s.fsave + k * F_FW : win;
-            const ldsd* rp = lane < 14 ? fk + lane * 11 : fc ? win + WF_CT + fcj * 10 : win;
+            // 16-byte aligned rows: [A~ | b~] / [K | k_ff] row `lane`, C^T row lane - 14, zeros
+            const ldsd2* rp = (const ldsd2*)(lane < 14 ? fk + lane * FR : fc ? win + WF_CT + fcj * 10 : s.zero);
 #pragma unroll
-            for (int l = 0; l < NX; ++l) row[l] = rp[l];
-            off = *(lane < 14 ? fk + lane * 11 + 10 : s.zero);
+            for (int l = 0; l < NX / 2; ++l) {
+                const d2 v = rp[l];
+                row[2 * l] = v.x;
+                row[2 * l + 1] = v.y;
+            }
+            off = *(lane < 14 ? fk + lane * FR + 10 : s.zero);
         }
         d2 xv[NX / 2];  // the chain input x_k, read after everything else
 #pragma unroll
@@ -653,16 +660,16 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         constexpr bool FIRST = decltype(Fc)::value;
         const bool fx = lane < NX, fu = lane >= NX && lane < 14;
         const ldsd* bc_row = fx ? win + F_AB + lane : fu ? win + WB_R + lane * 10 : win;
-        const int bc_str = fx ? 11 : 1;
+        const int bc_str = fx ? FR : 1;
         const ldsd* bc_ct = fx ? win + WB_R + R_CT + lane : s.zero;  // C^T[j][r] at + 10 j
-        const ldsd* bc_k = fx ? win + F_K + lane : s.zero;           // K[i][r] at + 11 i
+        const ldsd* bc_k = fx ? win + F_K + lane : s.zero;           // K[i][r] at + FR i
         const ldsd* bc_g = lane < 14 ? win + WB_R + R_G + lane : s.zero;
         const double mfx = fx ? 1.0 : 0.0;
         double mu_[NU];
     #pragma unroll
         for (int i = 0; i < NU; ++i) mu_[i] = lane == NX + i ? 1.0 : 0.0;
         const int bx = fx ? lane : 0;
-        const unsigned bc_st = lane < 14 ? lane * 11 + 10 : F_J;  // b~ rows (lanes < 10), k_ff rows (lanes 10..13)
+        const unsigned bc_st = lane < 14 ? lane * FR + 10 : F_J;  // b~ rows (lanes < 10), k_ff rows (lanes 10..13)
         ldsd* const bc_p = fx ? s.p + lane : s.junk;
         const int k = N - q;
         FSTAMP(7, mfx);
@@ -679,7 +686,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         for (int i = 0; i < NU; ++i) {
             bvv[i] = s.bv[k * NU + i];
             guw[i] = win[WB_R + R_G + NX + i];
-            kk[i] = bc_k[11 * i];
+            kk[i] = bc_k[FR * i];
         }
 #pragma unroll
         for (int l = 0; l < NX; ++l) row[l] = bc_row[l * bc_str];
