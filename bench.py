@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--prep-steps", type=int, default=50, help="timed preparation-only steps (0: skip)")
     ap.add_argument("--no-b1", action="store_true", help="skip the B=1 latency probe (profiling runs)")
     ap.add_argument("--no-c2", action="store_true", help="skip the CasADi-external (libsdf_l4c.so) call leg")
+    ap.add_argument("--no-c1", action="store_true", help="skip the B=1, N=20 controller-step leg (config C1)")
     ap.add_argument("--config", choices=("c3", "c5"), default="c3",
                     help="c3: the headline 1024 x 40 RTI (default); c5: 4x-wide SDF MLP + in-loop VAE encode, "
                          "N = 60, 4096 instances over 8 GPUs (512 per GPU)")
@@ -227,6 +228,10 @@ def main():
     c2 = None
     if rank == 0 and not args.no_c2:
         c2 = bench_c2(local, N, W, args.no_cpu_baseline)
+    # config C1 (B = 1, N = 20) through the controller API
+    c1 = None
+    if rank == 0 and not args.no_c1:
+        c1 = bench_c1(local, args.no_cpu_baseline)
 
     # traffic from the committed PMC profile of this same command (profiles/)
     traffic = None
@@ -304,11 +309,75 @@ def main():
         "cpu_baseline": cpu,
         "prep": prep_out,
         "c2": c2,
+        "c1": c1,
     }
     if rank == 0:
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_c1(device, no_cpu, steps=200):
+    """BASELINE.json configs[0] (C1): one quadrotor, N = 20, the controller's own control step
+    (Nmpc.set_x0 + Nmpc.solve: host arrays in, u_0 out, controller.py:72-81) repeated with the iterate
+    carried, p50 / p99 wall time per step.  Beside it the same closed loop on the host (the C oracle's
+    preparation phase and structured IPM, one thread), the CPU plumbing C1 names."""
+    from sdf_nmpc_amd.config import Config
+    from sdf_nmpc_amd.controller import Nmpc
+    from sdf_nmpc_amd.reference import Ref, yaw2quat
+    N = 20
+    cfg = Config(mpc__N=N)
+    n = Nmpc(cfg, batch=1, device=device)
+    rng = np.random.default_rng(11)
+    x0 = np.zeros(10)
+    x0[:3] = rng.uniform(-1, 1, 3)
+    x0[3:7] = yaw2quat(0.2)
+    n.set_sdf_flag(1.0)
+    n.set_latent(rng.normal(0, 1, 128), x0[:3] + 0.1, np.eye(3))
+    r = Ref(cfg)
+    r.p, r.q = x0[:3] + np.array([2.0, -1.0, 0.5]), yaw2quat(0.3)
+    r.use_weights(r.W_on)
+    for k in range(N + 1):
+        n.set_ref(r, k)
+    ts = []
+    for i in range(steps + 10):
+        t0 = time.perf_counter()
+        n.set_x0(x0)
+        n.solve()
+        t1 = time.perf_counter()
+        if i >= 10:
+            ts.append((t1 - t0) * 1e3)
+    res = {"p50_step_ms": float(np.percentile(ts, 50)), "p99_step_ms": float(np.percentile(ts, 99)), "steps": steps,
+           "path": "Nmpc.set_x0 + Nmpc.solve (host arrays, solver object, one SQP-RTI iteration), B=1, N=20"}
+    if not no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "oracle"))
+        import oracle as O  # CPU baseline leg only (the "port")
+        O.build()
+        from sdf_nmpc_amd import weights as W
+        onet = O.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed=0))
+        om = O.quad_model(cfg)
+        dt = n.ocp.dt
+        xs = np.repeat(x0[None, None], N + 1, axis=1)
+        us = np.broadcast_to(n.model.u_hover, (1, N, 4)).copy()
+        p = n.p.reshape(1, N + 1, -1)
+        prob = {"yref": n.y.reshape(1, N, -1), "W": n.W.reshape(1, N, -1), "yN": n.yN.reshape(1, -1),
+                "WN": n.WN.reshape(1, -1), "dt": dt}
+        cs = []
+        for i in range(steps + 5):
+            t0 = time.perf_counter()
+            xs[:, 0] = x0
+            lin = O.linearize_batch(om, onet, xs, us, p, dt, nthreads=1)
+            q = O.qp_ipm_batch(lin, dict(prob, x=xs, u=us), x0[None], n.model, nthreads=1)
+            xs, us = xs + q["dx"], us + q["du"]
+            t1 = time.perf_counter()
+            if i >= 5:
+                cs.append((t1 - t0) * 1e3)
+        res["cpu_baseline"] = {"p50_step_ms": float(np.percentile(cs, 50)), "p99_step_ms": float(np.percentile(cs, 99)),
+                               "cores": 1, "kind": "port",
+                               "sample": f"{steps} closed-loop steps of the same problem: C oracle preparation "
+                                         "(oracle/oracle.c) + structured Riccati IPM (oracle/qp_ipm.c), one thread"}
+    n.ocp.close()
+    return res
 
 
 def bench_c2(device, N, W, no_cpu, rtis=30):
