@@ -102,24 +102,43 @@ constexpr double T0 = QP_T0, L0 = QP_L0, LC = QP_LC, TAU_LO = QP_TAU_LO, TAU_HI 
 __device__ __forceinline__ int tri10(int a, int c) { return a * 10 - a * (a - 1) / 2 + (c - a); }  // a <= c
 __device__ __forceinline__ int tri14(int a, int c) { return a * 14 - a * (a - 1) / 2 + (c - a); }  // a <= c
 
-__device__ __forceinline__ double wsum(double v) {
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-__device__ __forceinline__ double wmax(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
-    return v;
-}
-__device__ __forceinline__ double wmin(double v) {
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o));
-    return v;
-}
 // value of lane l (wave-uniform l) in every lane, via scalar registers
 __device__ __forceinline__ double rdlane(double v, int l) {
     const unsigned long long u = (unsigned long long)__double_as_longlong(v);
     const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)u, l);
     const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(u >> 32), l);
     return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// DPP move of a double (both halves with the same control); rows outside row_mask keep `old`
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp64(double x, double old) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+    const unsigned long long o = (unsigned long long)__double_as_longlong(old);
+    const unsigned lo = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)o, (int)(unsigned)u, CTRL, ROWS, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_update_dpp((int)(unsigned)(o >> 32), (int)(unsigned)(u >> 32), CTRL, ROWS,
+                                                              0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// wave reduction on DPP (quad xor 1, 2, half-row and row mirrors, then row_bcast15 / row_bcast31 into
+// lane 63, read back through a scalar register): no LDS round trips, one fixed order in every lane
+template <class Op>
+__device__ __forceinline__ double wred(double v, double idn, Op op) {
+    v = op(v, dpp64<0xB1, 0xF>(v, idn));   // quad_perm [1, 0, 3, 2]
+    v = op(v, dpp64<0x4E, 0xF>(v, idn));   // quad_perm [2, 3, 0, 1]
+    v = op(v, dpp64<0x141, 0xF>(v, idn));  // row_half_mirror
+    v = op(v, dpp64<0x140, 0xF>(v, idn));  // row_mirror: every lane of a row holds the row's value
+    v = op(v, dpp64<0x142, 0xA>(v, idn));  // row_bcast15: rows 1, 3 += rows 0, 2
+    v = op(v, dpp64<0x143, 0xC>(v, idn));  // row_bcast31: rows 2, 3 += rows 0 + 1
+    return rdlane(v, 63);
+}
+__device__ __forceinline__ double wsum(double v) {
+    return wred(v, 0.0, [](double a, double b) { return a + b; });
+}
+__device__ __forceinline__ double wmax(double v) {
+    return wred(v, -__builtin_inf(), [](double a, double b) { return fmax(a, b); });
+}
+__device__ __forceinline__ double wmin(double v) {
+    return wred(v, __builtin_inf(), [](double a, double b) { return fmin(a, b); });
 }
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c) {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
