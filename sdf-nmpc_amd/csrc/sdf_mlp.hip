@@ -41,6 +41,12 @@ __device__ __forceinline__ f32x16 mfma(float a, float b, f32x16 c) {
 #define SDF_PF 3
 #endif
 
+#ifdef SDF_NO_SYNC  // diagnostic build: the kernel's time without its workgroup barriers (results invalid)
+#define SDF_SYNC() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup")
+#else
+#define SDF_SYNC() __syncthreads()
+#endif
+
 // Row held by accumulator register `reg` of lane half `h` (32x32 f32 MFMA C/D layout, gfx950).
 __device__ __forceinline__ int acc_row(int reg, int h) { return (reg & 3) + 8 * (reg >> 2) + 4 * h; }
 
@@ -214,7 +220,7 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
         posb[tid * 4 + 2] = r < A.rows ? p.z : 0.0f;
         instb[tid] = rr / A.rows_per_inst;
     }
-    __syncthreads();
+    SDF_SYNC();
 
     // ---- positional embedding in the (rb, cb = w) accumulator layout of the d e GEMM (waves 0..2)
     f32x16 gemb[RB][1];  // d e_m / d xb  (cos(xb) | cos(xb + pi/2) | 1 for m < 3 | 0 pad)
@@ -247,27 +253,27 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
                 if (m < KE) Ebuf[row * SE + m] = e;
             }
     }
-    __syncthreads();
+    SDF_SYNC();
 
     // ---- L1: h1 = sin(w0 (W1e e + c1))                 [M x 256], wave cols {w, w+4}
     f32x16 d1[RB][2], acc2[RB][2];
     init_hoisted(acc2, A.c13, 0, instb, w, lane);
     gemm<RB, 2, KE>(acc2, Ebuf, SE, A.wF1, w, lane);
     act_fwd(acc2, d1, Abuf, SA, w0, w, lane);
-    __syncthreads();
+    SDF_SYNC();
     // ---- L2: h2 = sin(w0 (W2 h1 + b2))                  [M x 256]
     f32x16 d2[RB][2];
     init_bias(acc2, A.b2, w, lane);
     gemm<RB, 2, N1>(acc2, Abuf, SA, A.wF2, w, lane);
     act_fwd(acc2, d2, Bbuf, SA, w0, w, lane);
-    __syncthreads();
+    SDF_SYNC();
     // ---- L3: h3 = sin(w0 (W3h h2 + W3e e + c3))        [M x 128], wave col {w}
     f32x16 d3[RB][1], acc1[RB][1];
     init_hoisted(acc1, A.c13, N1, instb, w, lane);
     gemm<RB, 1, N2>(acc1, Bbuf, SA, A.wF3h, w, lane);
     gemm<RB, 1, KE>(acc1, Ebuf, SE, A.wF3e, w, lane);
     act_fwd(acc1, d3, Abuf, SA, w0, w, lane);
-    __syncthreads();
+    SDF_SYNC();
     // ---- L4: h4 = sin(w0 (W4 h3 + b4))                  [M x 64], waves 2,3 (col block w-2)
     //      delta4 = (W5 * cos(t4)) * w0 -> Bbuf, h4 -> Ebuf
     if (w >= 2) {
@@ -286,7 +292,7 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
                 Bbuf[row * SA + cb4 * 32 + col] = (w5 * co) * w0;
             }
     }
-    __syncthreads();
+    SDF_SYNC();
     // ---- df = W5 h4 + b5 (one thread per row)
     float df = 0.0f;
     if (tid < M) {
@@ -298,7 +304,7 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
     zero(acc1);
     gemm<RB, 1, N4>(acc1, Bbuf, SA, A.wB4, w, lane);
     act_bwd(acc1, d3, Abuf, SA, w0, w, lane);
-    __syncthreads();
+    SDF_SYNC();
     // ---- b3: delta2 = ((delta3 W3h) * cos t2) * w0     -> Bbuf   [M x 256]
     //          d e  (partial) = delta3 W3e                (regs, waves 0..2)
     //          d z  (partial) = delta3 W3z                (regs, optional)
@@ -320,12 +326,12 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
         zero(dz);
         gemm<RB, 1, N3>(dz, Abuf, SA, A.wB3z, w, lane);
     }
-    __syncthreads();
+    SDF_SYNC();
     // ---- b2: delta1 = ((delta2 W2) * cos t1) * w0      -> Abuf   [M x 256]
     zero(acc2);
     gemm<RB, 2, N2>(acc2, Bbuf, SA, A.wB2, w, lane);
     act_bwd(acc2, d1, Abuf, SA, w0, w, lane);
-    __syncthreads();
+    SDF_SYNC();
     // ---- b1: d e += delta1 W1e (same K-split) ; d z += delta1 W1z
     if (w < 3) gemm<RB, 1, N1, 4, 0, 3 * N1 / 32>(de, Abuf, SA, A.wB1e, w, lane);
     else gemm<RB, 3, N1, 1, 3 * N1 / 32, N1 / 8>(de3, Abuf, SA, A.wB1e, 0, lane);
@@ -340,7 +346,7 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
             }
     }
     // ---- wave 3 hands its K-slice of d e to the owners of the column blocks (through Abuf)
-    __syncthreads();  // everyone is done reading delta1 in Abuf
+    SDF_SYNC();  // everyone is done reading delta1 in Abuf
     if (w == 3) {
 #pragma unroll
         for (int c = 0; c < 3; ++c)
@@ -349,7 +355,7 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
 #pragma unroll
                 for (int i = 0; i < 16; ++i) Abuf[(rb * 32 + acc_row(i, hh)) * SA + c * 32 + col] = de3[rb][c][i];
     }
-    __syncthreads();
+    SDF_SYNC();
     if (w < 3) {
 #pragma unroll
         for (int rb = 0; rb < RB; ++rb)
@@ -384,14 +390,14 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
                 red[(row * 3 + 2) * NE + m] = v2;
             }
     }
-    __syncthreads();
+    SDF_SYNC();
     if (tid < 3 * M) {
         const float* src = red + tid * NE;
         float s = 0.0f;
         for (int m = 0; m < NE; ++m) s += src[m];
         posb[(tid / 3) * 4 + 1 + tid % 3] = s;
     }
-    __syncthreads();
+    SDF_SYNC();
     if (tid < M && row0 + tid < A.rows) {
         const int r = row0 + tid;
         const float g0 = posb[tid * 4 + 1], g1 = posb[tid * 4 + 2], g2 = posb[tid * 4 + 3];
