@@ -76,11 +76,19 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    # SDFNMPC_DIST_BACKEND=gloo rehearses the multi-rank path with several ranks on one GPU (the 1-GPU
+    # test box); the product run is one rank per GPU over RCCL ("nccl")
+    backend = os.environ.get("SDFNMPC_DIST_BACKEND", "nccl")
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     import sdf_nmpc_amd  # noqa: F401
     from sdf_nmpc_amd import _lib, shard, synth, weights as W
@@ -455,11 +463,17 @@ def main_c5(args):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}: launch N>1 with torch.distributed.run")
+    backend = os.environ.get("SDFNMPC_DIST_BACKEND", "nccl")  # gloo: rehearsal with ranks sharing a GPU
+    if backend == "gloo":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     from sdf_nmpc_amd import _lib, shard, synth, vae as V, weights as W
     from sdf_nmpc_amd.config import Config
     from sdf_nmpc_amd.model import Quad

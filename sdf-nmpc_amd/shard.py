@@ -55,6 +55,8 @@ def broadcast_blob(blob, device, src=0):
     import torch
     import torch.distributed as dist
     rank = dist.get_rank()
+    if dist.get_backend() == "gloo":  # gloo broadcasts host tensors
+        device = "cpu"
     n = torch.tensor([len(blob) if rank == src else 0], dtype=torch.int64, device=device)
     dist.broadcast(n, src)
     buf = torch.empty(int(n.item()), dtype=torch.uint8, device=device)
@@ -87,6 +89,8 @@ def gather_rows(t, total: int, dst=0):
 def max_over_ranks(seconds: float, device) -> float:
     import torch
     import torch.distributed as dist
+    if dist.get_backend() == "gloo":  # gloo reduces host tensors
+        device = "cpu"
     t = torch.tensor([seconds], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
