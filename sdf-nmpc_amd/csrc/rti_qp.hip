@@ -302,68 +302,59 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
     const int b = node / N1, k = node - b * N1;
     double* Rk = A.work + (size_t)b * qp_work_doubles(N) + (size_t)k * REC;
     const double* Jh = A.Jh + ((size_t)b * N1 + k) * 30;
-    __shared__ double Js_[PACK_NODES][14 * 12], Ws_[PACK_NODES][12], rs_[PACK_NODES][12];  // J_y [14][ny], s_k W, r
-    double* Js = Js_[wv];
-    double* Ws = Ws_[wv];
-    double* rs = rs_[wv];
     const int ny = A.ny;
     if (k < N) {
+        // H = s_k J^T W J + lm_k I and g = s_k J^T W r in one f64 MFMA chain over the residuals (K = ny <= 12):
+        // A lane (g, c) = J(c, k) s_k W_k, B lane (g, c) = J(c, k) for c < 14 and r_k for c = 14, k = 4 st + g;
+        // D lane (g, c), register q: [H | g][g + 4 q][c]
         const size_t bk = (size_t)b * N + k;
         const double sk = A.cost_scaling ? A.dt[k] : 1.0;
         const double lmk = A.lm_scaling ? A.lm * A.dt[k] : A.lm;  // acados: Ts_k lm for k < N, lm at N
-        for (int e = lane; e < 154; e += 64) Js[(e / 11) * ny + e % 11] = A.Jy[bk * 154 + e];
-        if (lane < ny) {
-            const int i = lane;
-            double y;
-            if (i < 11) {
-                y = A.y[bk * 11 + i];
-            } else {  // sdf cost residual (gen_model.py:65-66): (1 - s/2)^4 of the flagged SDF value s = h[2]
-                const double t = 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2];
-                y = t * t * t * t;
+        const int g = lane >> 4, c = lane & 15;
+        const double ts = 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2];  // sdf cost (gen_model.py:65-66)
+        d4 D = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int st = 0; st < 3; ++st) {
+            const int kk = 4 * st + g;
+            double jv = 0.0, wk = 0.0, rv = 0.0;
+            if (kk < ny) {
+                wk = sk * A.W[bk * ny + kk];
+                const double y = kk < 11 ? A.y[bk * 11 + kk] : ts * ts * ts * ts;
+                rv = y - A.yref[bk * ny + kk];
+                if (c < 14)  // d y_kk / d (x, u)_c; the sdf cost row: -2 (1 - s/2)^3 J_h[2] on the state part
+                    jv = kk < 11 ? A.Jy[bk * 154 + c * 11 + kk] : (c < NX ? -2.0 * ts * ts * ts * Jh[c * 3 + 2] : 0.0);
             }
-            Ws[i] = sk * A.W[bk * ny + i];
-            rs[i] = y - A.yref[bk * ny + i];
+            D = mfma(jv * wk, c == 14 ? rv : jv, D);
         }
-        if (ny == 12 && lane < 14) {  // d/dw of the sdf cost: -2 (1 - s/2)^3 J_h[2] on the state part
-            const int a = lane;
-            const double t = 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2];
-            Js[a * 12 + 11] = a < 10 ? -2.0 * t * t * t * Jh[a * 3 + 2] : 0.0;
-        }
-        wave_sync();
         const double* AB = A.AB + bk * 140;
         const double* xn = A.xn + bk * 10;
         const double* xb1 = A.x + ((size_t)b * N1 + k + 1) * 10;
-        // e = lane, lane + 64: [A B]; lane + 128: AB tail | c | g | C^T; lane + 192, + 256: C^T tail | H | 0
+        // e = lane, lane + 64: [A B]; lane + 128: AB tail | c | (g below) | C^T; lane + 192, + 256: C^T tail | 0
         Rk[lane] = AB[lane];
         Rk[64 + lane] = AB[64 + lane];
         {
             const int e = 128 + lane;
-            double v;
-            if (e < R_C) {
-                v = AB[e];
-            } else if (e < R_G) {
-                v = xn[e - R_C] - xb1[e - R_C];
-            } else if (e < R_CT) {
-                const int a = e - R_G;
-                v = 0.0;
-                for (int i = 0; i < ny; ++i) v += Js[a * ny + i] * Ws[i] * rs[i];
-            } else {
+            if (e < R_C) Rk[e] = AB[e];
+            else if (e < R_G) Rk[e] = xn[e - R_C] - xb1[e - R_C];
+            else if (e >= R_CT) {
                 const int q = e - R_CT, j = q / 10;
-                v = Jh[(q - 10 * j) * 3 + j];
+                Rk[e] = Jh[(q - 10 * j) * 3 + j];
             }
-            Rk[e] = v;
         }
         for (int e = 192 + lane; e < REC; e += 64) {
-            double v = 0.0;
             if (e < R_H) {
                 const int q = e - R_CT, j = q / 10;
-                v = Jh[(q - 10 * j) * 3 + j];
-            } else if (e < R_H + 105) {
-                const int a = c_tri.a14[e - R_H], c = c_tri.c14[e - R_H];
-                for (int i = 0; i < ny; ++i) v += Js[a * ny + i] * Ws[i] * Js[c * ny + i];
-                v += (a == c ? lmk : 0.0);
+                Rk[e] = Jh[(q - 10 * j) * 3 + j];
+            } else if (e >= R_H + 105) {
+                Rk[e] = 0.0;
             }
-            Rk[e] = v;
+        }
+        // H (upper, + lm_k on the diagonal) and g from the accumulator lanes
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int a = g + 4 * q;
+            if (a < 14 && c < 14 && a <= c) Rk[R_H + tri14(a, c)] = D[q] + (a == c ? lmk : 0.0);
+            else if (a < 14 && c == 14) Rk[R_G + a] = D[q];
         }
     } else {
         const double* J = A.JyN + (size_t)b * 40;  // [10][4]
