@@ -394,6 +394,11 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
 #ifndef FSTAMP
 #define FSTAMP(i, v)
 #endif
+#ifdef QP_RSTAMPS  // row phases split: rows_pred | terms(1), rows_update | terms(0)
+#define RSTAMP(i) STAMP(i)
+#else
+#define RSTAMP(i)
+#endif
 
 __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     extern __shared__ __align__(16) double lds_q[];
@@ -905,15 +910,19 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         // the stop test needs, which keeps lambda / t -- and the Riccati data -- bounded
         return fmax(sig * mu, 1e-2 * A.tol);
     };
-    // corrector rows: step length, update of (t, lambda, du, dx), mu and the primal residual
-    auto rows_update = [&](double sigmu) {
+    // corrector rows: step length, update of (t, lambda, du, dx), mu and the primal residual.
+    // GPL > 0: every lane owns at most GPL soft groups (3 (N+1) <= 64 GPL); their directions (dt, dl) --
+    // the expensive part, two group evaluations with six reciprocals each -- are computed once, kept in
+    // registers between the step-length pass and the update pass.  GPL == 0: the generic loops recompute.
+    auto rows_update_t = [&](auto GPLc, double sigmu) {
+        constexpr int GPL = decltype(GPLc)::value;
+        constexpr int GA = GPL > 0 ? GPL : 1;
         double amax = 1.0;
         auto bound = [&](double t, double l, double dt, double dl) {
             if (dt < 0.0) amax = fmin(amax, -t * rcp_nr(dt));
             if (dl < 0.0) amax = fmin(amax, -l * rcp_nr(dl));
         };
         // direction of row r: dt = val(z_c) - t, dl = -sigma dt - l - (dt_a dl_a - sigma mu) / t
-        amax = 1.0;
         for (int r = lane; r < 8 * N; r += 64) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
             const double t = s.t[r], l = s.lam[r];
@@ -922,7 +931,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const double it = rcp_nr(t), sg = l * it;
             bound(t, l, dt, -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it);
         }
-        for (int e = lane; e < N1 * NS; e += 64) {
+        auto soft_dir = [&](int e, double* dt, double* dl) {
             const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
             const Grp ga = group(k, j, 0, 0.0), gc = group(k, j, 1, sigmu);
             double va[4], vc[4];
@@ -931,9 +940,30 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q];
-                const double dta = va[q] - t, dt = vc[q] - t;
+                const double dta = va[q] - t;
+                dt[q] = vc[q] - t;
                 const double it = rcp_nr(t), sg = l * it;
-            bound(t, l, dt, -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it);
+                dl[q] = -sg * dt[q] - l - (dta * (-sg * dta - l) - sigmu) * it;
+            }
+        };
+        double sdt[GA][4], sdl[GA][4];
+        if constexpr (GPL > 0) {
+#pragma unroll
+            for (int gi = 0; gi < GPL; ++gi) {
+                const int e = lane + 64 * gi;
+                if (e < N1 * NS) {
+                    soft_dir(e, sdt[gi], sdl[gi]);
+                    const int r0 = 8 * N + 4 * e;
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) bound(s.t[r0 + q], s.lam[r0 + q], sdt[gi][q], sdl[gi][q]);
+                }
+            }
+        } else {
+            for (int e = lane; e < N1 * NS; e += 64) {
+                soft_dir(e, sdt[0], sdl[0]);
+                const int r0 = 8 * N + 4 * e;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) bound(s.t[r0 + q], s.lam[r0 + q], sdt[0][q], sdl[0][q]);
             }
         }
         const double tau = fmin(TAU_HI, fmax(TAU_LO, 1.0 - mu));
@@ -953,21 +983,13 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             s.t[r] = tn;
             s.lam[r] = ln;
         }
-        for (int e = lane; e < N1 * NS; e += 64) {
-            const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
-            const Grp ga = group(k, j, 0, 0.0), gc = group(k, j, 1, sigmu);
-            double va[4], vc[4];
-            soft_vals(ga, k, j, s.cxa[e], va);
-            soft_vals(gc, k, j, s.cxc[e], vc);
+        auto soft_upd = [&](int e, const double* dt, const double* dl) {
+            const int r0 = 8 * N + 4 * e;
             double tn[4], ln[4];
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double t = s.t[r0 + q], l = s.lam[r0 + q];
-                const double dta = va[q] - t, dt = vc[q] - t;
-                const double it = rcp_nr(t), sg = l * it;
-            const double dl = -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it;
-                tn[q] = t + al * dt;
-                ln[q] = l + al * dl;
+                tn[q] = s.t[r0 + q] + al * dt[q];
+                ln[q] = s.lam[r0 + q] + al * dl[q];
                 lmu += tn[q] * ln[q];
                 lcm = fmax(lcm, tn[q] * ln[q]);
             }
@@ -976,6 +998,19 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
                 s.t[r0 + q] = tn[q];
                 s.lam[r0 + q] = ln[q];
             }
+        };
+        if constexpr (GPL > 0) {
+#pragma unroll
+            for (int gi = 0; gi < GPL; ++gi) {
+                const int e = lane + 64 * gi;
+                if (e < N1 * NS) soft_upd(e, sdt[gi], sdl[gi]);
+            }
+        } else {
+            for (int e = lane; e < N1 * NS; e += 64) {
+                double dt[4], dl[4];
+                soft_dir(e, dt, dl);
+                soft_upd(e, dt, dl);
+            }
         }
         for (int e = lane; e < N1 * NX; e += 64) s.dx[e] += al * (s.dxc[e] - s.dx[e]);
         for (int e = lane; e < N * NU; e += 64) s.du[e] += al * (s.duc[e] - s.du[e]);
@@ -983,6 +1018,13 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         cm = wmax(lcm);
         rp *= (1.0 - al);
         gap *= (1.0 - al);
+    };
+    const int gpl = (N1 * NS + 63) / 64;
+    auto rows_update = [&](double sigmu) {
+        if (gpl == 1) rows_update_t(IC<1>{}, sigmu);
+        else if (gpl == 2) rows_update_t(IC<2>{}, sigmu);
+        else if (gpl == 3) rows_update_t(IC<3>{}, sigmu);
+        else rows_update_t(IC<0>{}, sigmu);
     };
 
     // ------------------------------------------------------------ IPM: sweeps over the record stream
@@ -1063,6 +1105,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         sweep(IC<2>{});
         STAMP(3);
         const double sigmu = rows_pred();
+        RSTAMP(8);
         terms(1, sigmu);
         STAMP(4);
         sweep(IC<3>{});
@@ -1072,6 +1115,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         sweep(IC<4>{});
         STAMP(3);
         rows_update(sigmu);
+        RSTAMP(9);
         wave_sync();
         STAMP(6);
         ++it;

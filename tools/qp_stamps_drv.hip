@@ -23,7 +23,7 @@ int main(int argc, char** argv) {
   std::vector<double> st(B*16); hipMemcpy(st.data(),q.stamps,8*B*16,hipMemcpyDeviceToHost);
   std::vector<int> it(B); hipMemcpy(it.data(),q.iters,4*B,hipMemcpyDeviceToHost);
   double tot[16]={0}; int mx=0; for(int i=0;i<B;++i){for(int j=0;j<16;++j) tot[j]+=st[i*16+j]; if(it[i]>mx)mx=it[i];}
-  const char* ph[]={"setup","sweep0","bwd-factor","fwd(x2)","rows-pred+terms","bwd-corr","rows-upd+terms","c:pos+entry","f:entry+W","f:M_u","f:chol+kg","f:jos->Pa","f:stores","c:reads","c:chain","c:tail"};
+  const char* ph[]={"setup","sweep0","bwd-factor","fwd(x2)","rows-pred+terms","bwd-corr","rows-upd+terms","c:pos+entry","8:f-entry+W|r-pred","9:f-M_u|r-update","f:chol+kg","f:jos->Pa","f:stores","c:reads","c:chain","c:tail"};
   double mi=0; for(int i=0;i<B;++i) mi+=it[i]; std::vector<int> stt(B); hipMemcpy(stt.data(),q.status,4*B,hipMemcpyDeviceToHost); int nc=0; for(int i=0;i<B;++i) nc+=stt[i]!=0;
   printf("kernel %.3f ms, max iters %d, mean %.2f, not converged %d\n", ms, mx, mi/B, nc); double s=0; for(int j=0;j<16;++j) s+=tot[j];
   for(int j=0;j<16;++j) printf("  %-14s %8.0f cycles/instance (%.1f%%)\n", ph[j], tot[j]/B, 100*tot[j]/s);
