@@ -862,7 +862,10 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // gap = prod (1 - alpha): the stationarity residual of the starting point decays by exactly this
     // factor (every Newton system is solved for the new iterate), the stand-in for HPIPM's res_g test
     double mu = 0.0, cm = 0.0, rp = 0.0, gap = 1.0;
-    auto rows_pred = [&]() -> double {
+    // (GPL > 0: the soft rows' affine directions are computed once and kept in registers for both passes)
+    auto rows_pred_t = [&](auto GPLc) -> double {
+        constexpr int GPL = decltype(GPLc)::value;
+        constexpr int GA = GPL > 0 ? GPL : 1;
         double amax = 1.0;
         auto bound = [&](double t, double l, double dt, double dl) {
             if (dt < 0.0) amax = fmin(amax, -t * rcp_nr(dt));
@@ -874,15 +877,35 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const double dt = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
             bound(t, l, dt, -(l * rcp_nr(t)) * dt - l);
         }
-        for (int e = lane; e < N1 * NS; e += 64) {
-            const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
+        // affine direction of the four rows of soft group e: dt = val(z_a) - t, dl = -(lambda / t) dt - lambda
+        auto soft_dir = [&](int e, double* dt, double* dl) {
+            const int k = e / NS, j = e % NS, r0 = 8 * N + 4 * e;
             const Grp g = group(k, j, 0, 0.0);
             double v[4];
             soft_vals(g, k, j, s.cxa[e], v);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double t = s.t[r0 + q], l = s.lam[r0 + q], dt = v[q] - t;
-                bound(t, l, dt, -(l * rcp_nr(t)) * dt - l);
+                const double t = s.t[r0 + q], l = s.lam[r0 + q];
+                dt[q] = v[q] - t;
+                dl[q] = -(l * rcp_nr(t)) * dt[q] - l;
+            }
+        };
+        double sdt[GA][4], sdl[GA][4];
+        if constexpr (GPL > 0) {
+#pragma unroll
+            for (int gi = 0; gi < GPL; ++gi) {
+                const int e = lane + 64 * gi;
+                if (e < N1 * NS) {
+                    soft_dir(e, sdt[gi], sdl[gi]);
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) bound(s.t[8 * N + 4 * e + q], s.lam[8 * N + 4 * e + q], sdt[gi][q], sdl[gi][q]);
+                }
+            }
+        } else {
+            for (int e = lane; e < N1 * NS; e += 64) {
+                soft_dir(e, sdt[0], sdl[0]);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) bound(s.t[8 * N + 4 * e + q], s.lam[8 * N + 4 * e + q], sdt[0][q], sdl[0][q]);
             }
         }
         const double aa = wmin(amax);
@@ -893,15 +916,24 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             const double dt = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
             lmua += (t + aa * dt) * (l + aa * (-(l * rcp_nr(t)) * dt - l));
         }
-        for (int e = lane; e < N1 * NS; e += 64) {
-            const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
-            const Grp g = group(k, j, 0, 0.0);
-            double v[4];
-            soft_vals(g, k, j, s.cxa[e], v);
+        auto soft_mu = [&](int e, const double* dt, const double* dl) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double t = s.t[r0 + q], l = s.lam[r0 + q], dt = v[q] - t;
-                lmua += (t + aa * dt) * (l + aa * (-(l * rcp_nr(t)) * dt - l));
+                const double t = s.t[8 * N + 4 * e + q], l = s.lam[8 * N + 4 * e + q];
+                lmua += (t + aa * dt[q]) * (l + aa * dl[q]);
+            }
+        };
+        if constexpr (GPL > 0) {
+#pragma unroll
+            for (int gi = 0; gi < GPL; ++gi) {
+                const int e = lane + 64 * gi;
+                if (e < N1 * NS) soft_mu(e, sdt[gi], sdl[gi]);
+            }
+        } else {
+            for (int e = lane; e < N1 * NS; e += 64) {
+                double dt[4], dl[4];
+                soft_dir(e, dt, dl);
+                soft_mu(e, dt, dl);
             }
         }
         const double mua = wsum(lmua) / m;
@@ -909,6 +941,13 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         // centring target floored at 1e-2 tol (HPIPM's tau_min): no row is pushed below the complementarity
         // the stop test needs, which keeps lambda / t -- and the Riccati data -- bounded
         return fmax(sig * mu, 1e-2 * A.tol);
+    };
+    auto rows_pred = [&]() -> double {
+        const int gp = (N1 * NS + 63) / 64;
+        if (gp == 1) return rows_pred_t(IC<1>{});
+        if (gp == 2) return rows_pred_t(IC<2>{});
+        if (gp == 3) return rows_pred_t(IC<3>{});
+        return rows_pred_t(IC<0>{});
     };
     // corrector rows: step length, update of (t, lambda, du, dx), mu and the primal residual.
     // GPL > 0: every lane owns at most GPL soft groups (3 (N+1) <= 64 GPL); their directions (dt, dl) --
