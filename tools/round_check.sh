@@ -26,5 +26,8 @@ timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format cs
     python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 --prep-steps 2 --no-b1 --no-c2 --no-c1 > /dev/null 2> $O/fetch.err
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o p -- \
     python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 --prep-steps 2 --no-b1 --no-c2 --no-c1 > /dev/null 2> $O/write.err
+# the stamps driver is rebuilt from the current rti_qp.hip, so the stamps always describe this tree's kernel
+(cd $R && timeout -k 10 300 hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DQP_STAMPS -I sdf-nmpc_amd/csrc \
+    tools/qp_stamps_drv.hip sdf-nmpc_amd/csrc/rti_qp.hip -o tools/_qp_stamps_drv)
 timeout -k 10 200 python3 $R/tools/qp_stamps.py > $O/qp_stamps.txt 2>&1
 echo done
