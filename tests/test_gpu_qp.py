@@ -46,7 +46,7 @@ def solve(gpu_ctx, cfg, t, B, N, sdf_cost=False, **kw):
     return model
 
 
-@pytest.mark.parametrize("B,N,seed", [(3, 20, 1), (2, 40, 2), (2, 60, 5)])
+@pytest.mark.parametrize("B,N,seed", [(3, 20, 1), (2, 40, 2), (2, 60, 5), (2, 80, 6)])
 def test_qp_matches_exact_solution(gpu_ctx, oracle_lib, cfg, B, N, seed):
     import qp_oracle
     prob, x0, t = setup(gpu_ctx, cfg, B, N, seed)
@@ -149,7 +149,7 @@ def _agree(prob, x0, lin, model, got, ref, atol=ORC_ATOL):
             assert np.abs(E @ v - e).max() < 1e-9 and (G @ v + dd).min() > -1e-8
 
 
-@pytest.mark.parametrize("B,N,seed,noise", [(64, 40, 3, 0.05), (32, 20, 9, 0.5), (32, 60, 4, 0.2)])
+@pytest.mark.parametrize("B,N,seed,noise", [(64, 40, 3, 0.05), (32, 20, 9, 0.5), (32, 60, 4, 0.2), (16, 80, 7, 0.2)])
 def test_qp_matches_riccati_oracle_batch(gpu_ctx, oracle_lib, cfg, B, N, seed, noise):
     """A wider batch against the structured C IPM (oracle/qp_ipm.c), itself pinned to the exact solution."""
     prob, x0, t = setup(gpu_ctx, cfg, B, N, seed, x0_noise=noise)
