@@ -136,14 +136,14 @@ def main():
 
     x_init, u_init = bufs["x"].clone(), bufs["u"].clone()
 
-    def prep():  # preparation phase only
-        _lib.linearize(ctx, net, model, B, N, np_, bufs)
+    def prep():  # preparation phase only (linearisation + the QP's stage records)
+        _lib.rti_prepare(ctx, net, model, qopts, B, N, np_, bufs)
 
     def step():  # one SQP-RTI solve from the initial iterate: preparation, feedback (QP), update + u_0
         bufs["x"].copy_(x_init)
         bufs["u"].copy_(u_init)
-        _lib.linearize(ctx, net, model, B, N, np_, bufs)
-        _lib.qp_solve(ctx, qopts, B, N, bufs)
+        _lib.rti_prepare(ctx, net, model, qopts, B, N, np_, bufs)  # preparation: linearisation + QP records
+        _lib.qp_feedback(ctx, qopts, B, N, bufs)                     # feedback: the IPM
         _lib.rti_apply(ctx, B, N, bufs["x"], bufs["u"], bufs["dx"], bufs["du"], u0)
 
     def barrier():
@@ -186,7 +186,7 @@ def main():
     reps = max(5, min(args.steps, 20))
     for _ in range(reps):
         step()
-    names = ("sdf_hoist", "sdf_mlp", "linearize", "rti_qp_pack", "rti_qp", "rti_apply")
+    names = ("sdf_hoist", "sdf_mlp", "linearize", "rti_qp_pack", "rti_qp_pack_sdf", "rti_qp", "rti_apply")
     kst = {k: ctx.kernel_stats(k) for k in names}
     ctx.enable_timing(False)
     kms = {k: (v[0] / v[1] if v[1] else None) for k, v in kst.items()}
@@ -217,8 +217,8 @@ def main():
         def step1():
             b1["x"].copy_(x1)
             b1["u"].copy_(u1_)
-            _lib.linearize(ctx, net, model, 1, N, np_, b1)
-            _lib.qp_solve(ctx, qopts, 1, N, b1)
+            _lib.rti_prepare(ctx, net, model, qopts, 1, N, np_, b1)
+            _lib.qp_feedback(ctx, qopts, 1, N, b1)
             _lib.rti_apply(ctx, 1, N, b1["x"], b1["u"], b1["dx"], b1["du"], u01)
         for _ in range(5):
             step1()
@@ -529,8 +529,8 @@ def main_c5(args):
         _lib.pack_refs(ctx, ropts, B, N, np_, 11, rargs, L=128)
         bufs["x"].copy_(x_init)
         bufs["u"].copy_(u_init)
-        _lib.linearize(ctx, net, model, B, N, np_, bufs)
-        _lib.qp_solve(ctx, qopts, B, N, bufs)
+        _lib.rti_prepare(ctx, net, model, qopts, B, N, np_, bufs)  # preparation: linearisation + QP records
+        _lib.qp_feedback(ctx, qopts, B, N, bufs)                     # feedback: the IPM
         _lib.rti_apply(ctx, B, N, bufs["x"], bufs["u"], bufs["dx"], bufs["du"], u0)
 
     def timed(fn, k):
@@ -561,7 +561,7 @@ def main_c5(args):
     for _ in range(reps):
         step()
     names = ("vae_pre", "vae_stem", "vae_conv", "vae_head", "sdf_wide_hoist", "sdf_wide_emb", "sdf_wide_gemm",
-             "sdf_wide_final", "linearize", "ref_pack", "rti_qp_pack", "rti_qp", "rti_apply")
+             "sdf_wide_final", "linearize", "ref_pack", "rti_qp_pack", "rti_qp_pack_sdf", "rti_qp", "rti_apply")
     kms = {k: ctx.kernel_stats(k)[0] / reps for k in names}  # ms per step (all launches of that name)
     ctx.enable_timing(False)
     spec = V.DEFAULT_ENCODER

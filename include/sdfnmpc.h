@@ -217,6 +217,16 @@ int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_qu
 
 /* ---- batched QP (feedback phase) and the RTI step ---- */
 int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* opts, const sdfnmpc_qp_args* args);
+/* The same SQP-RTI step split the way acados splits it (rti_phase 1 / 2, ocp.py:110): everything that
+ * does not depend on x0 -- the linearisation and the QP's stage records (H, g, dynamics, constraint
+ * rows) -- in the preparation phase, the IPM alone in the feedback phase.  sdfnmpc_rti_prepare =
+ * sdfnmpc_linearize + the record pack (qp_args must name lin_args' iterate and outputs; the pack runs
+ * beside the SDF kernel); sdfnmpc_qp_feedback = the IPM on those records, once per preparation
+ * (SDFNMPC_E_ARG without a matching sdfnmpc_rti_prepare).  Results are bitwise those of
+ * sdfnmpc_linearize + sdfnmpc_qp_solve. */
+int sdfnmpc_rti_prepare(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* model,
+                        const sdfnmpc_lin_args* lin_args, const sdfnmpc_qp_opts* opts, const sdfnmpc_qp_args* qp_args);
+int sdfnmpc_qp_feedback(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* opts, const sdfnmpc_qp_args* args);
 /* x[B][N+1][10] += dx, u[B][N][4] += du, u0[B][4] = u[:, 0] (u0 may be NULL).  status [B] (may be NULL):
  * instances with status >= 2 (QP failure) keep x and u; their u0 is the unchanged u[:, 0]. */
 int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, const double* dx, const double* du,

@@ -26,7 +26,8 @@ SYMBOLS = [
     "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
-    "sdfnmpc_linearize", "sdfnmpc_shooting_grid", "sdfnmpc_qp_solve", "sdfnmpc_rti_apply", "sdfnmpc_pack_refs",
+    "sdfnmpc_linearize", "sdfnmpc_shooting_grid", "sdfnmpc_qp_solve", "sdfnmpc_rti_prepare", "sdfnmpc_qp_feedback",
+    "sdfnmpc_rti_apply", "sdfnmpc_pack_refs",
     "sdfnmpc_vae_load", "sdfnmpc_vae_free", "sdfnmpc_vae_size_latent", "sdfnmpc_vae_encode",
     "sdfnmpc_ctx_device", "sdfnmpc_dev_alloc", "sdfnmpc_dev_free", "sdfnmpc_memcpy",
     "sdfnmpc_solver_create", "sdfnmpc_solver_destroy", "sdfnmpc_solver_field", "sdfnmpc_solver_upload",
@@ -134,6 +135,8 @@ def load():
         "sdfnmpc_linearize": (i, [vp, vp, P(QuadModelC), P(LinArgsC)]),
         "sdfnmpc_shooting_grid": (i, [i, d, i, i, d, P(d), P(d)]),
         "sdfnmpc_qp_solve": (i, [vp, P(QpOptsC), P(QpArgsC)]),
+        "sdfnmpc_rti_prepare": (i, [vp, vp, P(QuadModelC), P(LinArgsC), P(QpOptsC), P(QpArgsC)]),
+        "sdfnmpc_qp_feedback": (i, [vp, P(QpOptsC), P(QpArgsC)]),
         "sdfnmpc_rti_apply": (i, [vp, i, i, vp, vp, vp, vp, vp, vp]),
         "sdfnmpc_pack_refs": (i, [vp, P(RefOptsC), P(RefArgsC)]),
         "sdfnmpc_vae_load": (i, [vp, vp, sz, P(vp)]),
@@ -331,6 +334,23 @@ def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
     """Enqueue the batched feedback-phase QP.  bufs: device tensors named as sdfnmpc_qp_args."""
     a = QpArgsC(B, N, *[_ptr(bufs.get(k)) for k in QP_IN + QP_OUT])
     _check(load().sdfnmpc_qp_solve(ctx.h, C.byref(opts), C.byref(a)))
+
+
+def rti_prepare(ctx: Context, net: Net, model: QuadModelC, opts: QpOptsC, B: int, N: int, np_: int, bufs: dict,
+                latent_mode=0):
+    """Enqueue the RTI preparation phase acados-style: linearisation + the QP's stage records (everything
+    but x0).  bufs: device tensors named as sdfnmpc_lin_args and sdfnmpc_qp_args."""
+    la = LinArgsC(B, N, np_, latent_mode, *[_ptr(bufs.get(k)) for k in
+                                            ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh",
+                                             "sdf")])
+    qa = QpArgsC(B, N, *[_ptr(bufs.get(k)) for k in QP_IN + QP_OUT])
+    _check(load().sdfnmpc_rti_prepare(ctx.h, net.h, C.byref(model), C.byref(la), C.byref(opts), C.byref(qa)))
+
+
+def qp_feedback(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
+    """Enqueue the RTI feedback phase: the IPM on the records of the last rti_prepare."""
+    a = QpArgsC(B, N, *[_ptr(bufs.get(k)) for k in QP_IN + QP_OUT])
+    _check(load().sdfnmpc_qp_feedback(ctx.h, C.byref(opts), C.byref(a)))
 
 
 def rti_apply(ctx: Context, B: int, N: int, x, u, dx, du, u0=None, status=None):

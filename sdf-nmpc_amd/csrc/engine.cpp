@@ -88,6 +88,13 @@ struct sdfnmpc_ctx {
     uint64_t h_net = 0;  // uid of the network the cached hoist belongs to
     std::map<std::string, KStat> stats;
     std::mutex mu;  // serialises the host-pointer path (CasADi externals may be called concurrently)
+    // stage records packed by sdfnmpc_rti_prepare, consumed by the next sdfnmpc_qp_feedback
+    struct {
+        bool valid = false;
+        int B = 0, N = 0;
+        const double* xn = nullptr;  // the lin outputs they were packed from
+        const void* work = nullptr;
+    } prep;
 };
 
 struct ScopedDevice {
@@ -919,8 +926,12 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
 
 // ------------------------------------------------------------------------------------------------
 // batched preparation phase
-extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
-                                 const sdfnmpc_lin_args* a) {
+// pk != NULL (sdfnmpc_rti_prepare): the QP stage records are packed in the same phase.  With ny == 11
+// the pack runs after the linearisation on the aux stream, beside the SDF kernel, and only the sdf row
+// of C^T waits for the join; with the sdf cost (ny == 12) H and g depend on h[2], so the whole pack
+// follows the join.
+static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
+                    const sdfnmpc_lin_args* a, const QpArgs* pk) {
     if (!ctx || !net || !mdl || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
     if (a->B < 0 || a->N < 1 || a->np < 17 + net->host.L || (a->latent_mode != 0 && a->latent_mode != 1))
         return fail(SDFNMPC_E_ARG, "bad B/N/np/latent_mode");
@@ -949,12 +960,26 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
         la.m.fov_off[i] = mdl->B_R_C[0 * 3 + i] * mdl->B_p_C[0] + mdl->B_R_C[1 * 3 + i] * mdl->B_p_C[1] +
                           mdl->B_R_C[2 * 3 + i] * mdl->B_p_C[2] + (i == 0 ? mdl->fov_const_offset : 0.0);
     la.m.max_df = net->host.max_df;
+    QpArgs pa{};
+    const bool split = pk && pk->ny == 11 && !ctx->serial_prep;  // pack beside the SDF kernel
+    if (pk) {
+        pa = *pk;
+        pa.pack_part = split ? 1 : 0;
+    }
     auto fork_lin = [&]() -> int {
         if (ctx->serial_prep) return SDFNMPC_OK;
         HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
         HIPCHK(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
         HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->aux); }, ctx->aux));
+        if (split) HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(pa, ctx->aux); }, ctx->aux));
         HIPCHK(hipEventRecord(ctx->ev_join, ctx->aux));
+        return SDFNMPC_OK;
+    };
+    // after the join: the rest of the pack on the main stream
+    auto finish_pack = [&]() -> int {
+        if (!pk) return SDFNMPC_OK;
+        if (split) HIPCHK(timed(ctx, "rti_qp_pack_sdf", [&] { return launch_rti_qp_pack_sdf(pa, ctx->stream); }));
+        else HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(pa, ctx->stream); }));
         return SDFNMPC_OK;
     };
     int rc;
@@ -975,10 +1000,10 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
         if (rc) return rc;
         if (ctx->serial_prep) {
             HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }, ctx->stream));
-            return SDFNMPC_OK;
+            return finish_pack();
         }
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
-        return SDFNMPC_OK;
+        return finish_pack();
     }
     rc = run_hoist<double>(ctx, net, a->p + 17, stride, n_inst, (float*)ctx->c13.p);
     if (rc) return rc;
@@ -989,18 +1014,24 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
     if (rc) return rc;
     if (ctx->serial_prep) {
         HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }, ctx->stream));
-        return SDFNMPC_OK;
+        return finish_pack();
     }
     HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
-    return SDFNMPC_OK;
+    return finish_pack();
+}
+
+extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
+                                 const sdfnmpc_lin_args* a) {
+    if (ctx) ctx->prep.valid = false;  // lin outputs may change under records packed earlier
+    return lin_impl(ctx, net, mdl, a, nullptr);
 }
 
 // ------------------------------------------------------------------------------------------------
 // batched QP (feedback phase) and RTI step
-extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* a) {
-    if (!ctx || !o || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
-    if (a->B < 0 || a->N < 1 || a->N > 200) return fail(SDFNMPC_E_ARG, "bad B/N for sdfnmpc_qp_solve");
-    if (a->B == 0) return SDFNMPC_OK;
+// validation and kernel arguments shared by sdfnmpc_qp_solve / sdfnmpc_rti_prepare / sdfnmpc_qp_feedback
+// (sizes the workspace; the caller holds the device scope)
+static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* a, QpArgs& q) {
+    if (a->B < 0 || a->N < 1 || a->N > 200) return fail(SDFNMPC_E_ARG, "bad B/N for the QP");
     if (!a->xn || !a->AB || !a->y || !a->Jy || !a->yN || !a->JyN || !a->h || !a->Jh || !a->x || !a->u || !a->x0 ||
         !a->yref || !a->W || !a->yNref || !a->WN || !a->dt || !a->dx || !a->du)
         return fail(SDFNMPC_E_ARG, "NULL array in sdfnmpc_qp_args");
@@ -1008,11 +1039,10 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
         return fail(SDFNMPC_E_ARG, "qp opts: lm > 0 (strict convexity), max_iter >= 1, tol > 0 required");
     if (o->ny != 11 && o->ny != 12) return fail(SDFNMPC_E_ARG, "qp opts: ny must be 11 or 12 (sdf_cost)");
     if (qp_lds_bytes(a->N) > 160 * 1024) return fail(SDFNMPC_E_UNSUPPORTED, "horizon too long for the LDS-resident QP");
-    ScopedDevice sd(ctx->device);
     HIPCHK(ctx->qpw.ensure((size_t)a->B * qp_work_doubles(a->N) * sizeof(double)));
     const bool own_st = !a->status || !a->iters || !a->res;
     if (own_st) HIPCHK(ctx->qpst.ensure((size_t)a->B * (2 * sizeof(int) + 2 * sizeof(double))));
-    QpArgs q{};
+    q = QpArgs{};
     q.B = a->B; q.N = a->N;
     q.xn = a->xn; q.AB = a->AB; q.y = a->y; q.Jy = a->Jy; q.yN = a->yN; q.JyN = a->JyN; q.h = a->h; q.Jh = a->Jh;
     q.x = a->x; q.u = a->u; q.x0 = a->x0; q.yref = a->yref; q.W = a->W; q.yNref = a->yNref; q.WN = a->WN; q.dt = a->dt;
@@ -1026,7 +1056,52 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
     for (int i = 0; i < 3; ++i) { q.lh[i] = o->lh[i]; q.uh[i] = o->uh[i]; q.zl[i] = o->zl[i]; q.Zl[i] = o->Zl[i]; }
     q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling; q.ny = o->ny;
     q.lm_scaling = o->lm_scaling;
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* a) {
+    if (!ctx || !o || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
+    ctx->prep.valid = false;  // the workspace is repacked here
+    if (a->B == 0) return SDFNMPC_OK;
+    ScopedDevice sd(ctx->device);
+    QpArgs q;
+    if (int rc = qp_build(ctx, o, a, q)) return rc;
     HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(q, ctx->stream); }));
+    HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_rti_prepare(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
+                                   const sdfnmpc_lin_args* la, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* qa) {
+    if (!ctx || !net || !mdl || !la || !o || !qa) return fail(SDFNMPC_E_ARG, "NULL argument");
+    ctx->prep.valid = false;
+    if (la->B != qa->B || la->N != qa->N) return fail(SDFNMPC_E_ARG, "rti_prepare: lin and qp args differ in B / N");
+    if (la->xn != qa->xn || la->AB != qa->AB || la->y != qa->y || la->Jy != qa->Jy || la->yN != qa->yN ||
+        la->JyN != qa->JyN || la->h != qa->h || la->Jh != qa->Jh || la->x != qa->x || la->u != qa->u)
+        return fail(SDFNMPC_E_ARG, "rti_prepare: the qp args must name the lin args' iterate and outputs");
+    if (la->B == 0) return SDFNMPC_OK;
+    ScopedDevice sd(ctx->device);
+    QpArgs q;
+    if (int rc = qp_build(ctx, o, qa, q)) return rc;
+    if (int rc = lin_impl(ctx, net, mdl, la, &q)) return rc;
+    ctx->prep.valid = true;
+    ctx->prep.B = qa->B;
+    ctx->prep.N = qa->N;
+    ctx->prep.xn = qa->xn;
+    ctx->prep.work = q.work;
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_qp_feedback(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* a) {
+    if (!ctx || !o || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
+    if (a->B == 0) return SDFNMPC_OK;
+    if (!ctx->prep.valid || ctx->prep.B != a->B || ctx->prep.N != a->N || ctx->prep.xn != a->xn)
+        return fail(SDFNMPC_E_ARG, "qp_feedback: no stage records from sdfnmpc_rti_prepare for these arguments");
+    ScopedDevice sd(ctx->device);
+    QpArgs q;
+    if (int rc = qp_build(ctx, o, a, q)) return rc;
+    if (q.work != ctx->prep.work) return fail(SDFNMPC_E_ARG, "qp_feedback: workspace moved since rti_prepare");
+    ctx->prep.valid = false;  // one feedback per preparation, as in acados' SQP-RTI
     HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
     return SDFNMPC_OK;
 }

@@ -24,6 +24,8 @@ struct QpArgs {
     int max_iter, cost_scaling;
     int lm_scaling;  // 1: lm dt_k at stages k < N, lm at N (acados' Ts-scaled Levenberg-Marquardt term)
     int ny;  // 11, or 12 with the sdf cost residual (formed in the pack kernel from h[2], J_h[2])
+    int pack_part;  // 0: whole stage records; 1: all but the sdf row of C^T, which
+                    // rti_qp_pack_sdf_kernel writes once the SDF kernel is done (needs ny == 11)
 };
 
 constexpr int QP_REC = 300;   // stage record: [A B | c | g | C^T | H upper | 0]            (rti_qp.hip)
@@ -53,6 +55,7 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
 __host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N) * sizeof(double); }
 
 hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s);  // stage records into the workspace
+hipError_t launch_rti_qp_pack_sdf(const QpArgs& a, hipStream_t s);  // the sdf row of C^T (after pack_part 1)
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);       // the IPM (after launch_rti_qp_pack)
 hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx, const double* du, double* u0,
                             const int* status, hipStream_t s);

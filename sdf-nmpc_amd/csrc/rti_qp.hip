@@ -311,7 +311,9 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
         const double sk = A.cost_scaling ? A.dt[k] : 1.0;
         const double lmk = A.lm_scaling ? A.lm * A.dt[k] : A.lm;  // acados: Ts_k lm for k < N, lm at N
         const int g = lane >> 4, c = lane & 15;
-        const double ts = 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2];  // sdf cost (gen_model.py:65-66)
+        // sdf cost (gen_model.py:65-66); h[2] is read only then (pack_part 1 runs beside the SDF kernel)
+        const double ts = ny > 11 ? 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2] : 0.0;
+        const int nct = A.pack_part == 1 ? 20 : 30;  // C^T entries written here (rows j < 2 | all)
         d4 D = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int st = 0; st < 3; ++st) {
@@ -336,7 +338,7 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
             const int e = 128 + lane;
             if (e < R_C) Rk[e] = AB[e];
             else if (e < R_G) Rk[e] = xn[e - R_C] - xb1[e - R_C];
-            else if (e >= R_CT) {
+            else if (e >= R_CT && e < R_CT + nct) {
                 const int q = e - R_CT, j = q / 10;
                 Rk[e] = Jh[(q - 10 * j) * 3 + j];
             }
@@ -344,7 +346,7 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
         for (int e = 192 + lane; e < REC; e += 64) {
             if (e < R_H) {
                 const int q = e - R_CT, j = q / 10;
-                Rk[e] = Jh[(q - 10 * j) * 3 + j];
+                if (q < nct) Rk[e] = Jh[(q - 10 * j) * 3 + j];
             } else if (e >= R_H + 105) {
                 Rk[e] = 0.0;
             }
@@ -361,7 +363,9 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
         const double* Wn = A.WN + (size_t)b * 4;
         const double* yn = A.yN + (size_t)b * 4;
         const double* rn = A.yNref + (size_t)b * 4;
+        const int nct = A.pack_part == 1 ? 20 : 30;
         for (int e = lane; e < REC; e += 64) {
+            if (e >= R_CT + nct && e < R_H) continue;  // the sdf row: rti_qp_pack_sdf_kernel
             double v = 0.0;
             if (e >= R_G && e < R_G + 10) {
                 const int a = e - R_G;
@@ -377,6 +381,19 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
             Rk[e] = v;
         }
     }
+}
+
+// The sdf row of C^T (J_h[.][2]) of every stage record: the part of the pack that waits for the SDF
+// kernel's epilogue when the rest ran beside it (pack_part 1).  One thread per (node, state).
+__global__ __launch_bounds__(256) void rti_qp_pack_sdf_kernel(QpArgs A) {
+    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+    const int N1 = A.N + 1;
+    if (i >= (long long)A.B * N1 * NX) return;
+    const long long node = i / NX;
+    const int l = (int)(i - node * NX);
+    const long long b = node / N1;
+    const int k = (int)(node - b * N1);
+    A.work[(size_t)b * qp_work_doubles(A.N) + (size_t)k * REC + R_CT + 20 + l] = A.Jh[(size_t)node * 30 + l * 3 + 2];
 }
 
 #ifdef QP_STAMPS  // diagnostic build only: per-phase cycle accounting (never in the product build)
@@ -1209,6 +1226,13 @@ hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     hipLaunchKernelGGL(rti_qp_pack_kernel, dim3((unsigned)((a.B * (a.N + 1) + PACK_NODES - 1) / PACK_NODES)),
                        dim3(64 * PACK_NODES), 0, s, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_rti_qp_pack_sdf(const QpArgs& a, hipStream_t s) {
+    const long long n = (long long)a.B * (a.N + 1) * NX;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(rti_qp_pack_sdf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

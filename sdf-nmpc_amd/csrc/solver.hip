@@ -4,7 +4,7 @@
 // preparation-phase outputs, QP results -- on one context (device + stream), so a controller drives
 // it with host arrays and no tensor framework: the counterpart of the AcadosOcpSolver object that
 // sdf_nmpc/ocp.py:127 builds (solver.set / cost_set / get / solve_for_x0 / reset), batched over B
-// instances.  The compute is the lower-level entry points (sdfnmpc_linearize, sdfnmpc_qp_solve,
+// instances.  The compute is the lower-level entry points (sdfnmpc_rti_prepare, sdfnmpc_qp_feedback,
 // sdfnmpc_rti_apply); this file adds buffer ownership, masked row uploads through a pinned staging
 // arena, and the asynchronous step / wait split that lets one host thread keep several devices busy.
 #include <hip/hip_runtime.h>
@@ -293,15 +293,15 @@ extern "C" int sdfnmpc_solver_step(sdfnmpc_solver* s) {
     la.B = s->B; la.N = s->N; la.np = s->np; la.latent_mode = s->latent_mode;
     la.x = s->x; la.u = s->u; la.p = s->p; la.dt = s->dt;
     la.xn = s->xn; la.AB = s->AB; la.y = s->y; la.Jy = s->Jy; la.yN = s->yN; la.JyN = s->JyN; la.h = s->h; la.Jh = s->Jh;
-    int rc = sdfnmpc_linearize(s->ctx, s->net, &s->model, &la);
-    if (rc) return rc;
     sdfnmpc_qp_args qa{};
     qa.B = s->B; qa.N = s->N;
     qa.xn = s->xn; qa.AB = s->AB; qa.y = s->y; qa.Jy = s->Jy; qa.yN = s->yN; qa.JyN = s->JyN; qa.h = s->h; qa.Jh = s->Jh;
     qa.x = s->x; qa.u = s->u; qa.x0 = s->x0; qa.yref = s->yref; qa.W = s->W; qa.yNref = s->yNref; qa.WN = s->WN;
     qa.dt = s->dt; qa.dx = s->dx; qa.du = s->du; qa.slack = s->slack; qa.status = s->status; qa.iters = s->iters;
     qa.res = s->res;
-    rc = sdfnmpc_qp_solve(s->ctx, &s->qp, &qa);
+    int rc = sdfnmpc_rti_prepare(s->ctx, s->net, &s->model, &la, &s->qp, &qa);  // preparation (+ stage records)
+    if (rc) return rc;
+    rc = sdfnmpc_qp_feedback(s->ctx, &s->qp, &qa);                             // feedback
     if (rc) return rc;
     rc = sdfnmpc_rti_apply(s->ctx, s->B, s->N, s->x, s->u, s->dx, s->du, s->u0, s->status);
     if (rc) return rc;
