@@ -1005,13 +1005,24 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
         HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
         return finish_pack();
     }
-    rc = run_hoist<double>(ctx, net, a->p + 17, stride, n_inst, (float*)ctx->c13.p);
-    if (rc) return rc;
-    if (!ctx->lin_first && (rc = fork_lin())) return rc;
-    // 3. network forward + position gradient, with the sdf row of h / J_h in its epilogue
-    rc = run_sdf(ctx, net, rows, nullptr, (const float*)ctx->c13.p,
-                 a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows, &cons);
-    if (rc) return rc;
+    if (rows <= SDF_ROW_PREP_MAX) {  // a few rows (B = 1): one workgroup per row, no hoist
+        if (!ctx->lin_first && (rc = fork_lin())) return rc;
+        SdfRowArgs ra = net->row;
+        ra.x = a->x; ra.p = a->p; ra.np = a->np;
+        ra.zd = a->p + 17; ra.zstride = stride; ra.rows_per_inst = a->latent_mode == 0 ? a->N + 1 : 1;
+        ra.h = a->h; ra.Jh = a->Jh; ra.max_df = net->host.max_df;
+        ra.out = sdf4;
+        ra.rows = (int)rows;
+        HIPCHK(timed(ctx, "sdf_row", [&] { return launch_sdf_row(ra, ctx->stream); }));
+    } else {
+        rc = run_hoist<double>(ctx, net, a->p + 17, stride, n_inst, (float*)ctx->c13.p);
+        if (rc) return rc;
+        if (!ctx->lin_first && (rc = fork_lin())) return rc;
+        // 3. network forward + position gradient, with the sdf row of h / J_h in its epilogue
+        rc = run_sdf(ctx, net, rows, nullptr, (const float*)ctx->c13.p,
+                     a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows, &cons);
+        if (rc) return rc;
+    }
     if (ctx->serial_prep) {
         HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }, ctx->stream));
         return finish_pack();

@@ -74,8 +74,18 @@ struct SdfRowArgs {
     float4* out;            // [rows] (df, d df / d pos)
     float* grad_latent;     // [rows][L] or NULL
     int rows;
+    // preparation-phase variant (sdfnmpc_linearize at a few rows, x != NULL): Co_p_B from x / p and the
+    // constraint epilogue exactly as sdf_mlp_kernel forms them (SdfArgs), the latent from the fp64
+    // stage parameters of the row's instance
+    const double *x, *p;    // [rows][10], [rows][np]
+    const double* zd;       // latent of row r at zd[(r / rows_per_inst) * zstride + k]
+    long long zstride;
+    int np, rows_per_inst;
+    double *h, *Jh;         // [rows][3], [rows][10][3]: the sdf row
+    double max_df;
 };
-constexpr int SDF_ROW_MAX = 16;  // host-path calls with at most this many rows use sdf_row_kernel
+constexpr int SDF_ROW_MAX = 16;       // host-path calls with at most this many rows use sdf_row_kernel
+constexpr int SDF_ROW_PREP_MAX = 64;  // and preparation phases with at most this many rows (B=1 at N <= 63)
 
 template <typename T>
 struct HoistArgs {

@@ -111,7 +111,17 @@ __global__ __launch_bounds__(64 * RW) void sdf_row_kernel(SdfRowArgs A) {
     __shared__ __align__(16) float part[RW * (C3 + 1)];
     __shared__ float red[4];
     const float w0 = A.w0;
-    const float4 p = A.pos[r];
+    float4 p;
+    if (A.x) {  // Co_p_B = W_R_Co^T (W_p_B - W_p_Co) in fp64, handed over as fp32 (sdf_mlp_kernel's)
+        const double* xr = A.x + (size_t)r * 10;
+        const double* pr = A.p + (size_t)r * A.np;
+        const double* R = pr + 4;
+        const double e0 = xr[0] - pr[1], e1 = xr[1] - pr[2], e2 = xr[2] - pr[3];
+        p = make_float4((float)((e0 * R[0] + e1 * R[3]) + e2 * R[6]), (float)((e0 * R[1] + e1 * R[4]) + e2 * R[7]),
+                        (float)((e0 * R[2] + e1 * R[5]) + e2 * R[8]), 0.0f);
+    } else {
+        p = A.pos[r];
+    }
     // ---- embedding (e = [x, sin(xb), sin(xb + pi/2)], sdf_wide.hip's arithmetic) and the latent
     for (int m = threadIdx.x; m < NE; m += 64 * RW) {
         float e = 0.0f, g = 0.0f;
@@ -131,7 +141,7 @@ __global__ __launch_bounds__(64 * RW) void sdf_row_kernel(SdfRowArgs A) {
         }
     }
     for (int k = threadIdx.x; k < L; k += 64 * RW) {
-        const float z = A.latent[(size_t)r * L + k];
+        const float z = A.zd ? (float)A.zd[(size_t)(r / A.rows_per_inst) * A.zstride + k] : A.latent[(size_t)r * L + k];
         in1[E + k] = z;
         in3[N2 + E + k] = z;
     }
@@ -211,7 +221,22 @@ __global__ __launch_bounds__(64 * RW) void sdf_row_kernel(SdfRowArgs A) {
         s0 = wave_sum(s0);
         s1 = wave_sum(s1);
         s2 = wave_sum(s2);
-        if (lane == 0) A.out[r] = make_float4(red[0], s0, s1, s2);
+        if (lane == 0) {
+            const float df = red[0];
+            A.out[r] = make_float4(df, s0, s1, s2);
+            if (A.h) {  // sdf row of the constraint vector and its Jacobian (gen_model.py:46-61), as sdf_mlp_kernel
+                const double* pr = A.p + (size_t)r * A.np;
+                const double flag = pr[0];
+                const double* R = pr + 4;  // W_R_Co row-major (== casadi reshape((3,3)).T)
+                A.h[(size_t)r * 3 + 2] = flag * (double)df + (1.0 - flag) * A.max_df;
+                double* J = A.Jh + (size_t)r * 30 + 2;
+#pragma unroll
+                for (int j = 0; j < 10; ++j)
+                    J[j * 3] = (j < 3) ? flag * (((double)s0 * R[j * 3 + 0] + (double)s1 * R[j * 3 + 1]) +
+                                                 (double)s2 * R[j * 3 + 2])
+                                       : 0.0;
+            }
+        }
     }
 }
 

@@ -60,7 +60,7 @@ def _cfg():
     return Config()
 
 
-@pytest.mark.parametrize("B,N,tile,mode", [(1, 20, 32, 0), (7, 40, 64, 0), (16, 40, 32, 1), (3, 60, 32, 0)])
+@pytest.mark.parametrize("B,N,tile,mode", [(1, 20, 32, 0), (1, 40, 32, 1), (7, 40, 64, 0), (16, 40, 32, 1), (3, 60, 32, 0)])
 def test_linearize_vs_oracle(gpu_ctx, oracle_lib, cfg, B, N, tile, mode):
     prob = synth.make_problem(cfg, B, N, seed=B * 100 + N)
     prob["p"][:, ::3, 0] = 0.0  # flag off at some nodes (gen_model.py:58-61)
