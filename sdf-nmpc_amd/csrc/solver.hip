@@ -35,6 +35,22 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(double* dst, int widt
     dst[(long long)idx[r] * width + col0 + c] = staged[i];
 }
 
+// x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (ocp.py:156-160): one thread per (instance, column), nodes in
+// ascending order, so the overlapping rows are read before they are overwritten
+__global__ __launch_bounds__(256) void shift_kernel(int B, int N, int k, double* x, double* u) {
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)B * 14) return;
+    const long long b = i / 14;
+    const int j = (int)(i - b * 14);
+    if (j < 10) {
+        double* xb = x + b * (N + 1) * 10 + j;
+        for (int n = k; n < N; ++n) xb[(n - k) * 10] = xb[n * 10];
+    } else {
+        double* ub = u + b * N * 4 + (j - 10);
+        for (int n = k; n < N; ++n) ub[(n - k) * 4] = ub[n * 4];
+    }
+}
+
 // x[b][k] = x0[b] (k = 0..N), u[b][k] = u_init (k < N)
 __global__ __launch_bounds__(256) void init_iterate_kernel(int B, int N, double* x, double* u, const double* x0,
                                                            double u0, double u1, double u2, double u3) {
@@ -70,7 +86,7 @@ struct sdfnmpc_solver {
     double *x = nullptr, *u = nullptr, *p = nullptr, *x0 = nullptr, *yref = nullptr, *W = nullptr, *yNref = nullptr,
            *WN = nullptr, *dt = nullptr, *xn = nullptr, *AB = nullptr, *y = nullptr, *Jy = nullptr, *yN = nullptr,
            *JyN = nullptr, *h = nullptr, *Jh = nullptr, *dx = nullptr, *du = nullptr, *res = nullptr, *u0 = nullptr,
-           *scratch = nullptr, *slack = nullptr;
+           *slack = nullptr;
     int *status = nullptr, *iters = nullptr;
     // pinned host memory: step outputs and the upload staging arena (reset after every wait)
     double* h_u0 = nullptr;
@@ -88,9 +104,7 @@ struct sdfnmpc_solver {
         (void)hipStreamSynchronize(stream);
         for (void* a : allocs) (void)hipFree(a);
         if (d_arena) (void)hipFree(d_arena);
-        if (h_u0) (void)hipHostFree(h_u0);
-        if (h_status) (void)hipHostFree(h_status);
-        if (h_iters) (void)hipHostFree(h_iters);
+        if (h_u0) (void)hipHostFree(h_u0);  // [u0 | status | iters] in one pinned block
         if (arena) (void)hipHostFree(arena);
         if (prev >= 0) (void)hipSetDevice(prev);
     }
@@ -173,10 +187,18 @@ extern "C" int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, c
     A(&s->yref, B * N * o->ny); A(&s->W, B * N * o->ny); A(&s->yNref, B * 4); A(&s->WN, B * 4); A(&s->dt, N);
     A(&s->xn, B * N * 10); A(&s->AB, B * N * 140); A(&s->y, B * N * 11); A(&s->Jy, B * N * 154); A(&s->yN, B * 4);
     A(&s->JyN, B * 40); A(&s->h, B * N1 * 3); A(&s->Jh, B * N1 * 30); A(&s->dx, B * N1 * 10); A(&s->du, B * N * 4);
-    A(&s->res, B * 2); A(&s->u0, B * 4); A(&s->scratch, B * N1 * 10); A(&s->slack, B * N1 * 6); A(&s->status, B); A(&s->iters, B);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&s->h_u0, B * 4 * sizeof(double), hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&s->h_status, B * sizeof(int), hipHostMallocDefault);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&s->h_iters, B * sizeof(int), hipHostMallocDefault);
+    A(&s->res, B * 2); A(&s->slack, B * N1 * 6);
+    // [u0 (B x 4 doubles) | status (B ints) | iters (B ints)] contiguous on both sides: one copy back per step
+    A(&s->u0, B * 5);
+    if (e == hipSuccess) {
+        s->status = (int*)(s->u0 + B * 4);
+        s->iters = s->status + B;
+        e = hipHostMalloc((void**)&s->h_u0, B * 5 * sizeof(double), hipHostMallocDefault);
+    }
+    if (e == hipSuccess) {
+        s->h_status = (int*)(s->h_u0 + B * 4);
+        s->h_iters = s->h_status + B;
+    }
     if (e == hipSuccess) e = hipMemcpyAsync(s->dt, o->dt, N * sizeof(double), hipMemcpyHostToDevice, s->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(s->stream);
     if (e != hipSuccess) {
@@ -274,12 +296,11 @@ extern "C" int sdfnmpc_solver_shift(sdfnmpc_solver* s, int k) {
     if (!s) return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "NULL solver");
     if (k <= 0 || k >= s->N) return SDFNMPC_OK;  // ocp.py:156: k > 0 shifts nodes k..N-1 down by k
     SolverDevice sd(s->device);
-    const size_t n1 = s->N + 1, n = s->N, m = s->N - k;
-    // x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (overlapping per row: through the scratch buffer)
-    SCHK(hipMemcpy2DAsync(s->scratch, m * 80, s->x + k * 10, n1 * 80, m * 80, s->B, hipMemcpyDeviceToDevice, s->stream));
-    SCHK(hipMemcpy2DAsync(s->x, n1 * 80, s->scratch, m * 80, m * 80, s->B, hipMemcpyDeviceToDevice, s->stream));
-    SCHK(hipMemcpy2DAsync(s->scratch, m * 32, s->u + k * 4, n * 32, m * 32, s->B, hipMemcpyDeviceToDevice, s->stream));
-    SCHK(hipMemcpy2DAsync(s->u, n * 32, s->scratch, m * 32, m * 32, s->B, hipMemcpyDeviceToDevice, s->stream));
+    // one launch (it was four strided copies through a scratch buffer: launch latency on the C1 path)
+    const long long n = (long long)s->B * 14;
+    hipLaunchKernelGGL(shift_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s->stream, s->B, s->N, k, s->x,
+                       s->u);
+    SCHK(hipGetLastError());
     return SDFNMPC_OK;
 }
 
@@ -305,9 +326,7 @@ extern "C" int sdfnmpc_solver_step(sdfnmpc_solver* s) {
     if (rc) return rc;
     rc = sdfnmpc_rti_apply(s->ctx, s->B, s->N, s->x, s->u, s->dx, s->du, s->u0, s->status);
     if (rc) return rc;
-    SCHK(hipMemcpyAsync(s->h_u0, s->u0, (size_t)s->B * 32, hipMemcpyDeviceToHost, s->stream));
-    SCHK(hipMemcpyAsync(s->h_status, s->status, (size_t)s->B * 4, hipMemcpyDeviceToHost, s->stream));
-    SCHK(hipMemcpyAsync(s->h_iters, s->iters, (size_t)s->B * 4, hipMemcpyDeviceToHost, s->stream));
+    SCHK(hipMemcpyAsync(s->h_u0, s->u0, (size_t)s->B * 40, hipMemcpyDeviceToHost, s->stream));  // u0, status, iters
     s->pending = true;
     return SDFNMPC_OK;
 }
