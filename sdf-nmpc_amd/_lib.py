@@ -499,14 +499,18 @@ class Solver:
         h = C.c_void_p()
         _check(load().sdfnmpc_solver_create(ctx.h, net.h, C.byref(o), C.byref(h)))
         self.h = h
+        self._shapes = {}
         self.u0 = np.zeros((self.B, 4))
         self.status = np.zeros(self.B, np.int32)
         self.iters = np.zeros(self.B, np.int32)
 
     def shape(self, name: str):
-        nodes, width = C.c_int(), C.c_int()
-        _check(load().sdfnmpc_solver_field(self.h, name.encode(), None, C.byref(nodes), C.byref(width)))
-        return (self.B, nodes.value, width.value)
+        shp = self._shapes.get(name)  # fixed at creation: cached (the per-step upload path asks for it)
+        if shp is None:
+            nodes, width = C.c_int(), C.c_int()
+            _check(load().sdfnmpc_solver_field(self.h, name.encode(), None, C.byref(nodes), C.byref(width)))
+            shp = self._shapes[name] = (self.B, nodes.value, width.value)
+        return shp
 
     def field(self, name: str) -> FieldView:
         p, nodes, width = C.c_void_p(), C.c_int(), C.c_int()
