@@ -186,7 +186,7 @@ def main():
     reps = max(5, min(args.steps, 20))
     for _ in range(reps):
         step()
-    names = ("sdf_hoist", "sdf_mlp", "linearize", "rti_qp_pack", "rti_qp_pack_sdf", "rti_qp", "rti_apply")
+    names = ("sdf_hoist", "sdf_mlp", "linearize", "rti_qp_pack", "rti_qp", "rti_apply")
     kst = {k: ctx.kernel_stats(k) for k in names}
     ctx.enable_timing(False)
     kms = {k: (v[0] / v[1] if v[1] else None) for k, v in kst.items()}
@@ -561,7 +561,7 @@ def main_c5(args):
     for _ in range(reps):
         step()
     names = ("vae_pre", "vae_stem", "vae_conv", "vae_head", "sdf_wide_hoist", "sdf_wide_emb", "sdf_wide_gemm",
-             "sdf_wide_final", "linearize", "ref_pack", "rti_qp_pack", "rti_qp_pack_sdf", "rti_qp", "rti_apply")
+             "sdf_wide_final", "linearize", "ref_pack", "rti_qp_pack", "rti_qp", "rti_apply")
     kms = {k: ctx.kernel_stats(k)[0] / reps for k in names}  # ms per step (all launches of that name)
     ctx.enable_timing(False)
     spec = V.DEFAULT_ENCODER

@@ -94,6 +94,7 @@ struct sdfnmpc_ctx {
         int B = 0, N = 0;
         const double* xn = nullptr;  // the lin outputs they were packed from
         const void* work = nullptr;
+        bool sdf_row_patch = false;  // the feedback's QP kernel copies the sdf row of C^T into them
     } prep;
 };
 
@@ -978,8 +979,8 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
     // after the join: the rest of the pack on the main stream
     auto finish_pack = [&]() -> int {
         if (!pk) return SDFNMPC_OK;
-        if (split) HIPCHK(timed(ctx, "rti_qp_pack_sdf", [&] { return launch_rti_qp_pack_sdf(pa, ctx->stream); }));
-        else HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(pa, ctx->stream); }));
+        // split: the sdf row of C^T is copied by rti_qp_kernel itself (sdf_row_patch), no launch here
+        if (!split) HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(pa, ctx->stream); }));
         return SDFNMPC_OK;
     };
     int rc;
@@ -1096,6 +1097,7 @@ extern "C" int sdfnmpc_rti_prepare(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, con
     if (int rc = qp_build(ctx, o, qa, q)) return rc;
     if (int rc = lin_impl(ctx, net, mdl, la, &q)) return rc;
     ctx->prep.valid = true;
+    ctx->prep.sdf_row_patch = q.ny == 11 && !ctx->serial_prep;  // lin_impl's split: records lack the sdf row
     ctx->prep.B = qa->B;
     ctx->prep.N = qa->N;
     ctx->prep.xn = qa->xn;
@@ -1113,6 +1115,7 @@ extern "C" int sdfnmpc_qp_feedback(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, c
     if (int rc = qp_build(ctx, o, a, q)) return rc;
     if (q.work != ctx->prep.work) return fail(SDFNMPC_E_ARG, "qp_feedback: workspace moved since rti_prepare");
     ctx->prep.valid = false;  // one feedback per preparation, as in acados' SQP-RTI
+    q.sdf_row_patch = ctx->prep.sdf_row_patch ? 1 : 0;
     HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
     return SDFNMPC_OK;
 }

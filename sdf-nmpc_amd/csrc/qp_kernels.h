@@ -24,8 +24,9 @@ struct QpArgs {
     int max_iter, cost_scaling;
     int lm_scaling;  // 1: lm dt_k at stages k < N, lm at N (acados' Ts-scaled Levenberg-Marquardt term)
     int ny;  // 11, or 12 with the sdf cost residual (formed in the pack kernel from h[2], J_h[2])
-    int pack_part;  // 0: whole stage records; 1: all but the sdf row of C^T, which
-                    // rti_qp_pack_sdf_kernel writes once the SDF kernel is done (needs ny == 11)
+    int pack_part;  // 0: whole stage records; 1: all but the sdf row of C^T (needs ny == 11), which
+                    // rti_qp_kernel then copies from J_h itself (sdf_row_patch)
+    int sdf_row_patch;  // rti_qp_kernel: copy J_h[.][2] into the records' C^T row 2 before the sweeps
 };
 
 constexpr int QP_REC = 300;   // stage record: [A B | c | g | C^T | H upper | 0]            (rti_qp.hip)
@@ -55,7 +56,6 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
 __host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N) * sizeof(double); }
 
 hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s);  // stage records into the workspace
-hipError_t launch_rti_qp_pack_sdf(const QpArgs& a, hipStream_t s);  // the sdf row of C^T (after pack_part 1)
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);       // the IPM (after launch_rti_qp_pack)
 hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx, const double* du, double* u0,
                             const int* status, hipStream_t s);

@@ -365,7 +365,7 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
         const double* rn = A.yNref + (size_t)b * 4;
         const int nct = A.pack_part == 1 ? 20 : 30;
         for (int e = lane; e < REC; e += 64) {
-            if (e >= R_CT + nct && e < R_H) continue;  // the sdf row: rti_qp_pack_sdf_kernel
+            if (e >= R_CT + nct && e < R_H) continue;  // the sdf row: rti_qp_kernel copies it (sdf_row_patch)
             double v = 0.0;
             if (e >= R_G && e < R_G + 10) {
                 const int a = e - R_G;
@@ -381,19 +381,6 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
             Rk[e] = v;
         }
     }
-}
-
-// The sdf row of C^T (J_h[.][2]) of every stage record: the part of the pack that waits for the SDF
-// kernel's epilogue when the rest ran beside it (pack_part 1).  One thread per (node, state).
-__global__ __launch_bounds__(256) void rti_qp_pack_sdf_kernel(QpArgs A) {
-    const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
-    const int N1 = A.N + 1;
-    if (i >= (long long)A.B * N1 * NX) return;
-    const long long node = i / NX;
-    const int l = (int)(i - node * NX);
-    const long long b = node / N1;
-    const int k = (int)(node - b * N1);
-    A.work[(size_t)b * qp_work_doubles(A.N) + (size_t)k * REC + R_CT + 20 + l] = A.Jh[(size_t)node * 30 + l * 3 + 2];
 }
 
 #ifdef QP_STAMPS  // diagnostic build only: per-phase cycle accounting (never in the product build)
@@ -451,6 +438,14 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         if (lane < 20) s.cst[lane] = v;
     }
     for (int e = lane; e < N1; e += 64) s.skv[e] = (A.cost_scaling && e < N) ? A.dt[e] : 1.0;
+    if (A.sdf_row_patch) {  // records packed beside the SDF kernel (pack_part 1): their sdf row of C^T
+        double* Rw = A.work + (size_t)b * qp_work_doubles(N);
+        for (int e = lane; e < N1 * NX; e += 64) {
+            const int k = e / NX, l = e - k * NX;
+            Rw[(size_t)k * REC + R_CT + 20 + l] = A.Jh[((size_t)b * N1 + k) * 30 + l * 3 + 2];
+        }
+        __threadfence_block();  // stored before any lane of the wave streams the records
+    }
     if (lane < NX) s.dx[lane] = A.x0[(size_t)b * 10 + lane] - A.x[(size_t)b * N1 * 10 + lane];
     if (lane < 48) s.zero[lane] = 0.0;
     __syncthreads();
@@ -1226,13 +1221,6 @@ hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     hipLaunchKernelGGL(rti_qp_pack_kernel, dim3((unsigned)((a.B * (a.N + 1) + PACK_NODES - 1) / PACK_NODES)),
                        dim3(64 * PACK_NODES), 0, s, a);
-    return hipGetLastError();
-}
-
-hipError_t launch_rti_qp_pack_sdf(const QpArgs& a, hipStream_t s) {
-    const long long n = (long long)a.B * (a.N + 1) * NX;
-    if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(rti_qp_pack_sdf_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 
