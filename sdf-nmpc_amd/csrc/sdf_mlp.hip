@@ -365,8 +365,11 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
     // ---- embedding backward: grad_c = sum_m (d e_m * g_m) * P[m][c]  (+ d e_c for m < 3)
     //      partials per (row, c, m) -> Ebuf..Bbuf (contiguous, both free), then one thread per
     //      (row, c) sums over m
-    static_assert(SE + SA >= 3 * NE, "reduction area");
-    float* red = Ebuf;  // [M][3][NE]
+    // rows of NE + 1 floats: the summing threads (one per (row, c), reading along m) then hit 32 distinct
+    // banks; at NE = 96 = 0 mod 32 every lane of a read would share one bank (32-way)
+    constexpr int NR = NE + 1;
+    static_assert(SE + SA >= 3 * NR, "reduction area");
+    float* red = Ebuf;  // [M][3][NR]
     if (w < 3) {
         const int m = w * 32 + col;
 #pragma unroll
@@ -385,14 +388,14 @@ __global__ __launch_bounds__(256, (M == 32) ? 2 : 1) void sdf_mlp_kernel(SdfArgs
                     v1 = u * ptab.y;
                     v2 = u * ptab.z;
                 }
-                red[(row * 3 + 0) * NE + m] = v0;
-                red[(row * 3 + 1) * NE + m] = v1;
-                red[(row * 3 + 2) * NE + m] = v2;
+                red[(row * 3 + 0) * NR + m] = v0;
+                red[(row * 3 + 1) * NR + m] = v1;
+                red[(row * 3 + 2) * NR + m] = v2;
             }
     }
     SDF_SYNC();
     if (tid < 3 * M) {
-        const float* src = red + tid * NE;
+        const float* src = red + tid * NR;
         float s = 0.0f;
         for (int m = 0; m < NE; ++m) s += src[m];
         posb[(tid / 3) * 4 + 1 + tid % 3] = s;
