@@ -69,6 +69,7 @@ constexpr int SLOT = QP_SLOT, PD = QP_RING;
 //   2, 4 forward          F[0, 192) | R[164, 228)      factor rows at 0, C^T at WF_CT
 //   3 backward corrector  F[0, 256) | R[100, 228)      factor record at 0, R[i] at WB_R + i (i >= 100)
 constexpr int WF_CT = 192, WB_R = 256 - 100;
+static_assert((WB_R + R_G + NX) % 2 == 0, "g~_u block of the corrector window is 16-byte aligned");
 __host__ __device__ constexpr int n_loads(int K) { return (K == 1 || K == 3) ? 6 : 4; }
 __host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K == 4) ? j < 3 : K == 3 ? j < 4 : false; }
 __host__ __device__ constexpr int load_at(int K, int j) {
@@ -709,12 +710,15 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
         // ---- every LDS read of the stage first (one round trip), the chain input p_{k+1} last
         double bvv[NU], guw[NU], kk[NU], row[NX];
-#pragma unroll
-        for (int i = 0; i < NU; ++i) {
-            bvv[i] = s.bv[k * NU + i];
-            guw[i] = win[WB_R + R_G + NX + i];
-            kk[i] = bc_k[FR * i];
+        {  // the uniform box and g~_u terms as 16-byte reads (both blocks are 16-byte aligned)
+            const ldsd2* bq = (const ldsd2*)(s.bv + k * NU);
+            const ldsd2* gq = (const ldsd2*)(win + WB_R + R_G + NX);
+            const d2 b0 = bq[0], b1 = bq[1], g0 = gq[0], g1 = gq[1];
+            bvv[0] = b0.x; bvv[1] = b0.y; bvv[2] = b1.x; bvv[3] = b1.y;
+            guw[0] = g0.x; guw[1] = g0.y; guw[2] = g1.x; guw[3] = g1.y;
         }
+#pragma unroll
+        for (int i = 0; i < NU; ++i) kk[i] = bc_k[FR * i];
 #pragma unroll
         for (int l = 0; l < NX; ++l) row[l] = bc_row[l * bc_str];
         const ldsd2* pc = (const ldsd2*)(win + F_PC);
