@@ -489,6 +489,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // lane r < 10: row r of A~ x + b~ (x_{k+1}); r = 10..13: row of K x + k_ff (u_k); r = 14..16:
     // (C x)_{r-14}; kind 0 (initial iterate, u = 0): rows r < 10 of A x + c from the stage record.
     // Factor rows of nodes < PD come from fsave (written late in the backward sweeps).
+    double chain = 0.0;  // p_{k+1} of the corrector sweep in lanes 0..9
     auto fw_stage = [&](auto Kc, int k, const int lane) {
         const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 17;
         const int fcj = fc ? lane - 14 : 0;
@@ -496,7 +497,6 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         ldsd* const dxo = K == 0 ? s.dx : s.dxc;
         ldsd* const duo = K == 4 ? s.duc : s.dua;
         ldsd* const cxo = K == 4 ? s.cxc : s.cxa;
-        const ldsd2* xp = (const ldsd2*)(dxo + k * NX);
         double row[NX], off;
         if constexpr (K == 0) {
             const ldsd* rp = fx ? win + R_AB + lane : fc ? win + R_CT + fcj * 10 : win;
@@ -516,6 +516,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             }
             off = *(lane < 14 ? fk + lane * FR + 10 : s.zero);
         }
+        const ldsd2* xp = (const ldsd2*)(dxo + k * NX);
         d2 xv[NX / 2];  // the chain input x_k, read after everything else
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) xv[l] = xp[l];
@@ -526,10 +527,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
             a0 = fma(row[2 * l], xv[l].x, a0);
             a1 = fma(row[2 * l + 1], xv[l].y, a1);
         }
+        const double z = a0 + a1;
         ldsd* dst = fc ? cxo + k * NS + fcj
                   : (k < N && fx) ? dxo + (k + 1) * NX + lane
                   : (K != 0 && k < N && fu) ? duo + k * NU + lane - NX : s.junk;
-        *dst = a0 + a1;
+        *dst = z;
     };
 
     // ------------------------------------------------------------ backward stage, factor
@@ -698,14 +700,13 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         for (int i = 0; i < NU; ++i) mu_[i] = lane == NX + i ? 1.0 : 0.0;
         const int bx = fx ? lane : 0;
         const unsigned bc_st = lane < 14 ? lane * FR + 10 : F_J;  // b~ rows (lanes < 10), k_ff rows (lanes 10..13)
-        ldsd* const bc_p = fx ? s.p + lane : s.junk;
         const int k = N - q;
         FSTAMP(7, mfx);
         double off = *bc_g;
 #pragma unroll
         for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * bc_ct[10 * j];
         if constexpr (FIRST) {  // p_N = g_N + sum_j gamma_j C_j^T
-            *bc_p = off;
+            chain = off;
             return;
         }
         // ---- every LDS read of the stage first (one round trip), the chain input p_{k+1} last
@@ -731,23 +732,22 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
         }
         const double cb = win[WB_R + R_C + bx], B0 = win[WB_R + 100 + bx], B1 = win[WB_R + 110 + bx];
         const double B2 = win[WB_R + 120 + bx], B3 = win[WB_R + 130 + bx];
-        const ldsd2* pp = (const ldsd2*)s.p;
-        d2 pv[NX / 2];
+        // the chain input p_{k+1}: lanes 0..9 of the register chain, broadcast through scalar registers
+        double pv[NX];
 #pragma unroll
-        for (int l = 0; l < NX / 2; ++l) pv[l] = pp[l];
-        __builtin_amdgcn_sched_barrier(0);
-        FSTAMP(13, pv[4].y + B3 + row[9] + Lv[4].y + pcv[4].y + kk[3]);
+        for (int l = 0; l < NX; ++l) pv[l] = rdlane(chain, l);
+        FSTAMP(13, pv[9] + B3 + row[9] + Lv[4].y + pcv[4].y + kk[3]);
         // g~_u (uniform) and the per-lane offset of the chain
 #pragma unroll
         for (int i = 0; i < NU; ++i) off += kk[i] * (guw[i] + bvv[i]) + mu_[i] * bvv[i];
         double a0 = off, a1 = 0.0;
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) {
-            a0 = fma(row[2 * l], pcv[l].x + pv[l].x, a0);
-            a1 = fma(row[2 * l + 1], pcv[l].y + pv[l].y, a1);
+            a0 = fma(row[2 * l], pcv[l].x + pv[2 * l], a0);
+            a1 = fma(row[2 * l + 1], pcv[l].y + pv[2 * l + 1], a1);
         }
         const double z = a0 + a1;
-        *bc_p = z;
+        chain = z;
         FSTAMP(14, z);
         // off the chain: k_ff, b~
         const double z0 = rdlane(z, 10), z1 = rdlane(z, 11), z2 = rdlane(z, 12), z3 = rdlane(z, 13);
