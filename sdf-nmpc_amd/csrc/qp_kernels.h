@@ -32,7 +32,7 @@ struct QpArgs {
 constexpr int QP_REC = 300;   // stage record: [A B | c | g | C^T | H upper | 0]            (rti_qp.hip)
 constexpr int QP_FREC = 190;  // factor record: [A~|b~ | K|k_ff (rows of 12) | chol(R^) (1/diag) | P_{k+1} c_k | 2 junk]
 constexpr int QP_RING = 3;    // stream positions in flight per wavefront
-constexpr int QP_SLOT = 6;    // 64-double loads per stream position (committed LDS window = 384 doubles)
+constexpr int QP_SLOT = 5;    // 64-double loads per stream position (committed LDS window = 320 doubles)
 
 // global workspace per instance: stage records and factor records for nodes 0..N
 __host__ __device__ inline size_t qp_work_doubles(int N) { return (size_t)(N + 1) * (QP_REC + QP_FREC); }
@@ -47,7 +47,7 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
            + 2 * qp_even(N1 * 3)            // cxa, cxc
            + QP_SLOT * 64                   // committed stream window
            + QP_RING * 168                  // [A~|b~ K|k_ff] of nodes 0..RING-1 (written late in a backward sweep)
-           + 16 + 48 + 2                    // corrector p; zero rows; junk
+           + 48 + 2                         // zero rows; junk
            + qp_even((size_t)N * 4) + qp_even(N1 * 3) + qp_even(N1)  // u, h, s_k
            + 2 * qp_even(N1 * 3)            // soft-row folds (w, gamma)
            + 2 * qp_even((size_t)N * 4)     // box terms (diag, v)

@@ -65,18 +65,19 @@ constexpr int SLOT = QP_SLOT, PD = QP_RING;
 // Window of one stream position per sweep kind: n_loads(K) loads of 64 consecutive doubles (lanes
 // clamped to the record), load j landing at window offset 64 j:
 //   0 initial forward     R[0, 256)                    AB, c, C^T in place
-//   1 backward factor     R[0, 384)                    the stage record in place; [R_Z, 384) reads 0
+//   1 backward factor     R[0, 320)                    the stage record in place; [R_Z, 320) reads 0
 //   2, 4 forward          F[0, 192) | R[164, 228)      factor rows at 0, C^T at WF_CT
-//   3 backward corrector  F[0, 256) | R[100, 228)      factor record at 0, R[i] at WB_R + i (i >= 100)
-constexpr int WF_CT = 192, WB_R = 256 - 100;
+//   3 backward corrector  F[0, 192) | R[100, 228)      factor record at 0, R[i] at WB_R + i (i >= 100)
+constexpr int WF_CT = 192, WB_R = 192 - 100;
 static_assert((WB_R + R_G + NX) % 2 == 0, "g~_u block of the corrector window is 16-byte aligned");
-__host__ __device__ constexpr int n_loads(int K) { return (K == 1 || K == 3) ? 6 : 4; }
-__host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K == 4) ? j < 3 : K == 3 ? j < 4 : false; }
+__host__ __device__ constexpr int n_loads(int K) { return (K == 1 || K == 3) ? 5 : 4; }
+__host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K == 3 || K == 4) ? j < 3 : false; }
 __host__ __device__ constexpr int load_at(int K, int j) {
-    return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 4 ? 64 * j : 100 + 64 * (j - 4));
+    return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 3 ? 64 * j : 100 + 64 * (j - 3));
 }
-static_assert(FREC == F_J + 2 && FREC % 2 == 0 && F_FW <= WF_CT && PD == 3 && SLOT == 6, "record layout");
-static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT, "window layout");
+static_assert(FREC == F_J + 2 && FREC % 2 == 0 && F_FW <= WF_CT && FREC <= 192 && PD == 3 && SLOT == 5, "record layout");
+static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT && WB_R + 228 <= 64 * SLOT && R_Z < 64 * SLOT,
+              "window layout");
 // IPM starting point and step fraction (the kernel waits for its slowest instance, so these were
 // chosen on the worst case over seeds / x0 spreads with the C restatement, oracle/qp_ipm.c):
 // t = max(row value, T0); lambda = L0 on the box rows and max(L0, LC s_k zl_j) on the four rows of
@@ -193,7 +194,6 @@ struct Smem {
     ldsd *cxa, *cxc;               // C dx of the affine / corrector solution
     ldsd* win;                     // committed stream window
     ldsd* fsave;                   // [A~|b~ K|k_ff] of nodes < PD
-    ldsd* p;                       // corrector Riccati vector p (the factor sweep keeps p in registers)
     ldsd *zero, *junk;             // 48 doubles that stay 0 (zero rows for strided reads); a store sink
     ldsd *uu, *hv, *skv;           // u (box constants), h, cost scaling per node
     ldsd *fw, *fg, *bd, *bv;       // soft folds [N+1][3] (w, gamma), box terms [N][4] (diag, v)
@@ -210,7 +210,7 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubl
     s.du = take(N * NU); s.dua = take(N * NU); s.duc = take(N * NU);
     s.cxa = take(N1 * NS); s.cxc = take(N1 * NS);
     s.win = take(SLOT * 64); s.fsave = take(PD * F_FW);
-    s.p = take(16); s.zero = take(48); s.junk = take(2);
+    s.zero = take(48); s.junk = take(2);
     s.uu = take(N * NU); s.hv = take(N1 * NS); s.skv = take(N1);
     s.fw = take(N1 * NS); s.fg = take(N1 * NS); s.bd = take(N * NU); s.bv = take(N * NU);
     s.cst = take(20);

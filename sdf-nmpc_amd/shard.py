@@ -30,7 +30,7 @@ LDS_PER_CU = 160 * 1024
 def qp_lds_bytes(N: int) -> int:
     even = lambda n: (n + 1) & ~1  # noqa: E731
     N1, m = N + 1, 8 * N + 12 * (N + 1)
-    d = (2 * even(m) + 2 * even(N1 * 10) + 3 * even(N * 4) + 2 * even(N1 * 3) + 6 * 64 + 3 * 168 + 16 + 48 + 2
+    d = (2 * even(m) + 2 * even(N1 * 10) + 3 * even(N * 4) + 2 * even(N1 * 3) + 5 * 64 + 3 * 168 + 48 + 2
          + even(N * 4) + even(N1 * 3) + even(N1) + 2 * even(N1 * 3) + 2 * even(N * 4) + 20)
     return 8 * d
 
