@@ -75,6 +75,10 @@ __host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K ==
 __host__ __device__ constexpr int load_at(int K, int j) {
     return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 3 ? 64 * j : 100 + 64 * (j - 3));
 }
+// extent of each record a sweep kind reads (lanes past it load the last needed element again, so a
+// 64-lane load touches only the cache lines the stage uses)
+__host__ __device__ constexpr int f_end(int K) { return (K == 2 || K == 4) ? F_FW : F_J; }
+__host__ __device__ constexpr int r_end(int K) { return K == 1 ? REC : R_CT + 30; }
 static_assert(FREC == F_J + 2 && FREC % 2 == 0 && F_FW <= WF_CT && FREC <= 192 && PD == 3 && SLOT == 5, "record layout");
 static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT && WB_R + 228 <= 64 * SLOT && R_Z < 64 * SLOT,
               "window layout");
@@ -469,8 +473,8 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
         for (int j = 0; j < n_loads(KI); ++j) {
             const int e = load_at(KI, j) + lane;
-            if (load_f(KI, j)) rs[j] = fb[e < FREC ? e : FREC - 1];
-            else rs[j] = rb[e < REC ? e : REC - 1];
+            if (load_f(KI, j)) rs[j] = fb[e < f_end(KI) ? e : f_end(KI) - 1];
+            else rs[j] = rb[e < r_end(KI) ? e : r_end(KI) - 1];
         }
     };
     auto commit = [&](auto Kc, const double* rs) {
