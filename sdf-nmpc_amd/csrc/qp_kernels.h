@@ -29,8 +29,8 @@ struct QpArgs {
     int sdf_row_patch;  // rti_qp_kernel: copy J_h[.][2] into the records' C^T row 2 before the sweeps
 };
 
-constexpr int QP_REC = 300;   // stage record: [A B | c | g | C^T | H upper | 0]            (rti_qp.hip)
-constexpr int QP_FREC = 190;  // factor record: [A~|b~ | K|k_ff (rows of 12) | chol(R^) (1/diag) | P_{k+1} c_k | 2 junk]
+constexpr int QP_REC = 304;   // stage record: [A B | c | g | C^T | H upper | 0 ..] (128-B rows) (rti_qp.hip)
+constexpr int QP_FREC = 192;  // factor record: [A~|b~ | K|k_ff (rows of 12) | chol(R^) (1/diag) | P_{k+1} c_k | 4 junk]
 constexpr int QP_RING = 3;    // stream positions in flight per wavefront
 constexpr int QP_SLOT = 5;    // 64-double loads per stream position (committed LDS window = 320 doubles)
 

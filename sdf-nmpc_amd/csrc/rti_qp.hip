@@ -79,7 +79,7 @@ __host__ __device__ constexpr int load_at(int K, int j) {
 // 64-lane load touches only the cache lines the stage uses)
 __host__ __device__ constexpr int f_end(int K) { return (K == 2 || K == 4) ? F_FW : F_J; }
 __host__ __device__ constexpr int r_end(int K) { return K == 1 ? REC : R_CT + 30; }
-static_assert(FREC == F_J + 2 && FREC % 2 == 0 && F_FW <= WF_CT && FREC <= 192 && PD == 3 && SLOT == 5, "record layout");
+static_assert(FREC == F_J + 4 && (REC * 8) % 128 == 0 && (FREC * 8) % 128 == 0 && F_FW <= WF_CT && FREC <= 192 && PD == 3 && SLOT == 5, "record layout");
 static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT && WB_R + 228 <= 64 * SLOT && R_Z < 64 * SLOT,
               "window layout");
 // IPM starting point and step fraction (the kernel waits for its slowest instance, so these were
