@@ -67,20 +67,21 @@ constexpr int SLOT = QP_SLOT, PD = QP_RING;
 //   0 initial forward     R[0, 256)                    AB, c, C^T in place
 //   1 backward factor     R[0, 320)                    the stage record in place; [R_Z, 320) reads 0
 //   2, 4 forward          F[0, 192) | R[164, 228)      factor rows at 0, C^T at WF_CT
-//   3 backward corrector  F[0, 192) | R[100, 228)      factor record at 0, R[i] at WB_R + i (i >= 100)
-constexpr int WF_CT = 192, WB_R = 192 - 100;
+//   3 backward corrector  F[0, 192) | R[96, 224)       factor record at 0, R[i] at WB_R + i (i >= 96; loads
+//                                                      start on a 128-byte line)
+constexpr int WF_CT = 192, WB_R = 192 - 96;
 static_assert((WB_R + R_G + NX) % 2 == 0, "g~_u block of the corrector window is 16-byte aligned");
 __host__ __device__ constexpr int n_loads(int K) { return (K == 1 || K == 3) ? 5 : 4; }
 __host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K == 3 || K == 4) ? j < 3 : false; }
 __host__ __device__ constexpr int load_at(int K, int j) {
-    return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 3 ? 64 * j : 100 + 64 * (j - 3));
+    return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 3 ? 64 * j : 96 + 64 * (j - 3));
 }
 // extent of each record a sweep kind reads (lanes past it load the last needed element again, so a
 // 64-lane load touches only the cache lines the stage uses)
 __host__ __device__ constexpr int f_end(int K) { return (K == 2 || K == 4) ? F_FW : F_J; }
 __host__ __device__ constexpr int r_end(int K) { return K == 1 ? REC : R_CT + 30; }
 static_assert(FREC == F_J + 4 && (REC * 8) % 128 == 0 && (FREC * 8) % 128 == 0 && F_FW <= WF_CT && FREC <= 192 && PD == 3 && SLOT == 5, "record layout");
-static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT && WB_R + 228 <= 64 * SLOT && R_Z < 64 * SLOT,
+static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT && WB_R + 96 + 128 <= 64 * SLOT && (96 * 8) % 128 == 0 && R_Z < 64 * SLOT,
               "window layout");
 // IPM starting point and step fraction (the kernel waits for its slowest instance, so these were
 // chosen on the worst case over seeds / x0 spreads with the C restatement, oracle/qp_ipm.c):
