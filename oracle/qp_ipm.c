@@ -28,7 +28,7 @@ enum { NX = 10, NU = 4, NS = 3, NW = 14 };
 
 typedef struct {
     double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3], lm, tol;
-    int max_iter, cost_scaling, lm_scaling;
+    int max_iter, cost_scaling, lm_scaling, nseg;
     double t0, l0, lc, tau_lo, tau_hi;  /* starting point / step fraction (rti_qp.hip's QP_T0 ... QP_TAU_HI) */
 } qp_opts_c;
 
@@ -78,6 +78,9 @@ typedef struct {
     stage_t* st;
     double x0[NX];                /* dx_0 */
     double *P, *p, *K, *kf;       /* Riccati workspace: (N+1) x NX x NX, (N+1) x NX, N x NU x NX, N x NU */
+    double* G;                    /* N x NU x NX: terminal-multiplier gains of the segmented solve */
+    int nseg;                     /* segments of the partitioned Riccati (1: the serial recursion) */
+    double seg_dev;               /* max relative gap between a segment's own x_b and the coupled one */
 } ipm_t;
 
 static void rows_at(const ipm_t* Q, const double* dx, const double* du, const double* sl, const double* su, double* v) {
@@ -99,35 +102,187 @@ static void rows_at(const ipm_t* Q, const double* dx, const double* du, const do
         }
 }
 
+/* Stage data of the Newton system at node k: the state block with the eliminated slack pairs folded
+ * in (Qx, qx), and the input block with the box terms (R0, ru). */
+static void stage_terms(const ipm_t* Q, int k, const double* sig, const double* v, double* Qx, double* qx, double* R0,
+                        double* S0, double* ru, double* bd) {
+    const int N = Q->N;
+    const qp_opts_c* o = Q->o;
+    const stage_t* S = &Q->st[k];
+    for (int a = 0; a < NX; ++a) {
+        for (int b = 0; b < NX; ++b) Qx[a * NX + b] = S->H[a][b];
+        qx[a] = S->g[a];
+    }
+    for (int j = 0; j < NS; ++j) {  /* eliminated slack pair */
+        const int r0 = 8 * N + 12 * k + 4 * j;
+        const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
+        const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
+        /* written without the cancellation of Hl - sig (sig -> inf on an active row); equal to
+         * sig (Hl - sig) / Hl and -(v + sig gl / Hl) + ... */
+        const double fw = sig[r0] * (Zs + sig[r0 + 2]) / Hl + sig[r0 + 1] * (Zs + sig[r0 + 3]) / Hu;
+        const double fg = -(v[r0] * (Zs + sig[r0 + 2]) + sig[r0] * (zs - v[r0 + 2])) / Hl +
+                          (v[r0 + 1] * (Zs + sig[r0 + 3]) + sig[r0 + 1] * (zs - v[r0 + 3])) / Hu;
+        for (int a = 0; a < NX; ++a) {
+            for (int b = 0; b < NX; ++b) Qx[a * NX + b] += fw * S->C[j][a] * S->C[j][b];
+            qx[a] += fg * S->C[j][a];
+        }
+    }
+    if (k == N) return;
+    for (int i = 0; i < NU; ++i) {
+        for (int j = 0; j < NU; ++j) R0[i * NU + j] = S->H[NX + i][NX + j];
+        bd[i] = sig[8 * k + i] + sig[8 * k + 4 + i];
+        R0[i * NU + i] += bd[i];
+        for (int b = 0; b < NX; ++b) S0[i * NX + b] = S->H[NX + i][b];
+        ru[i] = S->g[NX + i] - v[8 * k + i] + v[8 * k + 4 + i];
+    }
+}
+
+/* One backward Riccati stage k < N from the cost-to-go [P1 | p1] of node k + 1:
+ * R^ = R0 + B^T P1 B (Cholesky factor into Rc), [K | kf] = -R^-1 ([S0 | ru] + B^T [P1 A | P1 c + p1]),
+ * Ab = A + B K, and [Pk | pk] in the Joseph form [I;K]^T Hh [I;K] + Ab^T P1 Ab (a sum of PSD terms). */
+static int ric_stage(const ipm_t* Q, int k, const double* Qx, const double* qx, const double* R0, const double* S0,
+                     const double* ru, const double* bd, const double* P1, const double* p1, double* Pk, double* pk, double* Kk,
+                     double* kf, double* Ab, double* Rc) {
+    const stage_t* S = &Q->st[k];
+    /* PA = P A, PB = P B, Pc = P c + p */
+    double PA[NX * NX], PB[NX * NU], Pc[NX];
+    for (int a = 0; a < NX; ++a) {
+        for (int b = 0; b < NX; ++b) {
+            double s = 0.0;
+            for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->A[l][b];
+            PA[a * NX + b] = s;
+        }
+        for (int b = 0; b < NU; ++b) {
+            double s = 0.0;
+            for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->Bm[l][b];
+            PB[a * NU + b] = s;
+        }
+        double s = p1[a];
+        for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->c[l];
+        Pc[a] = s;
+    }
+    double* Rm = Rc;
+    double Sm[NU * NX], r[NU];
+    for (int i = 0; i < NU; ++i) {
+        for (int j = 0; j < NU; ++j) {
+            double s = S->H[NX + i][NX + j];
+            for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * PB[l * NU + j];
+            Rm[i * NU + j] = s;
+        }
+        Rm[i * NU + i] += bd[i];
+        for (int b = 0; b < NX; ++b) {
+            double s = S0[i * NX + b];
+            for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * PA[l * NX + b];
+            Sm[i * NX + b] = s;
+        }
+        double s = ru[i];
+        for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * Pc[l];
+        r[i] = s;
+    }
+    if (chol(NU, Rm)) return 1;
+    for (int b = 0; b < NX; ++b) {  /* K = -R^-1 S, column by column */
+        double col[NU];
+        for (int i = 0; i < NU; ++i) col[i] = Sm[i * NX + b];
+        chol_solve(NU, Rm, col);
+        for (int i = 0; i < NU; ++i) Kk[i * NX + b] = -col[i];
+    }
+    for (int i = 0; i < NU; ++i) kf[i] = r[i];
+    chol_solve(NU, Rm, kf);
+    for (int i = 0; i < NU; ++i) kf[i] = -kf[i];
+    {   /* P = [I;K]^T Hh [I;K] + Ab^T P1 Ab (sum of PSD terms), Ab = A + B K */
+        double PB1[NX];
+        for (int a = 0; a < NX; ++a)
+            for (int b = 0; b < NX; ++b) {
+                double s = S->A[a][b];
+                for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * Kk[i * NX + b];
+                Ab[a * NX + b] = s;
+            }
+        double xb[NX];  /* B kf + c */
+        for (int a = 0; a < NX; ++a) {
+            double s = S->c[a];
+            for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * kf[i];
+            xb[a] = s;
+        }
+        for (int a = 0; a < NX; ++a) {
+            double s = p1[a];
+            for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * xb[l];
+            PB1[a] = s;
+        }
+        double PAb[NX * NX];
+        for (int a = 0; a < NX; ++a)
+            for (int b = 0; b < NX; ++b) {
+                double s = 0.0;
+                for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * Ab[l * NX + b];
+                PAb[a * NX + b] = s;
+            }
+        double KR[NX * NU];  /* S0^T + K^T R0 : [NX][NU] */
+        for (int a = 0; a < NX; ++a)
+            for (int j = 0; j < NU; ++j) {
+                double s = S0[j * NX + a];
+                for (int i = 0; i < NU; ++i) s += Kk[i * NX + a] * R0[i * NU + j];
+                KR[a * NU + j] = s;
+            }
+        for (int a = 0; a < NX; ++a) {
+            for (int b = 0; b < NX; ++b) {
+                double s = Qx[a * NX + b];
+                for (int l = 0; l < NX; ++l) s += Ab[l * NX + a] * PAb[l * NX + b];
+                for (int j = 0; j < NU; ++j) s += KR[a * NU + j] * Kk[j * NX + b] + Kk[j * NX + a] * S0[j * NX + b];
+                Pk[a * NX + b] = s;
+            }
+            double s = qx[a];
+            for (int i = 0; i < NU; ++i) s += Kk[i * NX + a] * ru[i] + KR[a * NU + i] * kf[i];
+            for (int l = 0; l < NX; ++l) s += Ab[l * NX + a] * PB1[l];
+            pk[a] = s;
+        }
+    }
+    return 0;
+}
+
+/* slacks of node k from the eliminated rows at the state xk */
+static void node_slacks(const ipm_t* Q, int k, const double* sig, const double* v, const double* xk, double* sl,
+                        double* su) {
+    const int N = Q->N;
+    const qp_opts_c* o = Q->o;
+    const stage_t* S = &Q->st[k];
+    for (int j = 0; j < NS; ++j) {
+        const int r0 = 8 * N + 12 * k + 4 * j;
+        const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
+        const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
+        const double gl = zs - v[r0] - v[r0 + 2], gu = zs - v[r0 + 1] - v[r0 + 3];
+        double cx = 0.0;
+        for (int l = 0; l < NX; ++l) cx += S->C[j][l] * xk[l];
+        sl[k * NS + j] = -(gl + sig[r0] * cx) / Hl;
+        su[k * NS + j] = -(gu - sig[r0 + 1] * cx) / Hu;
+    }
+}
+
+/* u_k = K x_k + kf - G lam,  x_{k+1} = A x_k + B u_k + c  (G = NULL: no terminal multiplier) */
+static void fwd_stage(const ipm_t* Q, int k, const double* Kk, const double* kf, const double* G, const double* lam,
+                      const double* xk, double* uk, double* xn) {
+    const stage_t* S = &Q->st[k];
+    for (int i = 0; i < NU; ++i) {
+        double s = kf[i];
+        for (int l = 0; l < NX; ++l) s += Kk[i * NX + l] * xk[l];
+        if (G)
+            for (int l = 0; l < NX; ++l) s -= G[i * NX + l] * lam[l];
+        uk[i] = s;
+    }
+    for (int a = 0; a < NX; ++a) {
+        double s = S->c[a];
+        for (int l = 0; l < NX; ++l) s += S->A[a][l] * xk[l];
+        for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * uk[i];
+        xn[a] = s;
+    }
+}
+
 /* The Newton system as an LQR in the new iterate: Hessian H + D^T diag(sig) D, gradient g - D^T v.
  * Soft slacks are eliminated per row pair (a rank-3 fold on the node's state block), box terms land
  * on the input block.  Writes the solution (dx, du, sl, su); returns nonzero on a failed factorisation. */
 static int lqr(ipm_t* Q, const double* sig, const double* v, double* dx, double* du, double* sl, double* su) {
     const int N = Q->N;
-    const qp_opts_c* o = Q->o;
     for (int k = N; k >= 0; --k) {
-        const stage_t* S = &Q->st[k];
-        double Qx[NX * NX], qx[NX];
-        for (int a = 0; a < NX; ++a) {
-            for (int b = 0; b < NX; ++b) Qx[a * NX + b] = S->H[a][b];
-            qx[a] = S->g[a];
-        }
-        for (int j = 0; j < NS; ++j) {  /* eliminated slack pair */
-            const int r0 = 8 * N + 12 * k + 4 * j;
-            const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
-            const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
-            const double gl = zs - v[r0] - v[r0 + 2], gu = zs - v[r0 + 1] - v[r0 + 3];
-            /* written without the cancellation of Hl - sig (sig -> inf on an active row); equal to
-             * sig (Hl - sig) / Hl and -(v + sig gl / Hl) + ... */
-            (void)gl; (void)gu;
-            const double fw = sig[r0] * (Zs + sig[r0 + 2]) / Hl + sig[r0 + 1] * (Zs + sig[r0 + 3]) / Hu;
-            const double fg = -(v[r0] * (Zs + sig[r0 + 2]) + sig[r0] * (zs - v[r0 + 2])) / Hl +
-                              (v[r0 + 1] * (Zs + sig[r0 + 3]) + sig[r0 + 1] * (zs - v[r0 + 3])) / Hu;
-            for (int a = 0; a < NX; ++a) {
-                for (int b = 0; b < NX; ++b) Qx[a * NX + b] += fw * S->C[j][a] * S->C[j][b];
-                qx[a] += fg * S->C[j][a];
-            }
-        }
+        double Qx[NX * NX], qx[NX], R0[NU * NU], S0[NU * NX], ru[NU], bd[NU], Rc[NU * NU], Ab[NX * NX];
+        stage_terms(Q, k, sig, v, Qx, qx, R0, S0, ru, bd);
         double* Pk = Q->P + (size_t)k * NX * NX;
         double* pk = Q->p + (size_t)k * NX;
         if (k == N) {
@@ -135,137 +290,222 @@ static int lqr(ipm_t* Q, const double* sig, const double* v, double* dx, double*
             memcpy(pk, qx, sizeof qx);
             continue;
         }
-        const double* P1 = Q->P + (size_t)(k + 1) * NX * NX;
-        const double* p1 = Q->p + (size_t)(k + 1) * NX;
-        /* PA = P A, PB = P B, Pc = P c + p */
-        double PA[NX * NX], PB[NX * NU], Pc[NX];
-        for (int a = 0; a < NX; ++a) {
-            for (int b = 0; b < NX; ++b) {
-                double s = 0.0;
-                for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->A[l][b];
-                PA[a * NX + b] = s;
-            }
-            for (int b = 0; b < NU; ++b) {
-                double s = 0.0;
-                for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->Bm[l][b];
-                PB[a * NU + b] = s;
-            }
-            double s = p1[a];
-            for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * S->c[l];
-            Pc[a] = s;
-        }
-        double Rm[NU * NU], Sm[NU * NX], r[NU];
-        for (int i = 0; i < NU; ++i) {
-            for (int j = 0; j < NU; ++j) {
-                double s = S->H[NX + i][NX + j];
-                for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * PB[l * NU + j];
-                Rm[i * NU + j] = s;
-            }
-            Rm[i * NU + i] += sig[8 * k + i] + sig[8 * k + 4 + i];
-            for (int b = 0; b < NX; ++b) {
-                double s = S->H[NX + i][b];
-                for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * PA[l * NX + b];
-                Sm[i * NX + b] = s;
-            }
-            double s = S->g[NX + i] - v[8 * k + i] + v[8 * k + 4 + i];
-            for (int l = 0; l < NX; ++l) s += S->Bm[l][i] * Pc[l];
-            r[i] = s;
-        }
-        if (chol(NU, Rm)) return 1;
-        double* Kk = Q->K + (size_t)k * NU * NX;
-        double* kf = Q->kf + (size_t)k * NU;
-        for (int b = 0; b < NX; ++b) {  /* K = -R^-1 S, column by column */
-            double col[NU];
-            for (int i = 0; i < NU; ++i) col[i] = Sm[i * NX + b];
-            chol_solve(NU, Rm, col);
-            for (int i = 0; i < NU; ++i) Kk[i * NX + b] = -col[i];
-        }
-        for (int i = 0; i < NU; ++i) kf[i] = r[i];
-        chol_solve(NU, Rm, kf);
-        for (int i = 0; i < NU; ++i) kf[i] = -kf[i];
-        {   /* P = [I;K]^T Hh [I;K] + Ab^T P1 Ab (sum of PSD terms), Ab = A + B K */
-            double Ab[NX * NX], R0[NU * NU], S0[NU * NX], ru[NU], PB1[NX];
-            for (int i = 0; i < NU; ++i) {
-                for (int j = 0; j < NU; ++j) R0[i * NU + j] = S->H[NX + i][NX + j];
-                R0[i * NU + i] += sig[8 * k + i] + sig[8 * k + 4 + i];
-                for (int b = 0; b < NX; ++b) S0[i * NX + b] = S->H[NX + i][b];
-                ru[i] = S->g[NX + i] - v[8 * k + i] + v[8 * k + 4 + i];
-            }
-            for (int a = 0; a < NX; ++a)
-                for (int b = 0; b < NX; ++b) {
-                    double s = S->A[a][b];
-                    for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * Kk[i * NX + b];
-                    Ab[a * NX + b] = s;
-                }
-            double xb[NX];  /* B kf + c */
-            for (int a = 0; a < NX; ++a) {
-                double s = S->c[a];
-                for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * kf[i];
-                xb[a] = s;
-            }
-            for (int a = 0; a < NX; ++a) {
-                double s = p1[a];
-                for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * xb[l];
-                PB1[a] = s;
-            }
-            double PAb[NX * NX];
-            for (int a = 0; a < NX; ++a)
-                for (int b = 0; b < NX; ++b) {
-                    double s = 0.0;
-                    for (int l = 0; l < NX; ++l) s += P1[a * NX + l] * Ab[l * NX + b];
-                    PAb[a * NX + b] = s;
-                }
-            double KR[NX * NU];  /* S0^T + K^T R0 : [NX][NU] */
-            for (int a = 0; a < NX; ++a)
-                for (int j = 0; j < NU; ++j) {
-                    double s = S0[j * NX + a];
-                    for (int i = 0; i < NU; ++i) s += Kk[i * NX + a] * R0[i * NU + j];
-                    KR[a * NU + j] = s;
-                }
-            for (int a = 0; a < NX; ++a) {
-                for (int b = 0; b < NX; ++b) {
-                    double s = Qx[a * NX + b];
-                    for (int l = 0; l < NX; ++l) s += Ab[l * NX + a] * PAb[l * NX + b];
-                    for (int j = 0; j < NU; ++j) s += KR[a * NU + j] * Kk[j * NX + b] + Kk[j * NX + a] * S0[j * NX + b];
-                    Pk[a * NX + b] = s;
-                }
-                double s = qx[a];
-                for (int i = 0; i < NU; ++i) s += Kk[i * NX + a] * ru[i] + KR[a * NU + i] * kf[i];
-                for (int l = 0; l < NX; ++l) s += Ab[l * NX + a] * PB1[l];
-                pk[a] = s;
-            }
-        }
+        if (ric_stage(Q, k, Qx, qx, R0, S0, ru, bd, Pk + NX * NX, pk + NX, Pk, pk, Q->K + (size_t)k * NU * NX,
+                      Q->kf + (size_t)k * NU, Ab, Rc))
+            return 1;
     }
     /* forward: dx_0 fixed, du = K dx + k_ff, dx+ = A dx + B du + c; slacks from the eliminated rows */
     memcpy(dx, Q->x0, sizeof(double) * NX);
     for (int k = 0; k <= N; ++k) {
-        const stage_t* S = &Q->st[k];
-        const double* xk = dx + (size_t)k * NX;
-        for (int j = 0; j < NS; ++j) {
-            const int r0 = 8 * N + 12 * k + 4 * j;
-            const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
-            const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
-            const double gl = zs - v[r0] - v[r0 + 2], gu = zs - v[r0 + 1] - v[r0 + 3];
-            double cx = 0.0;
-            for (int l = 0; l < NX; ++l) cx += S->C[j][l] * xk[l];
-            sl[k * NS + j] = -(gl + sig[r0] * cx) / Hl;
-            su[k * NS + j] = -(gu - sig[r0 + 1] * cx) / Hu;
-        }
+        node_slacks(Q, k, sig, v, dx + (size_t)k * NX, sl, su);
         if (k == N) break;
-        const double* Kk = Q->K + (size_t)k * NU * NX;
-        const double* kf = Q->kf + (size_t)k * NU;
-        double* uk = du + (size_t)k * NU;
-        for (int i = 0; i < NU; ++i) {
-            double s = kf[i];
-            for (int l = 0; l < NX; ++l) s += Kk[i * NX + l] * xk[l];
-            uk[i] = s;
+        fwd_stage(Q, k, Q->K + (size_t)k * NU * NX, Q->kf + (size_t)k * NU, NULL, NULL, dx + (size_t)k * NX,
+                  du + (size_t)k * NU, dx + (size_t)(k + 1) * NX);
+    }
+    return 0;
+}
+
+/* ---- partitioned (parallel-in-time) Riccati: the scheme of csrc/rti_qp_seg.hip, in its order of
+ * operations.  The nodes split into P segments [a_i, a_{i+1}) (a_i = i (N+1) / P; the last one holds the
+ * terminal node).  Every segment i < P-1 runs the backward recursion with a zero cost-to-go at its end
+ * b = a_{i+1} and carries, besides its factors, the element (J, eta, Phi, beta, C) of its conditional value
+ * function (the Riccati form of the parallel LQ element of Sarkka & Garcia-Fernandez):
+ *     x_b = Phi x_a + beta - C lam_b,    lam_a = J x_a + eta + Phi^T lam_b,
+ * Phi the product of the closed-loop matrices A~, beta the closed-loop offsets, C the sum of
+ * Z_k R^_k^-1 Z_k^T over Z_k = Phi_{k+1->b} B_k, and lam_b = P_b x_b + p_b the costate at b.  With the true
+ * cost-to-go, the input of node k is u_k = K_k x_k + kf_k - G_k lam_b, G_k = R^_k^-1 Z_k^T.
+ * Coupling, serial over the segments: P_b = L L^T, S = I + L^T C L = U U^T, V = L U^-T (so Y = V V^T =
+ * (I + P_b C)^-1 P_b), X = V^T Phi,  z = V^T beta + U^-1 L^-1 p_b,
+ *     P_a = J + X^T X,   p_a = eta + X^T z              (sums of PSD terms)
+ *     lam_b = Lam x_a + lam0,  Lam = V X, lam0 = V z    (the costate offset by triangular solves)
+ *     x_b   = M x_a + m,       M = Phi - C Lam, m = beta - C lam0
+ * Measured on the C3 bench problem (tools/ipm_sweep.py, 4 seeds x 3 RTI steps x 256 instances):
+ * identical iteration counts to the serial recursion at P = 4 and 8.  Forming lam0 as Y (beta - C p_b)
+ * + p_b instead (cancellation of p_b against Y C p_b when C P_b is large) took the worst case from 13 to
+ * 34 (P = 4) / 100 iterations (P = 8); an explicit W = V U^-1 L^-1 for the p_b term to 15 / 24. */
+static int seg_a(int N, int P, int i) { return i * (N + 1) / P; }
+
+static void lsolve(const double* L, double* x) {  /* x <- L^-1 x (L lower) */
+    for (int i = 0; i < NX; ++i) {
+        double v = x[i];
+        for (int k = 0; k < i; ++k) v -= L[i * NX + k] * x[k];
+        x[i] = v / L[i * NX + i];
+    }
+}
+
+typedef struct {  /* a segment's element and coupling matrices */
+    double Phi[NX * NX], C[NX * NX], beta[NX], L[NX * NX], U[NX * NX], V[NX * NX], X[NX * NX];
+    double Lam[NX * NX], M[NX * NX];
+} seg_t;
+
+/* the vector part of a coupling: z = V^T beta + U^-1 L^-1 p_b (into z), lam0 = V z, m = beta - C lam0 */
+static void seg_vec(const seg_t* e, const double* pb, double* z, double* lam0, double* m) {
+    double q[NX];
+    memcpy(q, pb, sizeof q);
+    lsolve(e->L, q);
+    lsolve(e->U, q);
+    for (int r = 0; r < NX; ++r) {
+        double s = 0.0;
+        for (int k = 0; k < NX; ++k) s += e->V[k * NX + r] * e->beta[k];
+        z[r] = s + q[r];
+    }
+    for (int r = 0; r < NX; ++r) {
+        double s = 0.0;
+        for (int k = 0; k < NX; ++k) s += e->V[r * NX + k] * z[k];
+        lam0[r] = s;
+    }
+    for (int r = 0; r < NX; ++r) {
+        double s = 0.0;
+        for (int k = 0; k < NX; ++k) s += e->C[r * NX + k] * lam0[k];
+        m[r] = e->beta[r] - s;
+    }
+}
+
+static void matmul(const double* A, int ta, const double* B, double* D) {  /* D = op(A) B, op = A^T if ta */
+    for (int r = 0; r < NX; ++r)
+        for (int c = 0; c < NX; ++c) {
+            double s = 0.0;
+            for (int k = 0; k < NX; ++k) s += (ta ? A[k * NX + r] : A[r * NX + k]) * B[k * NX + c];
+            D[r * NX + c] = s;
         }
-        double* xn = dx + (size_t)(k + 1) * NX;
-        for (int a = 0; a < NX; ++a) {
-            double s = S->c[a];
-            for (int l = 0; l < NX; ++l) s += S->A[a][l] * xk[l];
-            for (int i = 0; i < NU; ++i) s += S->Bm[a][i] * uk[i];
-            xn[a] = s;
+}
+
+static int lqr_seg(ipm_t* Q, int P, const double* sig, const double* v, double* dx, double* du, double* sl, double* su) {
+    const int N = Q->N;
+    seg_t sg[16];
+    if (P > 16) P = 16;
+    if (P > N) P = N > 0 ? N : 1;
+    static const double zP[NX * NX], zp[NX];
+    for (int i = P - 1; i >= 0; --i) {  /* pass 1, every segment on its own */
+        const int a = seg_a(N, P, i), b = seg_a(N, P, i + 1);
+        seg_t* e = &sg[i];
+        memset(e, 0, sizeof *e);
+        for (int l = 0; l < NX; ++l) e->Phi[l * NX + l] = 1.0;
+        for (int k = (i == P - 1 ? N : b - 1); k >= a; --k) {
+            double Qx[NX * NX], qx[NX], R0[NU * NU], S0[NU * NX], ru[NU], bd[NU], Rc[NU * NU], Ab[NX * NX];
+            stage_terms(Q, k, sig, v, Qx, qx, R0, S0, ru, bd);
+            double* Pk = Q->P + (size_t)k * NX * NX;
+            double* pk = Q->p + (size_t)k * NX;
+            if (k == N) {
+                memcpy(Pk, Qx, sizeof Qx);
+                memcpy(pk, qx, sizeof qx);
+                continue;
+            }
+            const int end = (i < P - 1 && k == b - 1);
+            double* Kk = Q->K + (size_t)k * NU * NX;
+            double* kf = Q->kf + (size_t)k * NU;
+            if (ric_stage(Q, k, Qx, qx, R0, S0, ru, bd, end ? zP : Pk + NX * NX, end ? zp : pk + NX, Pk, pk, Kk, kf, Ab, Rc))
+                return 1;
+            if (i == P - 1) continue;
+            const stage_t* S = &Q->st[k];
+            double Z[NX * NU], *G = Q->G + (size_t)k * NU * NX, t[NX], Pn[NX * NX];
+            for (int l = 0; l < NX; ++l) {  /* Z = Phi B, G = R^-1 Z^T, C += Z G */
+                for (int j = 0; j < NU; ++j) {
+                    double s = 0.0;
+                    for (int q = 0; q < NX; ++q) s += e->Phi[l * NX + q] * S->Bm[q][j];
+                    Z[l * NU + j] = s;
+                }
+                double col[NU];
+                for (int j = 0; j < NU; ++j) col[j] = Z[l * NU + j];
+                chol_solve(NU, Rc, col);
+                for (int j = 0; j < NU; ++j) G[j * NX + l] = col[j];
+            }
+            for (int l = 0; l < NX; ++l)
+                for (int q = 0; q < NX; ++q) {
+                    double s = 0.0;
+                    for (int j = 0; j < NU; ++j) s += Z[l * NU + j] * G[j * NX + q];
+                    e->C[l * NX + q] += s;
+                }
+            for (int l = 0; l < NX; ++l) {  /* closed-loop offset c + B kf */
+                double s = S->c[l];
+                for (int j = 0; j < NU; ++j) s += S->Bm[l][j] * kf[j];
+                t[l] = s;
+            }
+            for (int l = 0; l < NX; ++l) {  /* [Phi | beta] <- [Phi A~ | Phi b~ + beta] */
+                double s = 0.0;
+                for (int q = 0; q < NX; ++q) s += e->Phi[l * NX + q] * t[q];
+                e->beta[l] += s;
+                for (int q = 0; q < NX; ++q) {
+                    double s2 = 0.0;
+                    for (int r = 0; r < NX; ++r) s2 += e->Phi[l * NX + r] * Ab[r * NX + q];
+                    Pn[l * NX + q] = s2;
+                }
+            }
+            memcpy(e->Phi, Pn, sizeof Pn);
+        }
+    }
+    double lam0[16][NX], mv[16][NX];
+    for (int i = P - 2; i >= 0; --i) {  /* coupling, backward: the true cost-to-go at every a_i */
+        const int a = seg_a(N, P, i), b = seg_a(N, P, i + 1);
+        seg_t* e = &sg[i];
+        const double* Pb = Q->P + (size_t)b * NX * NX;
+        const double* pb = Q->p + (size_t)b * NX;
+        memcpy(e->L, Pb, sizeof e->L);
+        if (chol(NX, e->L)) return 1;
+        for (int r = 0; r < NX; ++r)
+            for (int c = r + 1; c < NX; ++c) e->L[r * NX + c] = 0.0;
+        double T[NX * NX];
+        matmul(e->C, 0, e->L, T);       /* T = C L */
+        matmul(e->L, 1, T, e->U);       /* S = I + L^T T */
+        for (int r = 0; r < NX; ++r) e->U[r * NX + r] += 1.0;
+        if (chol(NX, e->U)) return 1;
+        for (int r = 0; r < NX; ++r)
+            for (int c = r + 1; c < NX; ++c) e->U[r * NX + c] = 0.0;
+        for (int r = 0; r < NX; ++r) {  /* row r of V = L U^-T: (U^-1 (row r of L)^T)^T */
+            double row[NX];
+            for (int c = 0; c < NX; ++c) row[c] = e->L[r * NX + c];
+            lsolve(e->U, row);
+            for (int c = 0; c < NX; ++c) e->V[r * NX + c] = row[c];
+        }
+        matmul(e->V, 1, e->Phi, e->X);  /* X = V^T Phi */
+        double z[NX];
+        seg_vec(e, pb, z, lam0[i], mv[i]);
+        matmul(e->V, 0, e->X, e->Lam);  /* Lam = V X */
+        matmul(e->C, 0, e->Lam, T);     /* M = Phi - C Lam */
+        for (int r = 0; r < NX * NX; ++r) e->M[r] = e->Phi[r] - T[r];
+        if (i == 0) continue;  /* x_0 is fixed: the cost-to-go at node 0 is never used */
+        double* Pa = Q->P + (size_t)a * NX * NX;
+        double* pa = Q->p + (size_t)a * NX;
+        for (int r = 0; r < NX; ++r) {
+            for (int c = 0; c < NX; ++c) {
+                double s = 0.0;
+                for (int q = 0; q < NX; ++q) s += e->X[q * NX + r] * e->X[q * NX + c];
+                Pa[r * NX + c] += s;
+            }
+            double s = 0.0;
+            for (int q = 0; q < NX; ++q) s += e->X[q * NX + r] * z[q];
+            pa[r] += s;
+        }
+    }
+    /* forward: boundary states by the coupling, then every segment on its own */
+    memcpy(dx, Q->x0, sizeof(double) * NX);
+    for (int i = 0; i < P; ++i) {
+        const int a = seg_a(N, P, i), b = seg_a(N, P, i + 1);
+        const seg_t* e = &sg[i];
+        double lam[NX], xb[NX];
+        const double* xa = dx + (size_t)a * NX;
+        if (i < P - 1)
+            for (int r = 0; r < NX; ++r) {
+                double sx = mv[i][r], sl2 = lam0[i][r];
+                for (int c = 0; c < NX; ++c) {
+                    sx += e->M[r * NX + c] * xa[c];
+                    sl2 += e->Lam[r * NX + c] * xa[c];
+                }
+                xb[r] = sx;
+                lam[r] = sl2;
+            }
+        for (int k = a; k < b; ++k) {
+            node_slacks(Q, k, sig, v, dx + (size_t)k * NX, sl, su);
+            if (k == N) break;
+            double xn[NX];
+            fwd_stage(Q, k, Q->K + (size_t)k * NU * NX, Q->kf + (size_t)k * NU, i < P - 1 ? Q->G + (size_t)k * NU * NX : NULL,
+                      lam, dx + (size_t)k * NX, du + (size_t)k * NU, k + 1 == b ? xn : dx + (size_t)(k + 1) * NX);
+            if (k + 1 == b) {
+                double d = 0.0;
+                for (int r = 0; r < NX; ++r) d = fmax(d, fabs(xn[r] - xb[r]) / (1.0 + fabs(xb[r])));
+                if (d > Q->seg_dev) Q->seg_dev = d;
+                memcpy(dx + (size_t)b * NX, xb, sizeof xb);
+            }
         }
     }
     return 0;
@@ -294,6 +534,9 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     Q.p = (double*)malloc(sizeof(double) * (size_t)N1 * NX);
     Q.K = (double*)malloc(sizeof(double) * (size_t)N * NU * NX);
     Q.kf = (double*)malloc(sizeof(double) * (size_t)N * NU);
+    Q.G = (double*)calloc((size_t)N * NU * NX, sizeof(double));
+    Q.nseg = o->nseg;
+    Q.seg_dev = 0.0;
     double* buf = (double*)calloc((size_t)(12 * m + 4 * (N1 * NX + N * NU + 2 * N1 * NS)), sizeof(double));
     double *t = buf, *lam = t + m, *sig = lam + m, *v = sig + m, *rv = v + m, *dta = rv + m, *dla = dta + m;
     double *dtc = dla + m, *dlc = dtc + m, *rw = dlc + m;  /* rw: spare */
@@ -400,7 +643,7 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
             sig[r] = lam[r] / t[r];
             v[r] = sig[r] * (t[r] - d0[r]);
         }
-        if (lqr(&Q, sig, v, adx, adu, asl, asu)) { fail = 1; break; }
+        if (Q.nseg > 1 ? lqr_seg(&Q, Q.nseg, sig, v, adx, adu, asl, asu) : lqr(&Q, sig, v, adx, adu, asl, asu)) { fail = 1; break; }
         rows_at(&Q, adx, adu, asl, asu, rv);
         for (int r = 0; r < m; ++r) {
             dta[r] = rv[r] - t[r];
@@ -416,7 +659,7 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         if (sigmu < 1e-2 * o->tol) sigmu = 1e-2 * o->tol;
         /* corrector */
         for (int r = 0; r < m; ++r) v[r] = sig[r] * (t[r] - d0[r]) - (dta[r] * dla[r] - sigmu) / t[r];
-        if (lqr(&Q, sig, v, cdx, cdu, csl, csu)) { fail = 1; break; }
+        if (Q.nseg > 1 ? lqr_seg(&Q, Q.nseg, sig, v, cdx, cdu, csl, csu) : lqr(&Q, sig, v, cdx, cdu, csl, csu)) { fail = 1; break; }
         rows_at(&Q, cdx, cdu, csl, csu, rv);
         for (int r = 0; r < m; ++r) {
             dtc[r] = rv[r] - t[r];
@@ -451,8 +694,8 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         }
     if (!isfinite(mu + rp)) fail = 1;
     *conv = fail ? -1 : (cm < o->tol && rp < o->tol && gap < o->tol);
-    if (res) { res[0] = cm; res[1] = rp; }
-    free(d0); free(buf); free(Q.st); free(Q.P); free(Q.p); free(Q.K); free(Q.kf);
+    if (res) { res[0] = cm; res[1] = rp; res[2] = Q.seg_dev; }
+    free(d0); free(buf); free(Q.st); free(Q.P); free(Q.p); free(Q.K); free(Q.kf); free(Q.G);
     return it;
 }
 
@@ -474,6 +717,7 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
     o.tol = opts[21];
     o.lm_scaling = opts[22] != 0.0;
     o.t0 = opts[23]; o.l0 = opts[24]; o.lc = opts[25]; o.tau_lo = opts[26]; o.tau_hi = opts[27];
+    o.nseg = (int)opts[28];
     o.max_iter = max_iter;
     o.cost_scaling = cost_scaling;
     const int N1 = N + 1;
@@ -486,7 +730,7 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
                              u + (size_t)b * N * NU, x0 + (size_t)b * NX, yref + (size_t)b * N * ny,
                              W + (size_t)b * N * ny, yNref + (size_t)b * 4, WN + (size_t)b * 4, dt, &o, ny,
                              dx + (size_t)b * N1 * NX, du + (size_t)b * N * NU,
-                             slack ? slack + (size_t)b * N1 * NS * 2 : NULL, &conv, res ? res + 2 * b : NULL);
+                             slack ? slack + (size_t)b * N1 * NS * 2 : NULL, &conv, res ? res + 3 * b : NULL);
         status[b] = conv < 0 ? 2 : conv ? 0 : 1;
     }
 }
