@@ -31,7 +31,7 @@
  *   sdfnmpc_solver_*                   the AcadosOcpSolver object Ocp builds (ocp.py:127) and drives:
  *                                      solver.set(k, 'x'|'u'|'p') / cost_set(k, 'yref'|'W') (ocp.py:
  *                                      146-170) -> _upload; solver.get -> _download; reset + init
- *                                      (ocp.py:144-153) -> _init; shift (ocp.py:156-160) -> _shift;
+ *                                      (ocp.py:144-149) -> _init; shift (ocp.py:152-156) -> _shift;
  *                                      solve_for_x0 (ocp.py:169) -> _step + _wait.  It owns the device
  *                                      workspace of B instances, so a controller needs no tensor library
  *
@@ -181,6 +181,16 @@ int sdfnmpc_ctx_use_null_stream(sdfnmpc_ctx* ctx);
 void* sdfnmpc_ctx_stream(sdfnmpc_ctx* ctx);
 int sdfnmpc_ctx_device(const sdfnmpc_ctx* ctx);
 int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx);
+/* the feedback-phase IPM kernel: SEGMENTED runs every instance on four wavefronts with a partitioned
+ * (parallel-in-time) Riccati recursion (csrc/rti_qp_seg.hip); SERIAL on one wavefront (csrc/rti_qp.hip).
+ * AUTO (default) = SERIAL; SEGMENTED applies where it supports the horizon (7 <= N <= 63).  The environment
+ * variable SDFNMPC_QP_KERNEL=serial|segmented sets the default of new contexts. */
+#define SDFNMPC_QP_AUTO 0
+#define SDFNMPC_QP_SERIAL 1
+#define SDFNMPC_QP_SEGMENTED 2
+int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel);
+/* the kernel a QP of horizon N runs on this context (SDFNMPC_QP_SERIAL or _SEGMENTED; -1 on bad arguments) */
+int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N);
 /* rows per SDF workgroup: 32 (2 workgroups / CU) or 64 (1 workgroup / CU); default 32 */
 int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows);
 /* per-kernel HIP-event timing on the context stream (off by default) */
@@ -298,7 +308,7 @@ int sdfnmpc_solver_upload(sdfnmpc_solver* s, const char* name, int col0, int nco
 int sdfnmpc_solver_download(sdfnmpc_solver* s, const char* name, void* host);
 /* reset + init (ocp.py:144-153): x0 = x_k = x0[b] for k = 0..N, u_k = u_init[4], dx = du = 0 */
 int sdfnmpc_solver_init(sdfnmpc_solver* s, const double* x0, const double* u_init);
-/* shift (ocp.py:156-160): x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (k <= 0 or k >= N: no-op) */
+/* shift (ocp.py:152-156): x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (k <= 0 or k >= N: no-op) */
 int sdfnmpc_solver_shift(sdfnmpc_solver* s, int k);
 /* enqueue one SQP-RTI iteration: x_0 = x0, preparation phase, QP, full step (failed instances keep their
  * iterate), then u_0 / status / iterations into pinned host memory.  Asynchronous. */

@@ -23,6 +23,7 @@ L4C_PATH = os.path.join(LIB_DIR, "libsdf_l4c.so")
 SYMBOLS = [
     "sdfnmpc_abi_version", "sdfnmpc_last_error", "sdfnmpc_ctx_create", "sdfnmpc_ctx_destroy",
     "sdfnmpc_ctx_set_stream", "sdfnmpc_ctx_use_null_stream", "sdfnmpc_ctx_stream", "sdfnmpc_ctx_synchronize", "sdfnmpc_ctx_set_tile_rows",
+    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_qp_kernel",
     "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
@@ -120,6 +121,8 @@ def load():
         "sdfnmpc_ctx_stream": (vp, [vp]),
         "sdfnmpc_ctx_synchronize": (i, [vp]),
         "sdfnmpc_ctx_set_tile_rows": (i, [vp, i]),
+        "sdfnmpc_ctx_set_qp_kernel": (i, [vp, i]),
+        "sdfnmpc_ctx_qp_kernel": (i, [vp, i]),
         "sdfnmpc_ctx_enable_timing": (i, [vp, i]),
         "sdfnmpc_ctx_kernel_stats": (i, [vp, C.c_char_p, P(d), P(ll)]),
         "sdfnmpc_ctx_reset_stats": (i, [vp]),
@@ -186,6 +189,16 @@ def _ptr(t):
     return t.data_ptr()
 
 
+def sync_producer(a):
+    """A torch CUDA tensor handed to a kernel of ours (which runs on a context stream, not torch's): wait
+    until torch's current stream on its device -- where a producing kernel or non_blocking copy was queued --
+    has finished.  DeviceArray / FieldView / host arrays need nothing.  torch is imported only here."""
+    if type(a).__module__.split(".")[0] == "torch" and getattr(a, "is_cuda", False):
+        import torch
+        torch.cuda.current_stream(a.device).synchronize()
+    return a
+
+
 class Context:
     """One HIP device + stream (sdfnmpc_ctx)."""
 
@@ -203,6 +216,16 @@ class Context:
 
     def set_tile_rows(self, rows: int):
         _check(load().sdfnmpc_ctx_set_tile_rows(self.h, rows))
+
+    QP_KERNELS = {"auto": 0, "serial": 1, "segmented": 2}
+
+    def set_qp_kernel(self, kind: str):
+        """'auto' (segmented where it supports N), 'serial' or 'segmented' (include/sdfnmpc.h)."""
+        _check(load().sdfnmpc_ctx_set_qp_kernel(self.h, self.QP_KERNELS[kind]))
+
+    def qp_kernel(self, N: int) -> str:
+        k = load().sdfnmpc_ctx_qp_kernel(self.h, N)
+        return {1: "serial", 2: "segmented"}.get(k, "invalid")
 
     def set_stream(self, stream):
         if stream is not None and int(stream) == 0:

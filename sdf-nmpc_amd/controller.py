@@ -5,11 +5,11 @@ an optional leading batch dimension (``batch`` instances solved together, one SQ
 ``solve``).  With ``batch=1`` the shapes are exactly the reference's.
 
   reset()                              controller.py:35    p, y, yN, W, WN zeroed, flag off, latent reset
-  set_sdf_flag(flag)                   controller.py:47
-  set_latent(latent, W_p_Bo, W_R_Bo)   controller.py:52    W_p_Co, W_R_Co (row-major 3x3), latent in p
-  reset_latent()                       controller.py:59
-  set_x0(x0)                           controller.py:67    first call initialises the OCP
-  solve()                              controller.py:74    shift + one RTI iteration; returns fail_count
+  set_sdf_flag(flag)                   controller.py:45
+  set_latent(latent, W_p_Bo, W_R_Bo)   controller.py:50    W_p_Co, W_R_Co (row-major 3x3), latent in p
+  reset_latent()                       controller.py:57
+  set_x0(x0)                           controller.py:65    first call initialises the OCP
+  solve()                              controller.py:72    shift + one RTI iteration; returns fail_count
   get_matrices(), get_u(), get_cmd_acc(), get_cmd_TRPYr(), get_openloop_traj(), eval(k), set_ref(ref, k)
 
 Host setters write the host arrays (``p``, ``y``, ``W``, ``yN``, ``WN``) and mark the rows and columns
@@ -96,6 +96,7 @@ class Nmpc:
         self.W = np.zeros(self._shape(self.N, m.ny))
         self.WN = np.zeros(self._shape(m.nyN))
         self.fail_count = 0
+        self.fail_counts = np.zeros(self.B, dtype=int)  # per-instance consecutive QP failures
         self.set_sdf_flag(False)
         self.reset_latent()
         for g in ("q_d", "yref", "W", "yNref", "WN"):
@@ -109,7 +110,7 @@ class Nmpc:
         self._mark("flag")
 
     def set_latent(self, latent, W_p_Bo, W_R_Bo):
-        """Latent and camera pose at the time of the image (controller.py:52-56), batched over a leading dim."""
+        """Latent and camera pose at the time of the image (controller.py:50-54), batched over a leading dim."""
         idx = self.cfg.mpc.p_idx
         W_R_Bo = np.asarray(W_R_Bo, dtype=float)
         W_p_Co = W_R_Bo @ np.asarray(self.cfg.sensor.B_p_C, dtype=float).ravel() + W_p_Bo
@@ -138,7 +139,7 @@ class Nmpc:
         self.x0 = x0
 
     def solve(self):
-        """One SQP-RTI iteration for every instance (controller.py:74-83)."""
+        """One SQP-RTI iteration for every instance (controller.py:72-81)."""
         try:
             self.ocp.shift(self.cfg.mpc.shift)
             self._flush()  # host-set regions; device-set regions are already in place
@@ -147,6 +148,11 @@ class Nmpc:
         except Exception as e:  # same contract as the reference: report, count, keep running
             print("solver failed:", e)
             self.fail_count += 1
+        # fail_count is batch-wide (any failed instance counts, as one reference solver per instance would
+        # for that instance); fail_counts holds the per-instance consecutive failures
+        mask = getattr(self.ocp, "fail_mask", None)
+        if mask is not None:
+            self.fail_counts = np.where(mask, getattr(self, "fail_counts", 0) + 1, 0)
         return self.fail_count
 
     # ---- getters
@@ -200,7 +206,7 @@ class Nmpc:
         if hasattr(a, "data_ptr"):
             if np.dtype(str(a.dtype).replace("torch.", "")) != np.float64:
                 raise TypeError(f"device input must be float64, got {a.dtype}")
-            return a
+            return _lib.sync_producer(a)  # a torch tensor may still be in flight on torch's stream
         return _lib.DeviceArray.from_numpy(self.ocp.ctx, np.asarray(a, dtype=np.float64))
 
     def gen_refs_device(self, mode="wps", wps=None, vw=None, weights=None):

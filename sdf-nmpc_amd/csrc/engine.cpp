@@ -76,6 +76,7 @@ struct sdfnmpc_ctx {
     hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     bool lin_first = false;
     bool serial_prep = false;  // diagnostic (SDFNMPC_SERIAL_PREP=1): linearize after the SDF kernel, same stream
+    int qp_kernel = SDFNMPC_QP_AUTO;  // SDFNMPC_QP_KERNEL=serial|segmented, or sdfnmpc_ctx_set_qp_kernel
     int tile_rows = 32;
     bool timing = false;
     DevBuf c13, sdf4, lat, out4, glat, qpw, qpst, wws;
@@ -95,6 +96,8 @@ struct sdfnmpc_ctx {
         const double* xn = nullptr;  // the lin outputs they were packed from
         const void* work = nullptr;
         bool sdf_row_patch = false;  // the feedback's QP kernel copies the sdf row of C^T into them
+        int ny = 0, cost_scaling = 0, lm_scaling = 0;  // the qp options the records were packed under
+        double lm = 0.0;
     } prep;
 };
 
@@ -166,6 +169,10 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
     c->lin_first = lf && *lf == '1';
     const char* sp = getenv("SDFNMPC_SERIAL_PREP");
     c->serial_prep = sp && *sp == '1';
+    if (const char* qk = getenv("SDFNMPC_QP_KERNEL")) {
+        if (!strcmp(qk, "serial")) c->qp_kernel = SDFNMPC_QP_SERIAL;
+        else if (!strcmp(qk, "segmented")) c->qp_kernel = SDFNMPC_QP_SEGMENTED;
+    }
     *out = c;
     return SDFNMPC_OK;
 }
@@ -256,6 +263,20 @@ extern "C" int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx) {
     ScopedDevice sd(ctx->device);
     HIPCHK(hipStreamSynchronize(ctx->stream));
     return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel) {
+    if (!ctx) return fail(SDFNMPC_E_ARG, "NULL context");
+    if (kernel != SDFNMPC_QP_AUTO && kernel != SDFNMPC_QP_SERIAL && kernel != SDFNMPC_QP_SEGMENTED)
+        return fail(SDFNMPC_E_ARG, "qp kernel: SDFNMPC_QP_AUTO, _SERIAL or _SEGMENTED");
+    ctx->qp_kernel = kernel;
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N) {
+    if (!ctx || N < 1) return -1;
+    if (ctx->qp_kernel != SDFNMPC_QP_SEGMENTED) return SDFNMPC_QP_SERIAL;  // AUTO: serial until the segmented is faster
+    return rti_qp_seg_supported(N) ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
 }
 
 extern "C" int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows) {
@@ -1071,6 +1092,13 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
     return SDFNMPC_OK;
 }
 
+// the IPM kernel of this context and horizon: the segmented one (four wavefronts per instance,
+// rti_qp_seg.hip) where it supports N, unless the context asks for the serial one (rti_qp.hip)
+static hipError_t qp_launch(sdfnmpc_ctx* ctx, const QpArgs& q) {
+    if (sdfnmpc_ctx_qp_kernel(ctx, q.N) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
+    return launch_rti_qp(q, ctx->stream);
+}
+
 extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* a) {
     if (!ctx || !o || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
     ctx->prep.valid = false;  // the workspace is repacked here
@@ -1079,7 +1107,7 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
     QpArgs q;
     if (int rc = qp_build(ctx, o, a, q)) return rc;
     HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(q, ctx->stream); }));
-    HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
+    HIPCHK(timed(ctx, "rti_qp", [&] { return qp_launch(ctx, q); }));
     return SDFNMPC_OK;
 }
 
@@ -1102,6 +1130,10 @@ extern "C" int sdfnmpc_rti_prepare(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, con
     ctx->prep.N = qa->N;
     ctx->prep.xn = qa->xn;
     ctx->prep.work = q.work;
+    ctx->prep.ny = q.ny;
+    ctx->prep.lm = q.lm;
+    ctx->prep.cost_scaling = q.cost_scaling;
+    ctx->prep.lm_scaling = q.lm_scaling;
     return SDFNMPC_OK;
 }
 
@@ -1114,9 +1146,12 @@ extern "C" int sdfnmpc_qp_feedback(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, c
     QpArgs q;
     if (int rc = qp_build(ctx, o, a, q)) return rc;
     if (q.work != ctx->prep.work) return fail(SDFNMPC_E_ARG, "qp_feedback: workspace moved since rti_prepare");
+    if (q.ny != ctx->prep.ny || q.lm != ctx->prep.lm || q.cost_scaling != ctx->prep.cost_scaling ||
+        q.lm_scaling != ctx->prep.lm_scaling)  // the stage records hold H, g packed under the prepare's options
+        return fail(SDFNMPC_E_ARG, "qp_feedback: ny / lm / cost_scaling / lm_scaling differ from sdfnmpc_rti_prepare's");
     ctx->prep.valid = false;  // one feedback per preparation, as in acados' SQP-RTI
     q.sdf_row_patch = ctx->prep.sdf_row_patch ? 1 : 0;
-    HIPCHK(timed(ctx, "rti_qp", [&] { return launch_rti_qp(q, ctx->stream); }));
+    HIPCHK(timed(ctx, "rti_qp", [&] { return qp_launch(ctx, q); }));
     return SDFNMPC_OK;
 }
 

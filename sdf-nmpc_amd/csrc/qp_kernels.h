@@ -33,9 +33,17 @@ constexpr int QP_REC = 304;   // stage record: [A B | c | g | C^T | H upper | 0 
 constexpr int QP_FREC = 192;  // factor record: [A~|b~ | K|k_ff (rows of 12) | chol(R^) (1/diag) | P_{k+1} c_k | 4 junk]
 constexpr int QP_RING = 3;    // stream positions in flight per wavefront
 constexpr int QP_SLOT = 5;    // 64-double loads per stream position (committed LDS window = 320 doubles)
+// segmented kernel (rti_qp_seg.hip): four wavefronts per instance, each a segment of the horizon
+constexpr int QP_NSEG = 4;  // at most
+constexpr int QP_FRECS = 368;  // its factor record: rows (+ chol(R^), kf_pred) | J c | Z | c, g, B, C^T copies | G | junk
+constexpr int QP_CPL = 640;    // coupling block per segment 0..2 (packed L, U, C; V, X, M, Lam; beta)
+constexpr int QP_PARK = 12 * 64;  // parked row state per wave
 
-// global workspace per instance: stage records and factor records for nodes 0..N
-__host__ __device__ inline size_t qp_work_doubles(int N) { return (size_t)(N + 1) * (QP_REC + QP_FREC); }
+// global workspace per instance: stage records of nodes 0..N, then factor records (each kernel lays its own
+// out from offset (N + 1) QP_REC; QP_FRECS >= QP_FREC), then the segmented kernel's coupling blocks
+__host__ __device__ inline size_t qp_work_doubles(int N) {
+    return (size_t)(N + 1) * (QP_REC + QP_FRECS) + 3 * (size_t)QP_CPL + QP_NSEG * (size_t)QP_PARK;
+}
 // LDS per instance (one wavefront); the order and sizes mirror carve() in rti_qp.hip (every block
 // rounded up to an even number of doubles so that 16-byte vector reads stay aligned)
 __host__ __device__ inline size_t qp_even(size_t n) { return (n + 1) & ~(size_t)1; }
@@ -54,9 +62,25 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
            + 20;                            // box / soft-row constants
 }
 __host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N) * sizeof(double); }
+// LDS per instance of the segmented kernel (mirrors seg_carve() in rti_qp_seg.hip)
+__host__ __device__ inline size_t qp_seg_lds_doubles(int N, int nseg) {
+    const size_t N1 = N + 1;
+    return qp_even(N1 * 10)                 // dxc
+           + 2 * qp_even((size_t)N * 4)     // dua, duc
+           + 2 * qp_even(N1 * 3)            // cxa, cxc
+           + 2 * qp_even(N1 * 3)            // fw, fg
+           + 2 * qp_even((size_t)N * 4)     // bd, bv
+           + qp_even(N1) + 20 + 48          // s_k, constants, zero rows
+           + nseg * (2 * 320 + 2 + 16 + 64)  // per wave: two stream windows, junk, lam_b, coupling vectors
+           + (QP_NSEG - 1) * 112 + 64;      // hand-off slots (P_b | p_b), reduction partials
+}
+__host__ __device__ inline size_t qp_seg_lds_bytes(int N, int nseg) { return qp_seg_lds_doubles(N, nseg) * sizeof(double); }
 
 hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s);  // stage records into the workspace
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);       // the IPM (after launch_rti_qp_pack)
+bool rti_qp_seg_supported(int N);                               // the segmented IPM handles this horizon
+int rti_qp_seg_count(int N);                                    // its segments (wavefronts) per instance
+hipError_t launch_rti_qp_seg(const QpArgs& a, hipStream_t s);   // the IPM, four wavefronts per instance
 hipError_t launch_rti_apply(int B, int N, double* x, double* u, const double* dx, const double* du, double* u0,
                             const int* status, hipStream_t s);
 

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void scatter_rows_kernel(double* dst, int widt
     dst[(long long)idx[r] * width + col0 + c] = staged[i];
 }
 
-// x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (ocp.py:156-160): one thread per (instance, column), nodes in
+// x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (ocp.py:152-156): one thread per (instance, column), nodes in
 // ascending order, so the overlapping rows are read before they are overwritten
 __global__ __launch_bounds__(256) void shift_kernel(int B, int N, int k, double* x, double* u) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -171,6 +171,9 @@ extern "C" int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, c
     if (o->B < 1 || o->N < 1 || o->np < 17 || (o->ny != 11 && o->ny != 12) || !o->dt ||
         (o->latent_mode != 0 && o->latent_mode != 1) || o->qp.ny != o->ny)
         return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "solver opts: B, N >= 1, np >= 17, ny in {11, 12} == qp.ny, dt required");
+    if (o->np < 17 + sdfnmpc_net_size_latent(net))  // the stage parameters end with the network's latent
+        return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, ("solver opts: np = " + std::to_string(o->np) + " < 17 + latent size " +
+                                                    std::to_string(sdfnmpc_net_size_latent(net)) + " of this network").c_str());
     auto* s = new sdfnmpc_solver();
     s->ctx = ctx;
     s->net = net;
@@ -249,9 +252,12 @@ extern "C" int sdfnmpc_solver_upload(sdfnmpc_solver* s, const char* name, int co
     int n_rows = 0;
     for (int r = 0; r < rows; ++r) n_rows += (!mask || mask[r]) ? 1 : 0;
     if (n_rows == 0) return SDFNMPC_OK;
-    char *vals = nullptr, *dvals = nullptr, *idx = nullptr, *didx = nullptr;
-    SCHK(s->stage((size_t)n_rows * ncol * 8, &vals, &dvals));
-    SCHK(s->stage((size_t)n_rows * 4, &idx, &didx));
+    // values and row indices in ONE reservation: a second stage() call could drain and reset the arena
+    // and hand out a block overlapping the first
+    char *vals = nullptr, *dvals = nullptr;
+    const size_t vbytes = ((size_t)n_rows * ncol * 8 + 15) & ~(size_t)15;
+    SCHK(s->stage(vbytes + (size_t)n_rows * 4, &vals, &dvals));
+    char *idx = vals + vbytes, *didx = dvals + vbytes;
     double* v = (double*)vals;
     int* ix = (int*)idx;
     for (int r = 0, q = 0; r < rows; ++r)
@@ -294,7 +300,7 @@ extern "C" int sdfnmpc_solver_init(sdfnmpc_solver* s, const double* x0, const do
 
 extern "C" int sdfnmpc_solver_shift(sdfnmpc_solver* s, int k) {
     if (!s) return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "NULL solver");
-    if (k <= 0 || k >= s->N) return SDFNMPC_OK;  // ocp.py:156: k > 0 shifts nodes k..N-1 down by k
+    if (k <= 0 || k >= s->N) return SDFNMPC_OK;  // ocp.py:153: k > 0 shifts nodes k..N-1 down by k
     SolverDevice sd(s->device);
     // one launch (it was four strided copies through a scratch buffer: launch latency on the C1 path)
     const long long n = (long long)s->B * 14;
@@ -308,7 +314,7 @@ extern "C" int sdfnmpc_solver_step(sdfnmpc_solver* s) {
     if (!s) return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "NULL solver");
     SolverDevice sd(s->device);
     const size_t n1 = s->N + 1;
-    // x_0 of the iterate = the measured state (Ocp.solve: solver.set(0, 'x', x0), ocp.py:165)
+    // x_0 of the iterate = the measured state (Ocp.solve: solver.set(0, 'x', x0), ocp.py:161)
     SCHK(hipMemcpy2DAsync(s->x, n1 * 80, s->x0, 80, 80, s->B, hipMemcpyDeviceToDevice, s->stream));
     sdfnmpc_lin_args la{};
     la.B = s->B; la.N = s->N; la.np = s->np; la.latent_mode = s->latent_mode;

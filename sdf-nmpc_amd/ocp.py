@@ -9,10 +9,10 @@ device workspace: no tensor library is involved).  The method names, argument me
 layouts are the reference's (plus an optional leading batch dimension):
 
   Ocp(model, build)                   ocp.py:17    shooting grid, solver buffers
-  init(x0)                            ocp.py:148   x_k = x0, u_k = u_hover
-  shift(k)                            ocp.py:156   x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1
-  solve(x0, y, yN, W, WN, p)          ocp.py:163   one SQP-RTI iteration, u = u_0
-  get_u(), get_t()                    ocp.py:175   last u_0, solve wall time [s]
+  init(x0)                            ocp.py:144   x_k = x0, u_k = u_hover
+  shift(k)                            ocp.py:152   x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1
+  solve(x0, y, yN, W, WN, p)          ocp.py:159   one SQP-RTI iteration, u = u_0
+  get_u(), get_t()                    ocp.py:173   last u_0, solve wall time [s]
   solver.get(k, 'x' | 'u'), solver.set(k, ...), solver.reset(), solver.get_stats('time_tot')
 
 Occupancy gate (north_star): with several ``devices`` the batch is split over as
@@ -178,18 +178,18 @@ class Ocp:
 
     # ---- the reference API
     def init(self, x0):
-        """ocp.py:148-153: reset, x_k = x0 for k = 0..N, u_k = u_hover."""
+        """ocp.py:144-149: reset, x_k = x0 for k = 0..N, u_k = u_hover."""
         x0 = np.broadcast_to(np.asarray(x0, dtype=np.float64), (self.B, 10))
         for p in self.parts:
             p.solver.init(x0[p.lo:p.hi], self.model.u_hover)
 
     def shift(self, k=1):
-        """ocp.py:156-160: x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (x_N and the tail keep their values)."""
+        """ocp.py:152-156: x_{i-k} = x_i, u_{i-k} = u_i for i = k..N-1 (x_N and the tail keep their values)."""
         for p in self.parts:
             p.solver.shift(int(k))
 
     def solve(self, x0, y, yN, W, WN, p):
-        """ocp.py:163-172: set x0 / references / weights (diagonals) / parameters, one SQP-RTI iteration.
+        """ocp.py:159-170: set x0 / references / weights (diagonals) / parameters, one SQP-RTI iteration.
         An argument given as None keeps the device buffer as it is (uploaded by Nmpc or written by a
         device-side setter)."""
         N, m = self.N, self.model
@@ -204,6 +204,10 @@ class Ocp:
         self.t = time.perf_counter() - t0
         self.status = np.concatenate([part.solver.status for part in self.parts])
         self.iters = np.concatenate([part.solver.iters for part in self.parts])
+        failed = self.status >= 2
+        if failed.any() and getattr(self, "u", None) is not None:  # as solve_for_x0 raising before `self.u = ...`
+            u0[failed] = np.reshape(self.u, u0.shape)[failed]   # (ocp.py:169): a failed instance keeps its last u_0
+        self.fail_mask = failed
         self.u = u0[0] if self.B == 1 else u0
         if (self.status == 1).any():  # acados status 2 (QP max_iter): solve_for_x0 warns, keeps the step
             warnings.warn(f"QP reached qp_solver_iter_max on {(self.status == 1).sum()} of {self.B} instances")

@@ -293,7 +293,7 @@ class VaeWrapper:
         if hasattr(img, "data_ptr"):  # already on the device: [B][H][W] float32 / uint16, used in place
             if tuple(img.shape)[0] != self.B or len(img.shape) != 3:
                 raise ValueError(f"expected a device array [{self.B}, H, W], got {tuple(img.shape)}")
-            self.img = img
+            self.img = _lib.sync_producer(img)  # a torch tensor may still be in flight on torch's stream
             return
         a = np.asarray(img)
         if a.dtype != np.uint16:
