@@ -62,19 +62,7 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
            + 20;                            // box / soft-row constants
 }
 __host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N) * sizeof(double); }
-// LDS per instance of the segmented kernel (mirrors seg_carve() in rti_qp_seg.hip)
-__host__ __device__ inline size_t qp_seg_lds_doubles(int N, int nseg) {
-    const size_t N1 = N + 1;
-    return qp_even(N1 * 10)                 // dxc
-           + 2 * qp_even((size_t)N * 4)     // dua, duc
-           + 2 * qp_even(N1 * 3)            // cxa, cxc
-           + 2 * qp_even(N1 * 3)            // fw, fg
-           + 2 * qp_even((size_t)N * 4)     // bd, bv
-           + qp_even(N1) + 20 + 48          // s_k, constants, zero rows
-           + nseg * (2 * 320 + 2 + 16 + 64)  // per wave: two stream windows, junk, lam_b, coupling vectors
-           + (QP_NSEG - 1) * 112 + 64;      // hand-off slots (P_b | p_b), reduction partials
-}
-__host__ __device__ inline size_t qp_seg_lds_bytes(int N, int nseg) { return qp_seg_lds_doubles(N, nseg) * sizeof(double); }
+size_t qp_seg_lds_bytes(int N);  // LDS per instance of the segmented kernel chosen for N (static; 0: unsupported)
 
 hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s);  // stage records into the workspace
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);       // the IPM (after launch_rti_qp_pack)

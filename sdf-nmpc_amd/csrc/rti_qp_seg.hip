@@ -52,12 +52,12 @@ constexpr int S_AB = 0, S_K = 10 * FR, S_PC = 14 * FR, S_Z = S_PC + 10, S_C = S_
 static_assert(S_PC == 168 && S_B == 242 && S_G == 312 && S_J + 4 <= FRECS && (FRECS * 8) % 128 == 0 && (S_GV + NX) % 2 == 0,
               "segmented factor record");
 // stream: per position WIN doubles land in one of two LDS windows of the wave by three 16-byte LDS-DMA
-// wave-instructions (the third on lanes 0..31); each lane's source granule is a per-sweep lane constant:
+// wave-instructions; each lane's source granule is a per-sweep lane constant:
 //   0 initial forward   R[0, 194) in place
 //   1 backward factor   R[0, 320) in place (granules past the record repeat its last zero granule)
 //   2, 4 forward        F[0, 168) | F[S_B, S_J) at WF_B: B at WF_B, C^T at WF_CT, G at WF_G
 //   3 corrector         F[0, S_G) in place
-constexpr int WIN = 320, WF_B = 168, WF_CT = WF_B + (S_CT - S_B), WF_G = WF_B + (S_G - S_B);
+constexpr int WIN = 384, WF_B = 168, WF_CT = WF_B + (S_CT - S_B), WF_G = WF_B + (S_G - S_B);
 static_assert(WF_G + 40 <= WIN && S_G <= WIN && REC / 2 <= WIN / 2, "windows");
 __device__ __forceinline__ int src_granule(int K, int wg) {  // source granule (2 doubles) of window granule wg
     if (K == 0) return wg < (R_CT + 30) / 2 ? wg : (R_CT + 30) / 2 - 1;
@@ -115,29 +115,30 @@ struct SegSmem {
     ldsd *slot, *red;               // hand-off slots [3][112], reduction partials
 };
 
-template <int NSEG>
-__device__ __forceinline__ SegSmem seg_carve(ldsd* q, int N, int w) {  // mirrors qp_seg_lds_doubles()
+// LDS layout for horizons N <= NMAX, at compile-time offsets (every LDS address an immediate: no base
+// registers); per-node arrays sized for NMAX
+template <int NSEG, int NMAX>
+struct SegLds {
+    static constexpr int ev(int n) { return (n + 1) & ~1; }
+    static constexpr int N1 = NMAX + 1;
+    static constexpr int DXC = 0, DUA = DXC + ev(N1 * NX), DUC = DUA + ev(NMAX * NU), CXA = DUC + ev(NMAX * NU),
+                         CXC = CXA + ev(N1 * NS), FW = CXC + ev(N1 * NS), FG = FW + ev(N1 * NS), BD = FG + ev(N1 * NS),
+                         BV = BD + ev(NMAX * NU), SKV = BV + ev(NMAX * NU), CST = SKV + ev(N1), ZERO = CST + 20, WINS = ZERO + 48,
+                         JUNK = WINS + NSEG * 2 * WIN, XLAM = JUNK + NSEG * 2, VEC = XLAM + NSEG * 16, SLOT = VEC + NSEG * 64,
+                         RED = SLOT + (NSEG_MAX - 1) * 112, TOTAL = RED + 64;
+};
+
+template <int NSEG, int NMAX>
+__device__ __forceinline__ SegSmem seg_carve(ldsd* q, int w) {
+    using L = SegLds<NSEG, NMAX>;
     SegSmem s;
-    auto take = [&](int n) { ldsd* r = q; q += (n + 1) & ~1; return r; };
-    const int N1 = N + 1;
-    s.dxc = take(N1 * NX);
-    s.dua = take(N * NU); s.duc = take(N * NU);
-    s.cxa = take(N1 * NS); s.cxc = take(N1 * NS);
-    s.fw = take(N1 * NS); s.fg = take(N1 * NS);
-    s.bd = take(N * NU); s.bv = take(N * NU);
-    s.skv = take(N1);
-    s.cst = take(20);
-    s.zero = take(48);
-    ldsd* win = take(NSEG * 2 * WIN);
-    ldsd* junk = take(NSEG * 2);
-    ldsd* xlam = take(NSEG * 16);
-    ldsd* vec = take(NSEG * 64);
-    s.slot = take((NSEG_MAX - 1) * 112);
-    s.red = take(64);
-    s.win = win + w * 2 * WIN;
-    s.junk = junk + 2 * w;
-    s.xlam = xlam + 16 * w;
-    s.vec = vec + 64 * w;
+    s.dxc = q + L::DXC; s.dua = q + L::DUA; s.duc = q + L::DUC; s.cxa = q + L::CXA; s.cxc = q + L::CXC;
+    s.fw = q + L::FW; s.fg = q + L::FG; s.bd = q + L::BD; s.bv = q + L::BV; s.skv = q + L::SKV;
+    s.cst = q + L::CST; s.zero = q + L::ZERO; s.slot = q + L::SLOT; s.red = q + L::RED;
+    s.win = q + L::WINS + w * 2 * WIN;
+    s.junk = q + L::JUNK + 2 * w;
+    s.xlam = q + L::XLAM + 16 * w;
+    s.vec = q + L::VEC + 64 * w;
     return s;
 }
 // vec area of a wave: invL 0, invU 10, beta 20, z 30, lam0 40, m 50
@@ -199,23 +200,27 @@ static_assert(F_NFIELD <= 26 && 8 * FRECS < 65536, "packed lane constants");
 }  // namespace
 
 #ifdef SEG_STAMPS  // diagnostic build only: per-wave, per-phase cycle accounting into A.stamps [B][4][16]
-#define SSTAMP_DECL long long st_t0 = clock64(), st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+#define SSTAMP_DECL long long st_t0 = clock64(), st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; int st_ph = 0;
+#define SSTAMP_PHASE(i) st_ph = (i)
 #define SSTAMP(i) do { const long long t1_ = clock64(); st_acc[i] += t1_ - st_t0; st_t0 = t1_; } while (0)
+#define SSTAMP_ARRIVE(body) do { SSTAMP(st_ph); body; SSTAMP(15); } while (0)
 #define SSTAMP_OUT if (lane == 0 && A.stamps) for (int i_ = 0; i_ < 16; ++i_) A.stamps[((size_t)b * NSEG_MAX + w) * 16 + i_] = (double)st_acc[i_];
 #else
 #define SSTAMP_DECL
+#define SSTAMP_PHASE(i)
 #define SSTAMP(i)
+#define SSTAMP_ARRIVE(body) body
 #define SSTAMP_OUT
 #endif
 
-template <int NSEG>
+template <int NSEG, int NMAX>
 __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
-    extern __shared__ __align__(16) double lds_q[];
+    __shared__ __align__(16) double lds_q[SegLds<NSEG, NMAX>::TOTAL];
     SSTAMP_DECL
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int N = A.N, N1 = N + 1, m = 8 * N + 12 * N1;
-    const SegSmem s = seg_carve<NSEG>((ldsd*)lds_q, N, w);
+    const SegSmem s = seg_carve<NSEG, NMAX>((ldsd*)lds_q, w);
     ldsd* const win = s.win;                                  // two windows; the coupling's scratch
     const int sa = w * N1 / NSEG, sb = (w + 1) * N1 / NSEG;  // this wave's nodes [sa, sb)
 #ifdef SEGX_NO_AUG
@@ -316,24 +321,27 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
     auto opmin = [](double a_, double c_) { return fmin(a_, c_); };
 
     // ------------------------------------------------------------ record stream (LDS-DMA, two windows)
-    // issue: the three DMA wave-instructions of one position, then one ordinary load whose completion
-    // the compiler tracks: VMEM operations of a wave complete in order, so once the token has arrived
-    // the window has too (the compiler counts every store issued in between)
+    // A stage issues its global stores before its refill and nothing to global memory after it, so when
+    // a stage starts, the only VMEM operations that may be newer than its window's DMA are the three of
+    // the latest refill: s_waitcnt vmcnt(3) retires its window (VMEM operations of a wave complete in
+    // order).  The compiler does not track LDS-DMA -> ds_read dependencies; these waits are the ordering.
     typedef __attribute__((address_space(3))) void ldsv;
-    auto issue = [&](auto KIc, ldsd* dst, int k, const int* sg) -> double {
+    auto issue = [&](auto KIc, ldsd* dst, int k, const int* sg) {
         constexpr int KI = decltype(KIc)::value;
         const double* base = (KI == 0 || KI == 1) ? R + (size_t)k * REC : F + (size_t)k * FRECS;
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the window's previous reads are done
         __builtin_amdgcn_global_load_lds((const void*)(base + 2 * sg[0]), (ldsv*)dst, 16, 0, 0);
         __builtin_amdgcn_global_load_lds((const void*)(base + 2 * sg[1]), (ldsv*)(dst + 128), 16, 0, 0);
-        if (lane < 32) __builtin_amdgcn_global_load_lds((const void*)(base + 2 * sg[2]), (ldsv*)(dst + 256), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)(base + 2 * sg[2]), (ldsv*)(dst + 256), 16, 0, 0);
         asm volatile("" ::: "memory");
-        return base[2 * sg[0]];
     };
-    auto arrived = [&](double tok) { asm volatile("" ::"v"(tok) : "memory"); };
+    auto arrived = [&]() { asm volatile("s_waitcnt vmcnt(3)" ::: "memory"); };
+    auto drained = [&]() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); };
     // one sweep over n positions, node(q) the node of position q, positions alternating between the
     // two windows; a stage calls refill() after its last window read, which issues position q + 2 into
-    // the window it has just read (lead: the rest of that stage plus the next one)
+    // the window it has just read (lead: the rest of that stage plus the next one).  The loop body is
+    // straight-line (refills past the end reload the last node), so the compiler counts the VMEM
+    // operations in flight exactly and waits only for the token of the window a stage reads.
     auto sweep = [&](auto Kc, int n, auto node, auto stage) {
         constexpr int K = decltype(Kc)::value;
         int sg[3];
@@ -341,22 +349,21 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         for (int j = 0; j < 3; ++j) sg[j] = opaque(src_granule(K, 64 * j + lane));
         ldsd* const w0 = win;
         ldsd* const w1 = win + WIN;
-        double t0 = issue(Kc, w0, node(0), sg);
-        double t1 = n > 1 ? issue(Kc, w1, node(1), sg) : t0;
-        for (int q = 0; q < n; q += 2) {
-            arrived(t0);
-            stage(q, node(q), w0, [&]() {
-                if (q + 2 < n) t0 = issue(Kc, w0, node(q + 2), sg);
-            });
-            if (q + 1 < n) {
-                arrived(t1);
-                stage(q + 1, node(q + 1), w1, [&]() {
-                    if (q + 3 < n) t1 = issue(Kc, w1, node(q + 3), sg);
-                });
-            }
+        auto nd = [&](int q) { return node(q < n ? q : n - 1); };
+        issue(Kc, w0, nd(0), sg);
+        issue(Kc, w1, nd(1), sg);
+        int q = 0;
+        for (; q + 1 < n; q += 2) {
+            SSTAMP_ARRIVE(arrived());
+            stage(q, node(q), w0, [&]() { issue(Kc, w0, nd(q + 2), sg); });
+            SSTAMP_ARRIVE(arrived());
+            stage(q + 1, node(q + 1), w1, [&]() { issue(Kc, w1, nd(q + 3), sg); });
         }
-        arrived(t0);
-        arrived(t1);
+        if (q < n) {
+            SSTAMP_ARRIVE(arrived());
+            stage(q, node(q), w0, [&]() {});
+        }
+        drained();
     };
 
     // ------------------------------------------------------------ forward stage
@@ -540,8 +547,11 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
             if (a_ >= NX && a_ < 14) Hh[2 + h] += (c == a_ ? s.bd[k * NU + a_ - NX] : 0.0) + (c == 14 ? s.bv[k * NU + a_ - NX] : 0.0);
         }
         const double hxa = cw[fget(f, F_HXU)];
-        refill();
         Ab = mfma(bm, kg, Ab);                  // [A~ | b~] = [A | c] + B [K | k_ff]
+        FBST(Ab[0], fget(f, F_SAB0));
+        FBST(Ab[1], fget(f, F_SAB1));
+        FBST(Ab[2], fget(f, F_SAB2));
+        refill();                               // after the stage's last window read and last store
         const d4 W2 = mfma(Ub, kg, W);          // [P A~ | P b~ + p]
         Hh = mfma(cg, fb, Hh);                  // + C^T diag(w) [C | gamma]
         Hh = mfma(hxa, kg, Hh);                 // H^_x T
@@ -558,9 +568,6 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
             Pn = mfma(e14, Psi[3], Pn);
             Psi = Pn;
         }
-        FBST(Ab[0], fget(f, F_SAB0));
-        FBST(Ab[1], fget(f, F_SAB1));
-        FBST(Ab[2], fget(f, F_SAB2));
     };
 
     // ------------------------------------------------------------ backward stage, corrector
@@ -569,6 +576,8 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
     // then w = L^-1 z_u, k_ff = -L^-T w, b~ = c + B k_ff (off the chain).  g~ = g + fold | box.
     double chain = 0.0;  // p_{k+1} in lanes 0..9
     double bacc = 0.0;   // beta of the corrector (lanes 0..9, segments 0..2)
+    double cfv = 0.0;    // the corrector's record row (b~ | k_ff) of node cpend, stored by the next stage
+    int cpend = -1;
     auto bc_stage = [&](auto Fc, auto AUGc, int k, const ldsd* cw, auto refill) {
         constexpr bool FIRST = decltype(Fc)::value;
         constexpr bool AUG = decltype(AUGc)::value;
@@ -583,6 +592,8 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         }
         if constexpr (FIRST) {  // p_N = g_N + sum_j gamma_j C_j^T
             chain = off;
+            if (cpend >= 0) bst(cfv, rsF, 8u * (lane < 14 ? lane * FR + 10 : S_J), (unsigned)cpend * (FRECS * 8u));
+            cpend = -1;
             refill();
             return;
         }
@@ -638,9 +649,11 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
             const double p0 = cw[S_K + 11], p1 = cw[S_K + FR + 11], p2 = cw[S_K + 2 * FR + 11], p3 = cw[S_K + 3 * FR + 11];
             dz = q0.x * (k0 - p0) + q0.y * (k1 - p1) + q1.x * (k2 - p2) + q1.y * (k3 - p3);
         }
+        // the previous stage's record row goes out now, ahead of this stage's refill; this one's waits
+        if (cpend >= 0) bst(cfv, rsF, 8u * (lane < 14 ? lane * FR + 10 : S_J), (unsigned)cpend * (FRECS * 8u));
         refill();
-        const double fv = fx ? bb : lane == NX ? k0 : lane == NX + 1 ? k1 : lane == NX + 2 ? k2 : k3;
-        bst(fv, rsF, 8u * (lane < 14 ? lane * FR + 10 : S_J), (unsigned)k * (FRECS * 8u));
+        cfv = fx ? bb : lane == NX ? k0 : lane == NX + 1 ? k1 : lane == NX + 2 ? k2 : k3;
+        cpend = k;
         if constexpr (AUG) bacc += fx ? dz : 0.0;
     };
 
@@ -952,6 +965,8 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
             if (w == st) xstep(xrow);
         }
         wg_sync();
+        SSTAMP(decltype(Kc)::value == 2 ? 4 : 9);
+        SSTAMP_PHASE(decltype(Kc)::value == 2 ? 12 : 14);
         if (aug) {
             sweep(Kc, nn, node_fw, [&](int q, int k, const ldsd* cw, auto rf) { fw_stage(Kc, IC<1>{}, k, k == sb - 1, cw, rf); (void)q; });
         } else {
@@ -1026,6 +1041,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         for (int r = 0; r < 4; ++r) Psi[r] = ((lane >> 4) + 4 * r == (lane & 15) && (lane & 15) < NX) ? 1.0 : 0.0;
         lam0 = 0.0;
         mvec = 0.0;
+        SSTAMP_PHASE(2);
 #ifndef SEGX_NO_FACTOR
         factor_sweep();
 #endif
@@ -1057,11 +1073,13 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         for (int st = NSEG - 2; st >= 0; --st) {
             wg_sync();
             if (w == st) {
+                SSTAMP(3);
 #ifndef SEGX_NO_COUPLE
                 mcouple();
                 wave_sync();
                 vcouple(eta, beta);
 #endif
+                SSTAMP(11);
             }
         }
         SSTAMP(3);
@@ -1070,7 +1088,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
 #endif
         unpark();
         wg_sync();
-        SSTAMP(4);
+        SSTAMP(12);
         // ---------------- predictor rows: affine step, mu_aff -> sigma mu
         double sigmu = 1e-10;
 #ifndef SEGX_NO_ROWS
@@ -1120,10 +1138,13 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         park();
         bacc = aug ? CP[CP_B + (lane < NX ? lane : 0)] : 0.0;
         chain = 0.0;
+        cpend = -1;
         SSTAMP(6);
+        SSTAMP_PHASE(7);
 #ifndef SEGX_NO_CORR
         corr_sweep();
 #endif
+        if (cpend >= 0) bst(cfv, rsF, 8u * (lane < 14 ? lane * FR + 10 : S_J), (unsigned)cpend * (FRECS * 8u));
         SSTAMP(7);
         if (!aug) {
             if (lane < NX) s.slot[112 * (NSEG - 2) + 100 + lane] = chain;
@@ -1134,9 +1155,13 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
 #pragma unroll 1
         for (int st = NSEG - 2; st >= 0; --st) {
             wg_sync();
+            if (w == st) {
+                SSTAMP(8);
 #ifndef SEGX_NO_COUPLE
-            if (w == st) vcouple(etac, betac);
+                vcouple(etac, betac);
 #endif
+                SSTAMP(13);
+            }
         }
         SSTAMP(8);
 #ifndef SEGX_NO_FWD
@@ -1144,7 +1169,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
 #endif
         unpark();
         wg_sync();
-        SSTAMP(9);
+        SSTAMP(14);
         // ---------------- step length, update, mu
 #ifdef SEGX_NO_ROWS
         mu *= 0.5; cm *= 0.5;
@@ -1230,35 +1255,56 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
     }
 }
 
-// segments per instance for horizon N (0: unsupported): every segment >= 2 nodes and a wave's box pairs
-// (4 per node) within its 64 lanes; three segments (168 registers per wave at 4 instances per CU) where they
-// suffice, else four (128 registers).  SDFNMPC_QP_NSEG overrides (diagnostic).
+// instantiations: (segments, largest horizon); a segment holds at most 16 nodes (a wave's box pairs, 4
+// per node, within its 64 lanes) and at least 2
+struct SegCfg {
+    int P, NMAX;
+};
+constexpr SegCfg SEG_CFGS[] = {{2, 31}, {3, 47}, {4, 63}};
+static size_t seg_lds_bytes(int P, int NMAX) {
+    switch (P) {
+        case 2: return sizeof(double) * SegLds<2, 31>::TOTAL;
+        case 3: return sizeof(double) * SegLds<3, 47>::TOTAL;
+        default: return sizeof(double) * SegLds<4, 63>::TOTAL;
+    }
+    (void)NMAX;
+}
+// segments per instance for horizon N (0: unsupported): three where they fit (168 registers per wave at
+// four instances per CU), else four.  SDFNMPC_QP_NSEG = 2, 3, 4 overrides (diagnostic).
 int rti_qp_seg_count(int N) {
-    auto fits = [&](int P) { return N + 1 >= 2 * P && (N + 1 + P - 1) / P <= 16 && qp_seg_lds_bytes(N, P) <= 160 * 1024; };
+    auto fits = [&](int P) {
+        for (const SegCfg& c : SEG_CFGS)
+            if (c.P == P) return N <= c.NMAX && N + 1 >= 2 * P;
+        return false;
+    };
     if (const char* e = getenv("SDFNMPC_QP_NSEG")) {
         const int P = atoi(e);
-        return (P >= 2 && P <= NSEG_MAX && fits(P)) ? P : 0;
+        return fits(P) ? P : 0;
     }
     return fits(3) ? 3 : fits(4) ? 4 : 0;
 }
 
 bool rti_qp_seg_supported(int N) { return rti_qp_seg_count(N) > 0; }
 
-template <int P>
+size_t qp_seg_lds_bytes(int N) {
+    const int P = rti_qp_seg_count(N);
+    for (const SegCfg& c : SEG_CFGS)
+        if (c.P == P) return seg_lds_bytes(c.P, c.NMAX);
+    return 0;
+}
+
+template <int P, int NMAX>
 static hipError_t launch_seg(const QpArgs& a, hipStream_t s) {
-    const size_t lds = qp_seg_lds_bytes(a.N, P);
-    hipError_t e = hipFuncSetAttribute((const void*)rti_qp_seg_kernel<P>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rti_qp_seg_kernel<P>, dim3(a.B), dim3(64 * P), lds, s, a);
+    hipLaunchKernelGGL((rti_qp_seg_kernel<P, NMAX>), dim3(a.B), dim3(64 * P), 0, s, a);
     return hipGetLastError();
 }
 
 hipError_t launch_rti_qp_seg(const QpArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     switch (rti_qp_seg_count(a.N)) {
-        case 2: return launch_seg<2>(a, s);
-        case 3: return launch_seg<3>(a, s);
-        case 4: return launch_seg<4>(a, s);
+        case 2: return launch_seg<2, 31>(a, s);
+        case 3: return launch_seg<3, 47>(a, s);
+        case 4: return launch_seg<4, 63>(a, s);
         default: return hipErrorInvalidValue;
     }
 }

@@ -113,7 +113,7 @@ def test_c5_qp_full_size_properties_and_oracle(run, oracle_lib):
     u_new = c5.prob["u"] + du
     assert (u_new >= m.lbu - 1e-7).all() and (u_new <= m.ubu + 1e-7).all()
     np.testing.assert_array_equal(u0, out["u"][:, 0])
-    assert not dx[:, 0].any()  # the step sets x_0 = x0 before linearising (Ocp.solve, ocp.py:165)
+    assert not dx[:, 0].any()  # the step sets x_0 = x0 before linearising (Ocp.solve, ocp.py:161)
     AB, c = out["AB"], out["xn"] - c5.prob["x"][:, 1:]
     pred = np.einsum("bkji,bkj->bki", AB[:, :, :10], dx[:, :-1]) + np.einsum("bkji,bkj->bki", AB[:, :, 10:], du) + c
     np.testing.assert_allclose(dx[:, 1:], pred, atol=1e-9)

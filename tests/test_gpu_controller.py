@@ -1,6 +1,6 @@
 """The controller mirror end to end on the GPU: Nmpc.set_x0 / set_latent / set_ref / solve (one
 SQP-RTI iteration per instance) against the CPU pipeline oracle.linearize_batch + qp_oracle
-(dense Mehrotra IPM) from the same iterate; Ocp.init / shift semantics (ocp.py:148-160)."""
+(dense Mehrotra IPM) from the same iterate; Ocp.init / shift semantics (ocp.py:144-156)."""
 import os
 
 import numpy as np

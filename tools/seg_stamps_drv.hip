@@ -23,10 +23,10 @@ int main(int argc, char** argv) {
   std::vector<double> st(B*64); hipMemcpy(st.data(),q.stamps,8*B*64,hipMemcpyDeviceToHost);
   std::vector<int> it(B); hipMemcpy(it.data(),q.iters,4*B,hipMemcpyDeviceToHost);
   int mx=0; double mi=0; for(int i=0;i<B;++i){ if(it[i]>mx)mx=it[i]; mi+=it[i]; }
-  const char* ph[]={"setup+sweep0","terms0+park","factor sweep","factor couple","pred fwd","rows pred","terms1+park","corr sweep","corr couple","corr fwd","rows update"};
+  const char* ph[]={"setup+sweep0","terms0+park","factor sweep","f-couple wait","pred x-chain","rows pred","terms1+park","corr sweep","c-couple wait","corr x-chain","rows update","f-couple own","pred fwd sweep","c-couple own","corr fwd sweep","window waits"};
   printf("kernel %.3f ms, max iters %d, mean %.2f\n", ms, mx, mi/B);
   for(int w=0;w<4;++w){ double tot[16]={0}, s=0; for(int i=0;i<B;++i) for(int j=0;j<16;++j) tot[j]+=st[(i*4+w)*16+j];
     for(int j=0;j<16;++j) s+=tot[j];
     printf("wave %d: total %.0f cycles/instance, per iteration %.0f\n", w, s/B, s/mi);
-    for(int j=0;j<11;++j) printf("  %-14s %8.0f cycles/iter (%.1f%%)\n", ph[j], tot[j]/mi, 100*tot[j]/s); }
+    for(int j=0;j<16;++j) printf("  %-14s %8.0f cycles/iter (%.1f%%)\n", ph[j], tot[j]/mi, 100*tot[j]/s); }
   return 0; }
