@@ -60,6 +60,7 @@ def lib():
         _lib.orc_vae_preprocess.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
                                             P(f), P(f)]
         _lib.orc_vae_encode.argtypes = [P(f), C.c_int, C.c_int, C.c_int, P(f), C.c_int, C.c_int, P(d), P(d)]
+        _lib.orc_vae_set_threads.argtypes = [C.c_int]
     return _lib
 
 
@@ -212,8 +213,10 @@ def vae_preprocess(img, shape, clip_scale, yz=None):
     return out
 
 
-def vae_encode(pre, flat_params, L=128, bn=True, stage_sums=False):
-    """Encoder.forward (network/vae.py:39-43) in fp64 on preprocessed images [B, H, W]."""
+def vae_encode(pre, flat_params, L=128, bn=True, stage_sums=False, nthreads=0):
+    """Encoder.forward (network/vae.py:39-43) in fp64 on preprocessed images [B, H, W]
+    (nthreads: OpenMP threads of the conv layers, 0 = the OpenMP default)."""
+    lib().orc_vae_set_threads(int(nthreads))
     pre = np.ascontiguousarray(pre, dtype=np.float32)
     if pre.ndim == 2:
         pre = pre[None]

@@ -19,6 +19,16 @@
 #include <stdlib.h>
 #include <string.h>
 
+/* OpenMP threads of the conv layers (0: the runtime default); set by the CPU-baseline leg of bench.py */
+static int g_vae_threads = 0;
+void orc_vae_set_threads(int n) { g_vae_threads = n > 0 ? n : 0; }
+#ifdef _OPENMP
+#include <omp.h>
+static int vae_threads(void) { return g_vae_threads > 0 ? g_vae_threads : omp_get_max_threads(); }
+#else
+static int vae_threads(void) { return 1; }
+#endif
+
 /* ---- preprocessing (fp32, torch order) ---- */
 void orc_vae_preprocess(const void* img, int dtype, int Hi, int Wi, int H, int W, float clip_scale,
                         const float* yz, float* out) {
@@ -67,7 +77,7 @@ static const float* take(cursor* c, long n) {
 /* out[co][oy][ox] = sum w[co][ci][ky][kx] in[ci][iy][ix] (+ bias) */
 static void conv2d(const double* in, int C, int H, int W, const float* w, const float* bias, int Co, int K,
                    int S, int P, double* out, int Ho, int Wo) {
-#pragma omp parallel for schedule(static)
+#pragma omp parallel for schedule(static) num_threads(vae_threads())
     for (int co = 0; co < Co; ++co) {
         double* o = out + (long)co * Ho * Wo;
         for (long i = 0; i < (long)Ho * Wo; ++i) o[i] = bias ? (double)bias[co] : 0.0;

@@ -23,7 +23,7 @@ L4C_PATH = os.path.join(LIB_DIR, "libsdf_l4c.so")
 SYMBOLS = [
     "sdfnmpc_abi_version", "sdfnmpc_last_error", "sdfnmpc_ctx_create", "sdfnmpc_ctx_destroy",
     "sdfnmpc_ctx_set_stream", "sdfnmpc_ctx_use_null_stream", "sdfnmpc_ctx_stream", "sdfnmpc_ctx_synchronize", "sdfnmpc_ctx_set_tile_rows",
-    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_qp_kernel",
+    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_qp_kernel", "sdfnmpc_qp_lds_bytes", "sdfnmpc_qp_capacity",
     "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
@@ -123,6 +123,8 @@ def load():
         "sdfnmpc_ctx_set_tile_rows": (i, [vp, i]),
         "sdfnmpc_ctx_set_qp_kernel": (i, [vp, i]),
         "sdfnmpc_ctx_qp_kernel": (i, [vp, i]),
+        "sdfnmpc_qp_lds_bytes": (C.c_longlong, [i]),
+        "sdfnmpc_qp_capacity": (C.c_longlong, [vp, i]),
         "sdfnmpc_ctx_enable_timing": (i, [vp, i]),
         "sdfnmpc_ctx_kernel_stats": (i, [vp, C.c_char_p, P(d), P(ll)]),
         "sdfnmpc_ctx_reset_stats": (i, [vp]),
@@ -226,6 +228,13 @@ class Context:
     def qp_kernel(self, N: int) -> str:
         k = load().sdfnmpc_ctx_qp_kernel(self.h, N)
         return {1: "serial", 2: "segmented"}.get(k, "invalid")
+
+    def qp_capacity(self, N: int) -> int:
+        """Instances this device solves in one wave of QP workgroups at horizon N (sdfnmpc_qp_capacity)."""
+        n = int(load().sdfnmpc_qp_capacity(self.h, N))
+        if n < 0:
+            raise SdfnmpcError(f"sdfnmpc_qp_capacity: bad arguments (N={N})")
+        return n
 
     def set_stream(self, stream):
         if stream is not None and int(stream) == 0:

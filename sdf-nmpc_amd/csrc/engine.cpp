@@ -78,6 +78,8 @@ struct sdfnmpc_ctx {
     bool serial_prep = false;  // diagnostic (SDFNMPC_SERIAL_PREP=1): linearize after the SDF kernel, same stream
     int qp_kernel = SDFNMPC_QP_AUTO;  // SDFNMPC_QP_KERNEL=serial|segmented, or sdfnmpc_ctx_set_qp_kernel
     int tile_rows = 32;
+    int n_cu = 0;              // compute units of the device (hipDeviceProp_t::multiProcessorCount)
+    size_t lds_per_cu = 0;     // LDS bytes per CU (hipDeviceProp_t::maxSharedMemoryPerMultiProcessor)
     bool timing = false;
     DevBuf c13, sdf4, lat, out4, glat, qpw, qpst, wws;
     // host-pointer path (sdf_eval_host, the CasADi external): pinned staging, its own hoist buffer and
@@ -146,6 +148,8 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
     HIPCHK(sdf_set_lds_limits());
     auto* c = new sdfnmpc_ctx();
     c->device = device;
+    c->n_cu = prop.multiProcessorCount;
+    c->lds_per_cu = prop.maxSharedMemoryPerMultiProcessor;
     if (stream) {
         c->stream = (hipStream_t)stream;
     } else {
@@ -277,6 +281,21 @@ extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N) {
     if (!ctx || N < 1) return -1;
     if (ctx->qp_kernel != SDFNMPC_QP_SEGMENTED) return SDFNMPC_QP_SERIAL;  // AUTO: serial until the segmented is faster
     return rti_qp_seg_supported(N) ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
+}
+
+extern "C" long long sdfnmpc_qp_lds_bytes(int N) {
+    return N < 1 ? -1 : (long long)qp_lds_bytes(N);
+}
+
+// Instances the context's device solves in one wave of QP workgroups: every CU holds as many
+// instances as its LDS fits (the QP keeps each instance's iterate, duals and record window in LDS;
+// rti_qp.hip: one 64-lane workgroup per instance, rti_qp_seg.hip: one workgroup of NSEG waves).
+extern "C" long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N) {
+    if (!ctx || N < 1) return -1;
+    if (ctx->n_cu <= 0 || ctx->lds_per_cu == 0) return -1;
+    const size_t per = sdfnmpc_ctx_qp_kernel(ctx, N) == SDFNMPC_QP_SEGMENTED ? qp_seg_lds_bytes(N) : qp_lds_bytes(N);
+    if (per == 0 || per > ctx->lds_per_cu) return 0;  // the horizon does not fit one CU's LDS
+    return (long long)ctx->n_cu * (long long)(ctx->lds_per_cu / per);
 }
 
 extern "C" int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows) {
@@ -1071,7 +1090,7 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
     if (o->lm <= 0.0 || o->max_iter < 1 || !(o->tol > 0.0))
         return fail(SDFNMPC_E_ARG, "qp opts: lm > 0 (strict convexity), max_iter >= 1, tol > 0 required");
     if (o->ny != 11 && o->ny != 12) return fail(SDFNMPC_E_ARG, "qp opts: ny must be 11 or 12 (sdf_cost)");
-    if (qp_lds_bytes(a->N) > 160 * 1024) return fail(SDFNMPC_E_UNSUPPORTED, "horizon too long for the LDS-resident QP");
+    if (qp_lds_bytes(a->N) > ctx->lds_per_cu) return fail(SDFNMPC_E_UNSUPPORTED, "horizon too long for the LDS-resident QP");
     HIPCHK(ctx->qpw.ensure((size_t)a->B * qp_work_doubles(a->N) * sizeof(double)));
     const bool own_st = !a->status || !a->iters || !a->res;
     if (own_st) HIPCHK(ctx->qpst.ensure((size_t)a->B * (2 * sizeof(int) + 2 * sizeof(double))));

@@ -16,7 +16,7 @@ layouts are the reference's (plus an optional leading batch dimension):
   solver.get(k, 'x' | 'u'), solver.set(k, ...), solver.reset(), solver.get_stats('time_tot')
 
 Occupancy gate (north_star): with several ``devices`` the batch is split over as
-many GPUs as it needs to fill (``shard.plan``: one GPU runs up to ``shard.gpu_capacity(N)`` instances
+many GPUs as it needs to fill (``shard.plan``: one GPU runs up to ``Context.qp_capacity(N)`` instances
 concurrently -- 1024 at N = 40), each part a contiguous instance range with its own context, network
 copy and solver; a step enqueues every part before waiting on any.
 
@@ -143,10 +143,14 @@ class Ocp:
         self.qp_opts = _lib.qp_opts(model, lm=float(cfg.mpc.lm_reg if lm is None else lm), max_iter=qp_iter_max,
                                     tol=qp_tol, lm_scaling=lm_scaling)
         devs = list(devices) if devices else [device]
-        self.plan = shard.plan(B, N, len(devs)) if ctx is None else [(0, 0, B)]
+        if ctx is None:  # the first device's context sizes the plan (sdfnmpc_qp_capacity)
+            c0 = _lib.Context(devs[0])
+            self.plan = shard.plan(B, c0.qp_capacity(N), len(devs))
+        else:
+            c0, self.plan = ctx, [(0, 0, B)]
         self.parts = []
         for slot, lo, hi in self.plan:
-            c = ctx if ctx is not None else _lib.Context(devs[slot])
+            c = c0 if slot == 0 else _lib.Context(devs[slot])
             n = net if (net is not None and slot == 0) else load_net(c, cfg, weights)
             s = _lib.Solver(c, n, self.cmodel, self.qp_opts, hi - lo, N, model.np, model.ny, self.dt)
             self.parts.append(_Part(lo, hi, c, n, s, ctx is None, n is not net))

@@ -19,34 +19,17 @@ def instance_range(total: int, world: int, rank: int):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
-# Occupancy of one MI355X for the feedback-phase QP (csrc/rti_qp.hip), the kernel a batch fills last:
-# one wavefront per instance, its iterate / duals / stream window LDS-resident, so the instances one
-# GPU runs concurrently are (LDS per CU // LDS per instance) x CUs.  Mirrors qp_lds_doubles() in
-# csrc/qp_kernels.h.
-GPU_CUS = 256
-LDS_PER_CU = 160 * 1024
-
-
-def qp_lds_bytes(N: int) -> int:
-    even = lambda n: (n + 1) & ~1  # noqa: E731
-    N1, m = N + 1, 8 * N + 12 * (N + 1)
-    d = (2 * even(m) + 2 * even(N1 * 10) + 3 * even(N * 4) + 2 * even(N1 * 3) + 5 * 64 + 3 * 168 + 48 + 2
-         + even(N * 4) + even(N1 * 3) + even(N1) + 2 * even(N1 * 3) + 2 * even(N * 4) + 20)
-    return 8 * d
-
-
-def gpu_capacity(N: int) -> int:
-    """Instances one GPU solves in a single wave of QP workgroups (1024 at N = 40)."""
-    return GPU_CUS * max(1, LDS_PER_CU // qp_lds_bytes(N))
-
-
-def plan(total: int, N: int, n_devices: int):
+def plan(total: int, capacity: int, n_devices: int):
     """The north_star's occupancy gate: shard the batch over more GPUs only when it exceeds what the GPUs
     in use already run concurrently -- G = min(n_devices, ceil(total / capacity)) devices, each with a
-    contiguous instance_range.  Returns [(device_slot, lo, hi)]."""
+    contiguous instance_range.  `capacity` = instances one GPU solves in one wave of QP workgroups, from
+    the library and the device (sdfnmpc_qp_capacity, _lib.Context.qp_capacity).
+    Returns [(device_slot, lo, hi)]."""
     if n_devices < 1:
         raise ValueError("no device to plan on")
-    G = max(1, min(n_devices, -(-total // gpu_capacity(N))))
+    if capacity < 1:
+        raise ValueError("the QP does not fit one GPU at this horizon (capacity 0)")
+    G = max(1, min(n_devices, -(-total // capacity)))
     return [(g,) + instance_range(total, G, g) for g in range(G)]
 
 

@@ -80,6 +80,27 @@ def test_two_rank_sharded_rti_equals_single_process():
     np.testing.assert_array_equal(full, ref)
 
 
+def test_qp_capacity_from_the_library():
+    """The occupancy gate's capacity comes from the C ABI (sdfnmpc_qp_capacity: device CUs x LDS per CU
+    // the kernel's LDS per instance) at N in {20, 40, 60, 80}; 1024 instances at N = 40 on an MI355X."""
+    import torch
+    from sdf_nmpc_amd import _lib
+    ctx = _lib.Context(0)
+    prop = torch.cuda.get_device_properties(0)
+    cus = prop.multi_processor_count
+    lds = 160 * 1024  # gfx950 LDS per CU
+    caps = {}
+    for N in (20, 40, 60, 80):
+        per = int(_lib.load().sdfnmpc_qp_lds_bytes(N))
+        assert per > 0
+        caps[N] = ctx.qp_capacity(N)
+        assert caps[N] == cus * (lds // per), (N, caps[N], cus, per)
+    assert caps[40] == 1024 and caps[20] >= caps[40] >= caps[60] >= caps[80] > 0
+    assert ctx.qp_capacity(400) == 0  # no instance of that horizon fits one CU's LDS
+    with pytest.raises(_lib.SdfnmpcError):
+        ctx.qp_capacity(0)
+
+
 def test_ocp_occupancy_gate_parts_equal_one_part():
     """Ocp over two device slots (both cuda:0 here): a batch above one GPU's capacity at N = 60 (512
     instances) is split into two parts by shard.plan; the result equals a single-part solve bitwise."""
@@ -90,7 +111,9 @@ def test_ocp_occupancy_gate_parts_equal_one_part():
     from sdf_nmpc_amd.ocp import Ocp
     from sdf_nmpc_amd.reference import Ref, yaw2quat
     Bt, cfg = 600, Config(mpc__N=60)
-    assert shard.gpu_capacity(60) == 512 and len(shard.plan(Bt, 60, 2)) == 2 and len(shard.plan(512, 60, 8)) == 1
+    from sdf_nmpc_amd import _lib
+    cap = _lib.Context(0).qp_capacity(60)
+    assert cap == 512 and len(shard.plan(Bt, cap, 2)) == 2 and len(shard.plan(512, cap, 8)) == 1
     rng = np.random.default_rng(4)
     x0 = np.zeros((Bt, 10))
     x0[:, :3] = rng.uniform(-1, 1, (Bt, 3))

@@ -8,7 +8,7 @@ import socket
 import numpy as np
 import pytest
 
-from sdf_nmpc_amd.shard import instance_range
+from sdf_nmpc_amd.shard import instance_range, plan
 
 
 @pytest.mark.parametrize("total,world", [(1024, 1), (1024, 8), (8192, 8), (1000, 3), (5, 8), (0, 2)])
@@ -20,6 +20,18 @@ def test_instance_ranges_partition(total, world):
         seen[lo:hi] += 1
         sizes.append(hi - lo)
     assert (seen == 1).all() and max(sizes) - min(sizes) <= 1
+
+
+def test_plan_occupancy_gate():
+    """shard.plan: G = min(devices, ceil(total / capacity)) contiguous parts; capacity 0 is refused."""
+    assert plan(1024, 1024, 8) == [(0, 0, 1024)]
+    assert plan(1025, 1024, 8) == [(0, 0, 513), (1, 513, 1025)]
+    assert [p[0] for p in plan(8192, 1024, 8)] == list(range(8))
+    assert len(plan(100000, 1024, 4)) == 4
+    with pytest.raises(ValueError):
+        plan(10, 0, 2)
+    with pytest.raises(ValueError):
+        plan(10, 1024, 0)
 
 
 def _free_port():
