@@ -41,6 +41,9 @@ def host_cpus():
     except (OSError, ValueError):
         pass
     info["cgroup_cpu_quota"] = quota
+    # threads that can run at once: the affinity set, capped by the cgroup's CPU quota (oversubscribing a
+    # 16-CPU quota with 256 threads measured 2.4x slower on the GPU box than 16 threads)
+    usable = info["affinity"] if quota is None else max(1, min(info["affinity"], int(quota + 0.5)))
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
         for line in out.splitlines():
@@ -49,7 +52,11 @@ def host_cpus():
                 info[k.strip()] = v.strip()
     except (OSError, subprocess.SubprocessError):
         pass
-    return info["affinity"], info
+    try:
+        info["physical_cores"] = int(info["Core(s) per socket"]) * int(info["Socket(s)"])
+    except (KeyError, ValueError):
+        info["physical_cores"] = None
+    return usable, info
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -318,8 +325,11 @@ def main():
                "sample": f"{S} of the {B} instances x {N + 1} nodes, best of 2 passes ({reps[0]:.2f} s, {reps[1]:.2f} s "
                          f"wall on {threads} threads): C oracle preparation (oracle/oracle.c, fp32 MLP + fp64 "
                          f"linearisation) + structured Riccati IPM QP (oracle/qp_ipm.c), OpenMP over instances on "
-                         f"every CPU the process may run on; 1-thread rate on {S1} instances = {S1 / cpu1_s:.1f}/s",
-               "value_1thread": S1 / cpu1_s, "host": host}
+                         f"every CPU the process may use at once (affinity set capped by the cgroup CPU quota); 1-thread rate on {S1} instances = {S1 / cpu1_s:.1f}/s",
+               "value_1thread": S1 / cpu1_s, "host": host,
+               # not measured: the whole host is not this process's to use (cgroup quota); the 1-thread rate
+               # x the host's physical cores is the ideal-scaling bound of an all-core run
+               "projected_all_cores": (S1 / cpu1_s * host["physical_cores"]) if host.get("physical_cores") else None}
 
     out = {
         "metric": "NMPC solves/sec at batch×N=1024×40 on 1/2/4/8 GPUs; p50 control-step latency",

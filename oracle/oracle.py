@@ -61,6 +61,7 @@ def lib():
                                             P(f), P(f)]
         _lib.orc_vae_encode.argtypes = [P(f), C.c_int, C.c_int, C.c_int, P(f), C.c_int, C.c_int, P(d), P(d)]
         _lib.orc_vae_set_threads.argtypes = [C.c_int]
+        _lib.orc_qp_trace.argtypes = [C.c_void_p, C.c_int]
     return _lib
 
 
@@ -170,7 +171,7 @@ QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", 
 
 
 # IPM starting point / step fraction of csrc/rti_qp.hip (QP_T0, QP_L0, QP_LC, QP_TAU_LO, QP_TAU_HI)
-QP_START = dict(t0=0.5, l0=1.0, lc=0.5, tau_lo=0.995, tau_hi=0.995, seg=1)
+QP_START = dict(t0=0.5, l0=1.0, lc=0.5, tau_lo=0.995, tau_hi=0.995, seg=1, gk=0, ga=1.0, gd=0.1, gbmin=0.1, gbmax=10.0)
 
 
 def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_scaling=True, nthreads=1, lm_scaling=True,
@@ -188,13 +189,14 @@ def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_sca
     opts = np.concatenate([model.lbu, model.ubu, model.lh, model.uh, model.zl, model.Zl, [lm, tol, float(bool(lm_scaling))],
                            [v for v in {**QP_START, **(start or {})}.values()]]).astype(np.float64)
     out = dict(dx=np.zeros((B, N + 1, 10)), du=np.zeros((B, N, 4)), slack=np.zeros((B, N + 1, 3, 2)),
-               iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32), res=np.zeros((B, 3)))
+               iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32), res=np.zeros((B, 4)))
     d = C.c_double
     ny = arrs["W"].shape[-1]
     lib().orc_qp_ipm_batch(B, N, *[_p(arrs[k], d) for k in QP_IN], _p(dt, d), _p(opts, d), max_iter,
                            int(bool(cost_scaling)), ny, _p(out["dx"], d), _p(out["du"], d), _p(out["slack"], d),
                            _p(out["iters"], C.c_int), _p(out["status"], C.c_int), _p(out["res"], d), nthreads)
     out["seg_dev"] = out["res"][:, 2].copy()  # segmented solve: gap between a segment's own x_b and the coupled one
+    out["gondzio"] = out["res"][:, 3].astype(np.int32)  # Gondzio correctors kept
     out["res"] = np.ascontiguousarray(out["res"][:, :2])
     return out
 

@@ -30,6 +30,11 @@ typedef struct {
     double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3], lm, tol;
     int max_iter, cost_scaling, lm_scaling, nseg;
     double t0, l0, lc, tau_lo, tau_hi;  /* starting point / step fraction (rti_qp.hip's QP_T0 ... QP_TAU_HI) */
+    /* Gondzio centrality correctors (off at gk = 0): up to gk extra solves on the factorisation of the
+     * iteration when the Mehrotra step is below ga; trial step min(1, alpha + gd), products projected
+     * onto [gbmin, gbmax] sigma mu; a corrector is kept when it lengthens the step by >= 0.1 gd */
+    int gk;
+    double ga, gd, gbmin, gbmax;
 } qp_opts_c;
 
 typedef struct {                  /* stage k < N, or the terminal node k = N (x part only) */
@@ -81,6 +86,7 @@ typedef struct {
     double* G;                    /* N x NU x NX: terminal-multiplier gains of the segmented solve */
     int nseg;                     /* segments of the partitioned Riccati (1: the serial recursion) */
     double seg_dev;               /* max relative gap between a segment's own x_b and the coupled one */
+    int gcount;                   /* Gondzio correctors kept (diagnostic) */
 } ipm_t;
 
 static void rows_at(const ipm_t* Q, const double* dx, const double* du, const double* sl, const double* su, double* v) {
@@ -520,6 +526,13 @@ static double step_max(int m, const double* t, const double* l, const double* dt
     return a;
 }
 
+/* diagnostic trace (tools/ipm_trace.py; single instance, one thread): per iteration
+ * [alpha_aff, alpha, mu, max t*lambda, rp, sigma*mu, the row of the max product, its t, its lambda] */
+#define TRACE_W 9
+static double* g_trace = NULL;
+static int g_trace_max = 0;
+void orc_qp_trace(double* buf, int max_rows) { g_trace = buf; g_trace_max = buf ? max_rows : 0; }
+
 /* One instance.  Returns IPM iterations (status via *conv: 1 converged). */
 static int solve_one(int N, const double* xn, const double* AB, const double* y, const double* Jy, const double* yN,
                      const double* JyN, const double* h, const double* Jh, const double* x, const double* u,
@@ -537,15 +550,19 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     Q.G = (double*)calloc((size_t)N * NU * NX, sizeof(double));
     Q.nseg = o->nseg;
     Q.seg_dev = 0.0;
-    double* buf = (double*)calloc((size_t)(12 * m + 4 * (N1 * NX + N * NU + 2 * N1 * NS)), sizeof(double));
+    Q.gcount = 0;
+    double* buf = (double*)calloc((size_t)(16 * m + 5 * (N1 * NX + N * NU + 2 * N1 * NS)), sizeof(double));
     double *t = buf, *lam = t + m, *sig = lam + m, *v = sig + m, *rv = v + m, *dta = rv + m, *dla = dta + m;
     double *dtc = dla + m, *dlc = dtc + m, *rw = dlc + m;  /* rw: spare */
     (void)rw;
-    double* zs = buf + 12 * m;
+    double* zs = buf + 12 * m;  /* 5 z-vectors, then dtg, dlg, gcum (3 m) */
     const int nz = N1 * NX + N * NU + 2 * N1 * NS;
     double *zdx = zs, *zdu = zdx + N1 * NX, *zsl = zdu + N * NU, *zsu = zsl + N1 * NS;          /* iterate */
     double *adx = zs + nz, *adu = adx + N1 * NX, *asl = adu + N * NU, *asu = asl + N1 * NS;     /* affine */
     double *cdx = zs + 2 * nz, *cdu = cdx + N1 * NX, *csl = cdu + N * NU, *csu = csl + N1 * NS; /* corrector */
+    double* gz = zs + 4 * nz;                                                                   /* Gondzio */
+    double *gdx = gz, *gdu = gdx + N1 * NX, *gsl = gdu + N * NU, *gsu = gsl + N1 * NS;
+    double *dtg = zs + 5 * nz, *dlg = dtg + m, *gcum = dlg + m;
 
     /* ---- stage data (the pack step of rti_qp.hip) */
     for (int k = 0; k <= N; ++k) {
@@ -668,7 +685,35 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         double tau = 1.0 - mu;  /* step fraction min(tau_hi, max(tau_lo, 1 - mu)) */
         if (tau < o->tau_lo) tau = o->tau_lo;
         if (tau > o->tau_hi) tau = o->tau_hi;
-        double al = tau * step_max(m, t, lam, dtc, dlc);
+        double amax = step_max(m, t, lam, dtc, dlc);
+        for (int gi = 0; gi < o->gk && amax < o->ga; ++gi) {  /* Gondzio correctors */
+            double at = amax + o->gd;
+            if (at > 1.0) at = 1.0;
+            const double lo = o->gbmin * sigmu, hi = o->gbmax * sigmu;
+            for (int r = 0; r < m; ++r) {
+                const double pv = (t[r] + at * dtc[r]) * (lam[r] + at * dlc[r]);
+                double c = 0.0;
+                if (pv < lo) c = lo - pv;
+                else if (pv > hi) c = (hi - pv) > -hi ? hi - pv : -hi;
+                rw[r] = c;  /* extra complementarity right-hand side */
+                v[r] = sig[r] * (t[r] - d0[r]) - (dta[r] * dla[r] - sigmu - rw[r] - gcum[r]) / t[r];
+            }
+            if (Q.nseg > 1 ? lqr_seg(&Q, Q.nseg, sig, v, gdx, gdu, gsl, gsu) : lqr(&Q, sig, v, gdx, gdu, gsl, gsu)) { fail = 1; break; }
+            rows_at(&Q, gdx, gdu, gsl, gsu, rv);
+            for (int r = 0; r < m; ++r) {
+                dtg[r] = rv[r] - t[r];
+                dlg[r] = -sig[r] * dtg[r] - lam[r] - (dta[r] * dla[r] - sigmu - rw[r] - gcum[r]) / t[r];
+            }
+            const double an = step_max(m, t, lam, dtg, dlg);
+            if (an < amax + 0.1 * o->gd) break;
+            amax = an;
+            for (int r = 0; r < m; ++r) { dtc[r] = dtg[r]; dlc[r] = dlg[r]; gcum[r] += rw[r]; }
+            memcpy(zs + 2 * nz, gz, sizeof(double) * nz);
+            Q.gcount++;
+        }
+        if (fail) break;
+        for (int r = 0; r < m; ++r) gcum[r] = 0.0;
+        double al = tau * amax;
         if (al > 1.0) al = 1.0;
         mu = 0.0;
         cm = 0.0;
@@ -682,6 +727,13 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         for (int e = 0; e < nz; ++e) zs[e] += al * (zs[2 * nz + e] - zs[e]);
         rp *= (1.0 - al);
         gap *= (1.0 - al);
+        if (g_trace && it < g_trace_max) {
+            double* tr = g_trace + (size_t)it * TRACE_W;
+            int rm = 0;
+            for (int r = 1; r < m; ++r)
+                if (t[r] * lam[r] > t[rm] * lam[rm]) rm = r;
+            tr[0] = aa + 10.0 * Q.gcount; tr[1] = al; tr[2] = mu; tr[3] = cm; tr[4] = rp; tr[5] = sigmu; tr[6] = rm; tr[7] = t[rm]; tr[8] = lam[rm];
+        }
         ++it;
 
     }
@@ -694,7 +746,7 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         }
     if (!isfinite(mu + rp)) fail = 1;
     *conv = fail ? -1 : (cm < o->tol && rp < o->tol && gap < o->tol);
-    if (res) { res[0] = cm; res[1] = rp; res[2] = Q.seg_dev; }
+    if (res) { res[0] = cm; res[1] = rp; res[2] = Q.seg_dev; res[3] = Q.gcount; }
     free(d0); free(buf); free(Q.st); free(Q.P); free(Q.p); free(Q.K); free(Q.kf); free(Q.G);
     return it;
 }
@@ -718,6 +770,7 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
     o.lm_scaling = opts[22] != 0.0;
     o.t0 = opts[23]; o.l0 = opts[24]; o.lc = opts[25]; o.tau_lo = opts[26]; o.tau_hi = opts[27];
     o.nseg = (int)opts[28];
+    o.gk = (int)opts[29]; o.ga = opts[30]; o.gd = opts[31]; o.gbmin = opts[32]; o.gbmax = opts[33];
     o.max_iter = max_iter;
     o.cost_scaling = cost_scaling;
     const int N1 = N + 1;
@@ -730,7 +783,7 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
                              u + (size_t)b * N * NU, x0 + (size_t)b * NX, yref + (size_t)b * N * ny,
                              W + (size_t)b * N * ny, yNref + (size_t)b * 4, WN + (size_t)b * 4, dt, &o, ny,
                              dx + (size_t)b * N1 * NX, du + (size_t)b * N * NU,
-                             slack ? slack + (size_t)b * N1 * NS * 2 : NULL, &conv, res ? res + 3 * b : NULL);
+                             slack ? slack + (size_t)b * N1 * NS * 2 : NULL, &conv, res ? res + 4 * b : NULL);
         status[b] = conv < 0 ? 2 : conv ? 0 : 1;
     }
 }
