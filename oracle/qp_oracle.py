@@ -134,6 +134,37 @@ def polish(q, sol, act_tol=1e-7):
     return out
 
 
+def polish_active_set(q, sol, act_tol=1e-7, max_swaps=200):
+    """polish() followed by active-set corrections until the KKT conditions hold: a violated row joins
+    the active set, an active row with a negative multiplier leaves it (one change per solve, the worst
+    first).  For a strictly convex QP the point that passes is its unique solution; near-degenerate
+    vertices (weakly active rows the IPM leaves at slack ~1e-6) need this where a single threshold cut
+    of the IPM point picks a wrong set."""
+    H, g, E, e, G, d = dense_problem(q)
+    z0 = np.concatenate([sol["dx"].ravel(), sol["du"].ravel(), sol["sl"].ravel(), sol["su"].ravel()])
+    act = (G @ z0 + d) < act_tol
+    nz, ne = H.shape[0], E.shape[0]
+    for _ in range(max_swaps):
+        Ga, da = G[act], d[act]
+        na = Ga.shape[0]
+        K = np.block([[H, E.T, -Ga.T], [E, np.zeros((ne, ne)), np.zeros((ne, na))], [Ga, np.zeros((na, ne + na))]])
+        x = np.linalg.lstsq(K, np.concatenate([-g, e, -da]), rcond=None)[0]
+        z, lam = x[:nz], x[nz + ne:]
+        viol = G @ z + d
+        iv = int(np.argmin(viol))
+        il = int(np.argmin(lam)) if na else -1
+        if viol[iv] < -1e-10 and (na == 0 or -viol[iv] >= -lam[il]):
+            act[iv] = True
+        elif na and lam[il] < -1e-10:
+            act[np.flatnonzero(act)[il]] = False
+        else:
+            break
+    out = _unpack(q, z)
+    out["min_dual"] = lam.min() if na else 0.0
+    out["max_violation"] = max(0.0, -viol.min())
+    return out
+
+
 def solve_dense(q, tol=1e-11, max_iter=100):
     """Mehrotra IPM on the full KKT system.  Returns dict(dx [N+1,10], du [N,4], sl, su [N+1,3], iters)."""
     N = q["N"]

@@ -29,7 +29,7 @@ def oracle_lib():
 def golden():
     import numpy as np
     d = os.path.join(ROOT, "tests", "golden")
-    return {k: np.load(os.path.join(d, f"{k}_golden.npz")) for k in ("sdf", "lin", "grid", "params")}
+    return {k: np.load(os.path.join(d, f"{k}_golden.npz")) for k in ("sdf", "lin", "grid", "params", "sdfc3")}
 
 
 @pytest.fixture(scope="session")

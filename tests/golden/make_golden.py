@@ -499,6 +499,38 @@ def wide_golden(n=128):
     print("wide_golden.npz", {k: v.shape for k, v in out.items()})
 
 
+def sdfc3_golden(stride=32):
+    """The reference's own NeuralDF (SIREN-init, seed 0) in fp32 and fp64 on every `stride`-th SDF row of
+    the bench workload C3 (1024 instances x 41 nodes, synthetic seed 1000): body positions in the
+    camera-origin frame (gen_model.py:50, as h_np) from the synthetic iterate and camera poses, and each
+    instance's latent -- the rows sdf_mlp sees in bench.py."""
+    from sdf_nmpc_amd import synth, _lib
+    from sdf_nmpc_amd.config import Config as AmdConfig
+    cfg = AmdConfig()
+    B, N = 1024, 40
+    _, dt = _lib.shooting_grid(N, cfg.mpc.T)  # as bench.py
+    prob = synth.make_problem(cfg, B, N, seed=1000, dt=dt)
+    x, pp = prob["x"].reshape(-1, 10), prob["p"].reshape(B * (N + 1), -1)
+    rows = np.arange(0, B * (N + 1), stride)
+    W_R_Co = pp[rows][:, P_IDX.W_R_Co].reshape(-1, 3, 3)
+    W_p_Co = pp[rows][:, P_IDX.W_p_Co]
+    pos = np.einsum("nji,nj->ni", W_R_Co, x[rows, :3] - W_p_Co)
+    lat = pp[rows][:, P_IDX.latent:P_IDX.latent + W.DEFAULT_SPEC.size_latent]
+    inp = np.concatenate([pos, lat], 1).astype(np.float32)
+    params = W.siren_weights(W.DEFAULT_SPEC, seed=0)
+    out = {"input": inp, "rows": rows, "sha256": np.frombuffer(hashlib.sha256(W.pack(W.DEFAULT_SPEC, params)).digest(),
+                                                                  dtype=np.uint8)}
+    for dtp, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        net = ref_net(W.DEFAULT_SPEC, params, dtp)
+        xx = torch.from_numpy(inp).to(dtp).requires_grad_(True)
+        df = net(xx)
+        (g,) = torch.autograd.grad(df.sum(), xx)
+        out[f"df_{tag}"] = df.detach().numpy()[:, 0]
+        out[f"grad_{tag}"] = g.numpy()[:, :3]
+    np.savez_compressed(os.path.join(HERE, "sdfc3_golden.npz"), **out)
+    print("sdfc3_golden.npz", {k: v.shape for k, v in out.items()})
+
+
 def vae_golden():
     import copy as _copy
     from sdf_nmpc.network.vae import Encoder
@@ -559,6 +591,6 @@ def vae_golden():
 if __name__ == "__main__":
     only = sys.argv[1:]
     for name, fn in (("sdf", sdf_golden), ("lin", lin_golden), ("grid", grid_golden), ("params", params_golden),
-                     ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden), ("wide", wide_golden)):
+                     ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden), ("wide", wide_golden), ("sdfc3", sdfc3_golden)):
         if not only or name in only:
             fn()

@@ -14,7 +14,10 @@ GPU and the oracle agree to U0_ATOL at every step.  With the flag on, the soft F
 random latents make the loop itself chaotic: a 1e-7 relative change of the latents -- the size of the
 fp32 rounding differences between any two SDF implementations -- grows about 5x per step in the
 oracle alone (2e-5 by step 4, O(1) by step 8).  There the check is that the GPU stays inside that
-envelope: |u_gpu - u_oracle| <= max(U0_ATOL, ENVELOPE x |u_oracle - u_oracle(latent x (1 + 1e-7))|)."""
+envelope: |u_gpu - u_oracle| <= max(U0_ATOL, ENVELOPE x |u_oracle - u_oracle(latent x (1 + 1e-7))|).
+The chaos comes from the synthetic network's df (~0) sitting below the SDF bound (0.37): every SDF row
+is active.  With the bound lowered under the network's range (mpc.bound_margin = -0.6) the flag-on loop
+is contractive -- the SDF rows live in every QP but inactive -- and all K steps are pinned to U0_ATOL."""
 import numpy as np
 import pytest
 
@@ -59,10 +62,16 @@ def _oracle_loop(O, onet, n, cfg, x0, p, K):
     return np.array(u_hist), xs, us
 
 
-@pytest.mark.parametrize("shift,flag", [(0, 0.0), (1, 0.0), (0, 1.0), (1, 1.0)])
-def test_closed_loop_matches_oracle_pipeline(oracle_lib, shift, flag):
+@pytest.mark.parametrize("shift,flag,margin", [(0, 0.0, None), (1, 0.0, None), (0, 1.0, None), (1, 1.0, None),
+                                                (0, 1.0, -0.6), (1, 1.0, -0.6)])
+def test_closed_loop_matches_oracle_pipeline(oracle_lib, shift, flag, margin):
+    """margin = -0.6 (mpc.bound_margin): the SDF lower bound drops below the synthetic network's range, so
+    with the flag on the SDF rows are live (h[2] = the network's df, J_h row 2 its gradient, every node)
+    but inactive; the loop is then contractive (tools/closed_loop_probe.py: a 1e-7 latent change stays
+    at 1e-8) and all K steps are pinned to U0_ATOL with the SDF in the QP."""
     O = oracle_lib
-    cfg = Config(mpc__N=20, mpc__shift=shift)
+    over = {} if margin is None else {"mpc__bound_margin": margin}
+    cfg = Config(mpc__N=20, mpc__shift=shift, **over)
     B = 4
     n = Nmpc(cfg, batch=B)
     x0 = scenario(n, np.random.default_rng(31))
@@ -78,7 +87,12 @@ def test_closed_loop_matches_oracle_pipeline(oracle_lib, shift, flag):
     ug = np.array(ug)
     uo, xs, us = _oracle_loop(O, onet, n, cfg, x0, n.p, K)
     d = np.abs(ug - uo).max(axis=(1, 2))
-    if flag == 0.0:  # contractive loop: step-by-step parity, and the carried iterates agree
+    if margin is not None:  # the SDF rows are live and inactive along the whole loop
+        lin = O.linearize_batch(O.quad_model(cfg), onet, xs, us, n.p, n.ocp.dt)
+        h2 = lin["h"][..., 2]
+        assert np.abs(lin["Jh"][..., 2]).max() > 1e-3 and np.ptp(h2) > 1e-3
+        assert (h2 > n.model.lh[2] + 0.05).all() and (h2 < n.model.uh[2] - 0.05).all()
+    if flag == 0.0 or margin is not None:  # contractive loop: step-by-step parity, carried iterates agree
         assert d.max() <= U0_ATOL, d
         xgpu, ugpu = n.get_matrices()
         np.testing.assert_allclose(ugpu, us, rtol=0, atol=U0_ATOL)

@@ -65,6 +65,68 @@ def test_qp_matches_exact_solution(gpu_ctx, oracle_lib, cfg, B, N, seed):
         np.testing.assert_allclose(sl[..., 1], ref["su"], rtol=0, atol=SOL_ATOL)
 
 
+@pytest.mark.parametrize("kernel", ["serial", "segmented"])
+def test_qp_exact_solution_64_c3_instances(gpu_ctx, oracle_lib, kernel):
+    """64 QPs of the bench workload C3 (every 32nd instance + the 32 most degenerate of the rest) against
+    their exact, KKT-checked solutions (tests/golden/make_qp_exact.py), on the C oracle's linearisation so
+    both sides solve the same QP.  Every instance: status 0; objective within the stop test's duality-gap
+    bound m * tol of F*; (dx, du) and u_0 within the strong-convexity bound sqrt(2 (F - F*) / mu) of the
+    exact point (mu = the smallest eigenvalue of the (dx, du) Hessian, > 0 by the LM term) and within
+    5e-5 absolute; the fraction within SOL_ATOL is reported."""
+    import os, sys
+    import torch
+    import qp_oracle
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_qp_exact as MX
+    ex = np.load(os.path.join(os.path.dirname(__file__), "golden", "qp_exact_golden.npz"))
+    cfg, model, prob, x0, lin = MX.problem()
+    sel = ex["sel"]
+    B, N = len(sel), MX.N
+    dev = torch.device("cuda", gpu_ctx.device)
+    t = {k: torch.from_numpy(np.ascontiguousarray(v[sel])).to(dev) for k, v in lin.items()}
+    for k, v in dict(x=prob["x"], u=prob["u"], x0=x0, yref=prob["yref"], W=prob["W"], yNref=prob["yN"],
+                     WN=prob["WN"]).items():
+        t[k] = torch.from_numpy(np.ascontiguousarray(v[sel])).to(dev)
+    t["dt"] = torch.from_numpy(np.ascontiguousarray(prob["dt"])).to(dev)
+    for k, sh in dict(dx=(B, N + 1, 10), du=(B, N, 4), slack=(B, N + 1, 3, 2), res=(B, 2)).items():
+        t[k] = torch.full(sh, float("nan"), dtype=torch.float64, device=dev)
+    t["status"] = torch.full((B,), -1, dtype=torch.int32, device=dev)
+    t["iters"] = torch.full((B,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    gpu_ctx.set_qp_kernel(kernel)
+    try:
+        assert gpu_ctx.qp_kernel(N) == kernel
+        _lib.qp_solve(gpu_ctx, _lib.qp_opts(model, tol=QP_TOL), B, N, t)
+        gpu_ctx.synchronize()
+    finally:
+        gpu_ctx.set_qp_kernel("auto")
+    assert (t["status"].cpu().numpy() == 0).all()
+    du, dx, sl = t["du"].cpu().numpy(), t["dx"].cpu().numpy(), t["slack"].cpu().numpy()
+    nv = (N + 1) * 10 + N * 4
+    err_du, err_u0, bound = np.zeros(B), np.zeros(B), np.zeros(B)
+    for i, b in enumerate(sel):
+        q = qp_oracle.stage_qp({k: v[b] for k, v in lin.items()}, prob["x"][b], prob["u"][b], x0[b], prob["yref"][b],
+                               prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], model, 10.0)
+        H, g, E, e, G, d = qp_oracle.dense_problem(q)
+        z = np.concatenate([dx[i].ravel(), du[i].ravel(), sl[i][..., 0].ravel(), sl[i][..., 1].ravel()])
+        zs = np.concatenate([ex["dx"][i].ravel(), ex["du"][i].ravel(), ex["sl"][i].ravel(), ex["su"][i].ravel()])
+        assert np.abs(E @ z - e).max() < 1e-9 and (G @ z + d).min() > -1e-8
+        dF = 0.5 * z @ H @ z + g @ z - ex["F"][i]
+        assert dF <= G.shape[0] * QP_TOL, (b, dF)
+        # strong convexity in (dx, du) of the objective minimised over the slacks: F(z) - F* >= mu/2 |dz|^2
+        # (+1e-9: the stopped point is feasible to 1e-9, which can put F below F* by that order)
+        bound[i] = np.sqrt(2.0 * (max(dF, 0.0) + 1e-9) / ex["mu"][i])
+        dz = np.linalg.norm((z - zs)[:nv])
+        err_u0[i] = np.abs(du[i, 0] - ex["du"][i, 0]).max()
+        err_du[i] = np.abs(du[i] - ex["du"][i]).max()
+        assert dz <= bound[i] and err_u0[i] <= bound[i], (b, dz, err_u0[i], bound[i])
+    print(f"\n{kernel}: |du - du*| max {err_du.max():.2e} median {np.median(err_du):.2e}, within {SOL_ATOL:g} on "
+          f"{(err_du <= SOL_ATOL).sum()}/{B}; |u0 - u0*| max {err_u0.max():.2e}; strong-convexity bound max "
+          f"{bound.max():.2e}; iterations max {t['iters'].cpu().numpy().max()}")
+    assert err_du.max() <= 5e-5
+    np.testing.assert_allclose(dx, ex["dx"], rtol=0, atol=5e-5)
+
+
 def test_qp_full_size_feasibility_and_determinism(gpu_ctx, cfg):
     """B=1024, N=40: every instance converges within qp_solver_iter_max = 100 (ocp.py:115); the solution
     satisfies the input boxes, x0 and the linearised dynamics; two solves agree bit for bit."""

@@ -41,6 +41,27 @@ def test_oracle_f64_equals_reference_f64(golden, oracle_lib, variant):
     assert np.array_equal(gp, gf[:, :3])
 
 
+def test_oracle_f64_equals_reference_f64_on_c3_rows(golden, oracle_lib, cfg):
+    """The C3-row fixture (every 32nd SDF row of the bench workload): its inputs are the rows the bench
+    builds (camera-frame body positions from the synthetic iterate, the instance latents), and the fp64
+    restatement reproduces the reference's fp64 outputs on them."""
+    from sdf_nmpc_amd import _lib, synth
+    g = golden["sdfc3"]
+    params = W.siren_weights(W.DEFAULT_SPEC, 0)
+    assert hashlib.sha256(W.pack(W.DEFAULT_SPEC, params)).digest() == g["sha256"].tobytes()
+    _, dt = _lib.shooting_grid(40, cfg.mpc.T)
+    prob = synth.make_problem(cfg, 1024, 40, seed=1000, dt=dt)
+    rows = g["rows"]
+    x, p = prob["x"].reshape(-1, 10)[rows], prob["p"].reshape(1024 * 41, -1)[rows]
+    pos = np.einsum("nji,nj->ni", p[:, 4:13].reshape(-1, 3, 3), x[:, :3] - p[:, 1:4])
+    np.testing.assert_array_equal(g["input"][:, :3], pos.astype(np.float32))
+    np.testing.assert_array_equal(g["input"][:, 3:], p[:, 17:].astype(np.float32))
+    net = oracle_lib.Net(W.DEFAULT_SPEC, params)
+    df, gp, _ = net.f64(g["input"].astype(np.float64))
+    assert np.abs(df - g["df_f64"]).max() < 1e-12
+    assert np.abs(gp - g["grad_f64"]).max() < 1e-12
+
+
 def test_oracle_f32_within_parity_bar(golden, oracle_lib):
     """fp32 restatement vs the reference fp32 / fp64 on deployed-scale (SIREN-init) weights."""
     g = golden["sdf"]

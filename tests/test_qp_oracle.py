@@ -122,3 +122,35 @@ def test_riccati_ipm_solution_is_feasible(oracle_lib, cfg):
         lin["xn"] - prob["x"][:, 1:]
     np.testing.assert_allclose(r["dx"][:, 1:], pred, atol=1e-9)
     assert (r["slack"] >= -1e-8).all()
+
+
+def test_c_ipm_against_exact_c3_fixture(oracle_lib):
+    """The C restatement (the GPU kernels' algorithm) on the 64 C3 QPs of tests/golden/qp_exact_golden.npz:
+    converged, feasible, within the duality-gap bound of F*, and (dx, du) inside the strong-convexity ball
+    around the exact solution (the same checks tests/test_gpu_qp.py makes of the kernels)."""
+    import os
+    import sys
+    import qp_oracle
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import make_qp_exact as MX
+    ex = np.load(os.path.join(os.path.dirname(__file__), "golden", "qp_exact_golden.npz"))
+    cfg, model, prob, x0, lin = MX.problem()
+    sel, N = ex["sel"], MX.N
+    nv = (N + 1) * 10 + N * 4
+    r = oracle_lib.qp_ipm_batch({k: v[sel] for k, v in lin.items()},
+                                {k: (v if k == "dt" else v[sel]) for k, v in prob.items()}, x0[sel], model,
+                                tol=1e-8, nthreads=8)
+    assert (r["status"] == 0).all()
+    for i, b in enumerate(sel):
+        q = qp_oracle.stage_qp({k: v[b] for k, v in lin.items()}, prob["x"][b], prob["u"][b], x0[b], prob["yref"][b],
+                               prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], model, 10.0)
+        H, g, E, e, G, d = qp_oracle.dense_problem(q)
+        z = np.concatenate([r["dx"][i].ravel(), r["du"][i].ravel(), r["slack"][i][..., 0].ravel(),
+                            r["slack"][i][..., 1].ravel()])
+        zs = np.concatenate([ex["dx"][i].ravel(), ex["du"][i].ravel(), ex["sl"][i].ravel(), ex["su"][i].ravel()])
+        assert np.abs(E @ zs - e).max() < 1e-9 and (G @ zs + d).min() > -1e-9  # the fixture is feasible
+        assert np.abs(E @ z - e).max() < 1e-9 and (G @ z + d).min() > -1e-8
+        dF = 0.5 * z @ H @ z + g @ z - ex["F"][i]
+        assert -1e-9 <= dF <= G.shape[0] * 1e-8
+        assert np.linalg.norm((z - zs)[:nv]) <= np.sqrt(2.0 * (max(dF, 0.0) + 1e-9) / ex["mu"][i])
+    assert np.abs(r["du"] - ex["du"]).max() <= 5e-5
