@@ -17,7 +17,7 @@ struct QpArgs {
     int *status, *iters;
     double* res;      // [B][2] (mu, max primal residual)
     double* work;     // [B][qp_work_doubles(N)]
-    double* stamps;   // [B][16] cycle counters of the QP_STAMPS diagnostic build (NULL otherwise)
+    double* stamps;   // cycle counters of the stamps diagnostic builds, serial [B][16] / segmented [B][4][24] of the QP_STAMPS diagnostic build (NULL otherwise)
     // model / options
     double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3];
     double lm, tol;

@@ -71,7 +71,8 @@ __device__ __forceinline__ int src_granule(int K, int wg) {  // source granule (
 // of the wave's lanes parked during the factor sweep
 constexpr int CP_L = 0, CP_U = 56, CP_V = 112, CP_X = 212, CP_C = 312, CP_SC = 368, CP_M = 368, CP_LM = 468, CP_B = 568,
               CPL = QP_CPL;
-static_assert(CP_B + 10 <= CPL && CP_SC <= 2 * WIN, "coupling block");
+constexpr int CP_PHI = WIN;  // [Phi | beta] tile (16 x 16) from mchain to moff, in the second window
+static_assert(CP_B + 10 <= CPL && CP_SC <= WIN && CP_PHI + 256 <= 2 * WIN, "coupling block");
 
 __device__ __forceinline__ int trl(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower, j <= i
 
@@ -93,7 +94,7 @@ __device__ __forceinline__ void chol_cols(double (&col)[NX], double (&inv)[NX], 
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
         const double d = rdlane(col[j], j);
-        const double iv = rsqrt2(d);
+        const double iv = rsqrt_nr(d);
         inv[j] = iv;
         const double lcj = col[j] * iv;  // L[c][j] (A symmetric: A[j][c] = A[c][j])
 #pragma unroll
@@ -199,12 +200,12 @@ static_assert(F_NFIELD <= 26 && 8 * FRECS < 65536, "packed lane constants");
 
 }  // namespace
 
-#ifdef SEG_STAMPS  // diagnostic build only: per-wave, per-phase cycle accounting into A.stamps [B][4][16]
-#define SSTAMP_DECL long long st_t0 = clock64(), st_acc[16] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0}; int st_ph = 0;
+#ifdef SEG_STAMPS  // diagnostic build only: per-wave, per-phase cycle accounting into A.stamps [B][4][24]
+#define SSTAMP_DECL long long st_t0 = clock64(), st_acc[24] = {}; int st_ph = 0;
 #define SSTAMP_PHASE(i) st_ph = (i)
 #define SSTAMP(i) do { const long long t1_ = clock64(); st_acc[i] += t1_ - st_t0; st_t0 = t1_; } while (0)
 #define SSTAMP_ARRIVE(body) do { SSTAMP(st_ph); body; SSTAMP(15); } while (0)
-#define SSTAMP_OUT if (lane == 0 && A.stamps) for (int i_ = 0; i_ < 16; ++i_) A.stamps[((size_t)b * NSEG_MAX + w) * 16 + i_] = (double)st_acc[i_];
+#define SSTAMP_OUT if (lane == 0 && A.stamps) for (int i_ = 0; i_ < 24; ++i_) A.stamps[((size_t)b * NSEG_MAX + w) * 24 + i_] = (double)st_acc[i_];
 #else
 #define SSTAMP_DECL
 #define SSTAMP_PHASE(i)
@@ -218,6 +219,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
     __shared__ __align__(16) double lds_q[SegLds<NSEG, NMAX>::TOTAL];
     SSTAMP_DECL
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+    // Stage code re-derives its lane index behind opaque() (`const int lane = opaque(lane_k)`): the lane
+    // predicates are then recomputed per stage (a few VALU ops) instead of being hoisted to the prologue,
+    // where each one held a 64-bit SGPR mask for the whole kernel and the masks spilled to VGPR lanes.
+    const int lane_k = lane;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int N = A.N, N1 = N + 1, m = 8 * N + 12 * N1;
     const SegSmem s = seg_carve<NSEG, NMAX>((ldsd*)lds_q, w);
@@ -370,6 +375,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
     // lane r < 10: x_{k+1}[r]; 10..13: u_k; 14..16: (C x_k)_{r-14}.  K == 0: the initial iterate
     // (rows of A x + c from the stage record).  LAM: the costate term -[B G; G] lam_b of segments 0..2.
     auto fw_stage = [&](auto Kc, auto LAMc, int k, bool seg_end, const ldsd* cw, auto refill) {
+        const int lane = opaque(lane_k);
         constexpr int K = decltype(Kc)::value;
         constexpr bool LAM = decltype(LAMc)::value;
         const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 17;
@@ -432,6 +438,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
     d4 Psi = {0.0, 0.0, 0.0, 0.0};  // [Phi | beta]^T (rows 0..9: Phi^T, row 14: beta), segments 0..2
     d4 Cg = {0.0, 0.0, 0.0, 0.0};   // C, segments 0..2
     auto bf_stage = [&](auto Fc, auto AUGc, int k, const FConst& f, const ldsd* cw, auto refill) {
+        const int lane = opaque(lane_k);
         constexpr bool FIRST = decltype(Fc)::value;  // the terminal node
         constexpr bool AUG = decltype(AUGc)::value;
         const int g = lane >> 4, c = lane & 15;
@@ -579,6 +586,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
     double cfv = 0.0;    // the corrector's record row (b~ | k_ff) of node cpend, stored by the next stage
     int cpend = -1;
     auto bc_stage = [&](auto Fc, auto AUGc, int k, const ldsd* cw, auto refill) {
+        const int lane = opaque(lane_k);
         constexpr bool FIRST = decltype(Fc)::value;
         constexpr bool AUG = decltype(AUGc)::value;
         const bool fx = lane < NX, fu = lane >= NX && lane < 14;
@@ -725,7 +733,8 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
 
     // ------------------------------------------------------------ coupling of segment w < 3
     // matrix part: from P_b (slot w) and this wave's J | eta (Pa), Psi, Cg; scratch = the two windows
-    auto mcouple = [&]() {
+    auto mchain = [&]() {
+        const int lane = opaque(lane_k);
         const int g = lane >> 4, c = lane & 15;
         const ldsd* Pb = s.slot + 112 * w;
         ldsd* vv = s.vec;
@@ -734,6 +743,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) col[i] = lane < NX ? Pb[i * NX + lane] : (i == (lane & 7) ? 1.0 : 0.0);
         chol_cols(col, inv, lane);
+        SSTAMP(16);
         if (lane < NX) {
 #pragma unroll
             for (int i = 0; i < NX; ++i)
@@ -760,6 +770,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         S = mfma(Lt[0], T[0], S);
         S = mfma(Lt[1], T[1], S);
         S = mfma(Lt[2], T[2], S);
+        SSTAMP(17);
         // U = chol(S): S through the V area of the scratch
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -770,6 +781,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
 #pragma unroll
         for (int i = 0; i < NX; ++i) col[i] = lane < NX ? win[CP_V + i * NX + lane] : (i == (lane & 7) ? 1.0 : 0.0);
         chol_cols(col, inv, lane);
+        SSTAMP(18);
         if (lane < NX) {
 #pragma unroll
             for (int i = 0; i < NX; ++i)
@@ -789,6 +801,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
 #pragma unroll
             for (int i = j + 1; i < NX; ++i) y[i] = fma(-rdlane(col[i], j), y[j], y[i]);
         }
+        SSTAMP(19);
         // Psi (Phi^T) into the X area; beta into vec
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
@@ -835,11 +848,30 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
                 if (row < NX && c < NX) Pd[row * NX + c] = Pn[r];
             }
         }
-        // Lam = V X, M = Phi - C Lam  (rows to the coupling block for the x chain)
+        // [Phi | beta] for moff, in the second window (free during the coupling): rows 10..15 of the tile
+        // are 0 (row < NX) -- 16 x 16 slots
+#pragma unroll
+        for (int r = 0; r < 4; ++r) win[CP_PHI + (g + 4 * r) * 16 + c] = Ph[r];
+        SSTAMP(20);
+    };
+    // off the chain (runs while the next segment couples): Lam = V X, M = Phi - C Lam (rows to the
+    // coupling block for the x chain), C and the scratch to the coupling block
+    auto moff = [&]() {
+        const int lane = opaque(lane_k);
+        const int g = lane >> 4, c = lane & 15;
+        d4 cPh, cVTt, cX;  // [Phi | beta], V^T and X tiles from the scratch
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int row = g + 4 * r, rc = row < NX ? row : 0, cc = c < NX ? c : 0;
+            const bool in = row < NX && c < NX;
+            cPh[r] = win[CP_PHI + row * 16 + c];
+            cVTt[r] = in ? win[CP_V + cc * NX + rc] : 0.0;
+            cX[r] = in ? win[CP_X + rc * NX + cc] : 0.0;
+        }
         d4 Lm = {0.0, 0.0, 0.0, 0.0};
-        Lm = mfma(VTt[0], X[0], Lm);
-        Lm = mfma(VTt[1], X[1], Lm);
-        Lm = mfma(VTt[2], X[2], Lm);
+        Lm = mfma(cVTt[0], cX[0], Lm);
+        Lm = mfma(cVTt[1], cX[1], Lm);
+        Lm = mfma(cVTt[2], cX[2], Lm);
         d4 D = {0.0, 0.0, 0.0, 0.0};
         D = mfma(Cg[0], Lm[0], D);
         D = mfma(Cg[1], Lm[1], D);
@@ -848,19 +880,21 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         for (int r = 0; r < 4; ++r) {
             const int row = g + 4 * r;
             if (row < NX && c < NX) {
-                CP[CP_M + row * NX + c] = Ph[r] - D[r];
+                CP[CP_M + row * NX + c] = cPh[r] - D[r];
                 CP[CP_LM + row * NX + c] = Lm[r];
                 if (row >= c) win[CP_C + trl(row, c)] = Cg[r];
             }
+            if (row < NX && c == 14) CP[CP_B + row] = cPh[r];  // beta of [Phi | beta]
         }
         wave_sync();
         for (int e = lane; e < CP_SC; e += 64) CP[e] = win[e];
-        if (lane < NX) CP[CP_B + lane] = vv[V_B + lane];
+        SSTAMP(21);
     };
     // vector part: eta, beta (lanes 0..9), p_b (slot w) -> p_a (slot w - 1, if w > 0), lam0, m (lanes 0..9);
     // scratch holds L, U, V, X, C of this segment, vec the reciprocal diagonals
     double lam0 = 0.0, mvec = 0.0;
-    auto vcouple = [&](double eta, double beta) {
+    auto vchain = [&](double eta, double beta) {
+        const int lane = opaque(lane_k);
         const ldsd* pb = s.slot + 112 * w + 100;
         ldsd* vv = s.vec;
         if (lane < NX) vv[V_B + lane] = beta;
@@ -897,24 +931,31 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
             vv[V_L0 + lane] = l0;
             if (w > 0) s.slot[112 * (w - 1) + 100 + lane] = pa;
         }
+        lam0 = l0;
+    };
+    // off the chain: m = beta - C lam0 (needs C in the scratch: after moff)
+    auto voff = [&](double beta) {
+        const int lane = opaque(lane_k);
+        const int r = lane < NX ? lane : 0;
         wave_sync();
         double mm = beta;
 #pragma unroll
         for (int k = 0; k < NX; ++k) {
             const int lo = r < k ? r : k, hi = r < k ? k : r;
-            mm = fma(-win[CP_C + trl(hi, lo)], vv[V_L0 + k], mm);
+            mm = fma(-win[CP_C + trl(hi, lo)], s.vec[V_L0 + k], mm);
         }
-        lam0 = l0;
         mvec = mm;
     };
     // x chain step of segment w: x_b = M x_a + m (lanes 0..9), lam_b = Lam x_a + lam0 (lanes 16..25)
     auto xload = [&](double (&xrow)[NX]) {  // issued before the chain wait
+        const int lane = opaque(lane_k);
         const int r = lane & 15;
         const double* src = CP + ((lane >> 4) == 1 ? CP_LM : CP_M) + (r < NX ? r : 0) * NX;
 #pragma unroll
         for (int l = 0; l < NX; ++l) xrow[l] = src[l];
     };
     auto xstep = [&](const double (&xrow)[NX]) {
+        const int lane = opaque(lane_k);
         const int r = lane & 15, hi = lane >> 4;
         if (lane < NX) s.vec[V_M + lane] = mvec;
         if (lane < NX) s.vec[V_L0 + lane] = lam0;
@@ -1069,19 +1110,35 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
                 wave_sync();
             }
         }
+        // the chain hands P_a, p_a down segment by segment; each segment's off-chain part runs while the
+        // segment before it couples (wave 0's after the loop)
 #pragma unroll 1
         for (int st = NSEG - 2; st >= 0; --st) {
             wg_sync();
             if (w == st) {
                 SSTAMP(3);
 #ifndef SEGX_NO_COUPLE
-                mcouple();
+                mchain();
                 wave_sync();
-                vcouple(eta, beta);
+                vchain(eta, beta);
 #endif
                 SSTAMP(11);
             }
+#ifndef SEGX_NO_COUPLE
+            if (w == st + 1 && st + 1 < NSEG - 1) {
+                SSTAMP(3);
+                moff();
+                voff(beta);
+                SSTAMP(11);
+            }
+#endif
         }
+#ifndef SEGX_NO_COUPLE
+        if (w == 0) {
+            moff();
+            voff(beta);
+        }
+#endif
         SSTAMP(3);
 #ifndef SEGX_NO_FWD
         forward(IC<2>{});
@@ -1158,11 +1215,21 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
             if (w == st) {
                 SSTAMP(8);
 #ifndef SEGX_NO_COUPLE
-                vcouple(etac, betac);
+                vchain(etac, betac);
 #endif
                 SSTAMP(13);
             }
+#ifndef SEGX_NO_COUPLE
+            if (w == st + 1 && st + 1 < NSEG - 1) {
+                SSTAMP(8);
+                voff(betac);
+                SSTAMP(13);
+            }
+#endif
         }
+#ifndef SEGX_NO_COUPLE
+        if (w == 0) voff(betac);
+#endif
         SSTAMP(8);
 #ifndef SEGX_NO_FWD
         forward(IC<4>{});

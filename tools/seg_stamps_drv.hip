@@ -16,17 +16,17 @@ int main(int argc, char** argv) {
   for(int i=0;i<4;++i){q.lbu[i]=opt[i];q.ubu[i]=opt[4+i];} for(int i=0;i<3;++i){q.lh[i]=opt[8+i];q.uh[i]=opt[11+i];q.zl[i]=opt[14+i];q.Zl[i]=opt[17+i];}
   q.lm=opt[20]; q.tol=opt[21]; q.max_iter=100; q.cost_scaling=1; q.lm_scaling=1; q.ny=11;
   hipMalloc(&q.dx,8*B*(N+1)*10); hipMalloc(&q.du,8*B*N*4); hipMalloc(&q.status,4*B); hipMalloc(&q.iters,4*B); hipMalloc(&q.res,16*B);
-  hipMalloc(&q.work,8*B*qp_work_doubles(N)); hipMalloc(&q.stamps,8*B*64);
+  hipMalloc(&q.work,8*B*qp_work_doubles(N)); hipMalloc(&q.stamps,8*B*96);
   for (int r=0;r<3;++r) { launch_rti_qp_pack(q,0); launch_rti_qp_seg(q,0); }
   hipEvent_t a,b; hipEventCreate(&a); hipEventCreate(&b); launch_rti_qp_pack(q,0); hipEventRecord(a); launch_rti_qp_seg(q,0); hipEventRecord(b); hipEventSynchronize(b);
   float ms; hipEventElapsedTime(&ms,a,b);
-  std::vector<double> st(B*64); hipMemcpy(st.data(),q.stamps,8*B*64,hipMemcpyDeviceToHost);
+  std::vector<double> st(B*96); hipMemcpy(st.data(),q.stamps,8*B*96,hipMemcpyDeviceToHost);
   std::vector<int> it(B); hipMemcpy(it.data(),q.iters,4*B,hipMemcpyDeviceToHost);
   int mx=0; double mi=0; for(int i=0;i<B;++i){ if(it[i]>mx)mx=it[i]; mi+=it[i]; }
-  const char* ph[]={"setup+sweep0","terms0+park","factor sweep","f-couple wait","pred x-chain","rows pred","terms1+park","corr sweep","c-couple wait","corr x-chain","rows update","f-couple own","pred fwd sweep","c-couple own","corr fwd sweep","window waits"};
+  const char* ph[]={"setup+sweep0","terms0+park","factor sweep","f-couple wait","pred x-chain","rows pred","terms1+park","corr sweep","c-couple wait","corr x-chain","rows update","f-couple own","pred fwd sweep","c-couple own","corr fwd sweep","window waits","cpl chol(Pb)","cpl T,S","cpl chol(S)","cpl V","cpl X,Pa","cpl offchain","-","-"};
   printf("kernel %.3f ms, max iters %d, mean %.2f\n", ms, mx, mi/B);
-  for(int w=0;w<4;++w){ double tot[16]={0}, s=0; for(int i=0;i<B;++i) for(int j=0;j<16;++j) tot[j]+=st[(i*4+w)*16+j];
-    for(int j=0;j<16;++j) s+=tot[j];
+  for(int w=0;w<4;++w){ double tot[24]={0}, s=0; for(int i=0;i<B;++i) for(int j=0;j<24;++j) tot[j]+=st[(i*4+w)*24+j];
+    for(int j=0;j<24;++j) s+=tot[j];
     printf("wave %d: total %.0f cycles/instance, per iteration %.0f\n", w, s/B, s/mi);
-    for(int j=0;j<16;++j) printf("  %-14s %8.0f cycles/iter (%.1f%%)\n", ph[j], tot[j]/mi, 100*tot[j]/s); }
+    for(int j=0;j<22;++j) printf("  %-14s %8.0f cycles/iter (%.1f%%)\n", ph[j], tot[j]/mi, 100*tot[j]/s); }
   return 0; }
