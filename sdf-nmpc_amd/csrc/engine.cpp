@@ -85,6 +85,8 @@ struct sdfnmpc_ctx {
     // host-pointer path (sdf_eval_host, the CasADi external): pinned staging, its own hoist buffer and
     // the latents it was computed for (consecutive acados calls share one latent: the hoist is reused)
     float* h_pin = nullptr;
+    float* h_pin_dev = nullptr;  // the same pinned block as the device sees it (zero-copy row path)
+    bool row_zc = true;          // SDFNMPC_ROW_ZC=0: the row path stages through device buffers instead
     size_t h_pin_bytes = 0;
     DevBuf hin, hout, hc13;
     std::vector<float> h_lat;
@@ -171,6 +173,7 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
     }
     const char* lf = getenv("SDFNMPC_LIN_FIRST");
     c->lin_first = lf && *lf == '1';
+    if (const char* zc = getenv("SDFNMPC_ROW_ZC")) c->row_zc = *zc != '0';
     const char* sp = getenv("SDFNMPC_SERIAL_PREP");
     c->serial_prep = sp && *sp == '1';
     if (const char* qk = getenv("SDFNMPC_QP_KERNEL")) {
@@ -891,8 +894,10 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
         ctx->h_pin = nullptr;
         ctx->h_pin_bytes = 0;
-        HIPCHK(hipHostMalloc((void**)&ctx->h_pin, bytes, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc((void**)&ctx->h_pin, bytes, hipHostMallocMapped));
         ctx->h_pin_bytes = bytes;
+        ctx->h_pin_dev = nullptr;
+        if (hipHostGetDevicePointer((void**)&ctx->h_pin_dev, ctx->h_pin, 0) != hipSuccess) ctx->h_pin_dev = nullptr;
     }
     float* hp = ctx->h_pin;
     float* hl = hp + (size_t)rows * 4;
@@ -903,7 +908,19 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         for (int k = 0; k < L; ++k) hl[(size_t)r * L + k] = (float)in[(size_t)r * D + 3 + k];
     }
     const bool use_row = !net->wide && rows <= SDF_ROW_MAX;
-    if (use_row) {  // the latency path: one launch, no hoist (sdf_row.hip)
+    if (use_row && ctx->row_zc && ctx->h_pin_dev) {  // the latency path: one launch on the pinned block itself (zero-copy:
+        // the kernel reads the ~0.5 KB input over PCIe and writes its result straight into host memory,
+        // no staging copies), no hoist (sdf_row.hip)
+        float* dp = ctx->h_pin_dev;
+        SdfRowArgs ra = net->row;
+        ra.pos = (const float4*)dp;
+        ra.latent = dp + (size_t)rows * 4;
+        ra.out = (float4*)(dp + nin);
+        ra.grad_latent = grad ? dp + nin + (size_t)rows * 4 : nullptr;
+        ra.rows = rows;
+        HIPCHK(timed(ctx, "sdf_row", [&] { return launch_sdf_row(ra, ctx->stream); }));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    } else if (use_row) {  // pinned block not device-mapped: staging copies
         HIPCHK(ctx->hin.ensure(nin * sizeof(float)));
         HIPCHK(ctx->hout.ensure(nin * sizeof(float)));
         float* dpos = (float*)ctx->hin.p;

@@ -75,6 +75,14 @@ constexpr int CP_PHI = WIN;  // [Phi | beta] tile (16 x 16) from mchain to moff,
 static_assert(CP_B + 10 <= CPL && CP_SC <= WIN && CP_PHI + 256 <= 2 * WIN, "coupling block");
 
 __device__ __forceinline__ int trl(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower, j <= i
+// v[i] in the lanes with i == idx, as a chain of v_cndmask (a nested ?: of computed values compiles to a
+// divergent branch tree: exec save / restore per level)
+__device__ __forceinline__ double sel4(int i, double v0, double v1, double v2, double v3) {
+    double r = v3;
+    r = i == 2 ? v2 : r;
+    r = i == 1 ? v1 : r;
+    return i == 0 ? v0 : r;
+}
 
 // raw workgroup barrier: LDS operations drained, nothing else (global memory is wave-private here)
 __device__ __forceinline__ void wg_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
@@ -462,7 +470,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         const int og01 = fget(f, F_OG01);
         const double og0 = cw[og01], og1 = cw[og01 + 4], og2v = cw[fget(f, F_OG2)];
         const double bq0 = cw[fget(f, F_BQ0)], bq1 = cw[fget(f, F_BQ1)], bq2 = cw[fget(f, F_BQ2)];
-        const double hv0 = cw[fget(f, F_V0)] + (c == NX + g ? s.bd[k * NU + g] : 0.0) + (c == 14 ? s.bv[k * NU + g] : 0.0);
+        // box folds: unconditional LDS reads scaled by 0 / 1 lane masks (a conditional read is a divergent
+        // branch: exec save / restore around it, ten of them per stage before)
+        const double bdg = s.bd[k * NU + g], bvg = s.bv[k * NU + g];
+        const double hv0 = cw[fget(f, F_V0)] + (c == NX + g ? 1.0 : 0.0) * bdg + (c == 14 ? 1.0 : 0.0) * bvg;
         d4 W = {0.0, 0.0, 0.0, 0.0};
         W = mfma(Pa[0], og0, W);
         W = mfma(Pa[1], og1, W);
@@ -507,7 +518,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
             const double k2 = (-y2 - l32 * k3) * i2;
             const double k1 = (-y1 - l21 * k2 - l31 * k3) * i1;
             const double k0 = (-y0 - l10 * k1 - l20 * k2 - l30 * k3) * i0;
-            kg = g == 0 ? k0 : g == 1 ? k1 : g == 2 ? k2 : k3;
+            kg = sel4(g, k0, k1, k2, k3);
             __builtin_amdgcn_sched_barrier(0);
             if constexpr (AUG) {
                 const double z0 = __shfl(zt, c), z1 = __shfl(zt, 16 + c), z2 = __shfl(zt, 32 + c), z3 = __shfl(zt, 48 + c);
@@ -520,23 +531,31 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
                 const double g2 = (h2 - l32 * g3) * i2;
                 const double g1 = (h1 - l21 * g2 - l31 * g3) * i1;
                 const double g0 = (h0 - l10 * g1 - l20 * g2 - l30 * g3) * i0;
-                const double zsel = g == 0 ? h0 : g == 1 ? h1 : g == 2 ? h2 : h3;
-                const double gsel = g == 0 ? g0 : g == 1 ? g1 : g == 2 ? g2 : g3;
+                const double zsel = sel4(g, h0, h1, h2, h3);
+                const double gsel = sel4(g, g0, g1, g2, g3);
                 Cg = mfma(zsel, zsel, Cg);  // C += Zh Zh^T
                 FBST(zt, fget(f, F_SZ));
                 FBST(gsel, fget(f, F_SG));
                 FBST(kg, fget(f, F_SKP));
             }
             // chol(R^) packed into column 11 of rows 0..9: i0 l10 i1 l20 l21 i2 l30 l31 l32 i3
-            const double lv = lane == 0 ? i0 : lane == 1 ? l10 : lane == 2 ? i1 : lane == 3 ? l20 : lane == 4 ? l21
-                            : lane == 5 ? i2 : lane == 6 ? l30 : lane == 7 ? l31 : lane == 8 ? l32 : i3;
+            double lv = i3;  // selects, not a branch tree
+            lv = lane == 8 ? l32 : lv;
+            lv = lane == 7 ? l31 : lv;
+            lv = lane == 6 ? l30 : lv;
+            lv = lane == 5 ? i2 : lv;
+            lv = lane == 4 ? l21 : lv;
+            lv = lane == 3 ? l20 : lv;
+            lv = lane == 2 ? i1 : lv;
+            lv = lane == 1 ? l10 : lv;
+            lv = lane == 0 ? i0 : lv;
             FBST(lv, lane < NX ? 8 * (lane * FR + 11) : SJB);
             FBST(kg, fget(f, F_SK));
         }
         __builtin_amdgcn_sched_barrier(0);
         // ---- region 3: Joseph form [P | p] <- T^T H^ T + A~^T [P A~ | P b~ + p], T = [I 0; K k_ff; 0 1],
         // with [P A~ | P b~ + p] = [P A | P c + p] + (P B) [K | k_ff]
-        const double hua = cw[fget(f, F_HUU)] + ((c & 3) == g ? s.bd[k * NU + g] : 0.0);
+        const double hua = cw[fget(f, F_HUU)] + ((c & 3) == g ? 1.0 : 0.0) * bdg;
         const double V = mfma4(hua, kg, hv0);  // rows 10..13 of H^ T
         const int ab01 = fget(f, F_AB01);
         d4 Ab;
@@ -551,7 +570,9 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const int a_ = g + 4 * (2 + h);
-            if (a_ >= NX && a_ < 14) Hh[2 + h] += (c == a_ ? s.bd[k * NU + a_ - NX] : 0.0) + (c == 14 ? s.bv[k * NU + a_ - NX] : 0.0);
+            const bool in = a_ >= NX && a_ < 14;
+            const int bi = in ? a_ - NX : 0;
+            Hh[2 + h] += (in && c == a_ ? 1.0 : 0.0) * s.bd[k * NU + bi] + (in && c == 14 ? 1.0 : 0.0) * s.bv[k * NU + bi];
         }
         const double hxa = cw[fget(f, F_HXU)];
         Ab = mfma(bm, kg, Ab);                  // [A~ | b~] = [A | c] + B [K | k_ff]
@@ -660,7 +681,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
         // the previous stage's record row goes out now, ahead of this stage's refill; this one's waits
         if (cpend >= 0) bst(cfv, rsF, 8u * (lane < 14 ? lane * FR + 10 : S_J), (unsigned)cpend * (FRECS * 8u));
         refill();
-        cfv = fx ? bb : lane == NX ? k0 : lane == NX + 1 ? k1 : lane == NX + 2 ? k2 : k3;
+        cfv = fx ? bb : sel4(lane - NX, k0, k1, k2, k3);
         cpend = k;
         if constexpr (AUG) bacc += fx ? dz : 0.0;
     };
