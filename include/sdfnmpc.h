@@ -181,16 +181,20 @@ int sdfnmpc_ctx_use_null_stream(sdfnmpc_ctx* ctx);
 void* sdfnmpc_ctx_stream(sdfnmpc_ctx* ctx);
 int sdfnmpc_ctx_device(const sdfnmpc_ctx* ctx);
 int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx);
-/* the feedback-phase IPM kernel: SEGMENTED runs every instance on four wavefronts with a partitioned
- * (parallel-in-time) Riccati recursion (csrc/rti_qp_seg.hip); SERIAL on one wavefront (csrc/rti_qp.hip).
- * AUTO (default) = SERIAL; SEGMENTED applies where it supports the horizon (7 <= N <= 63).  The environment
- * variable SDFNMPC_QP_KERNEL=serial|segmented sets the default of new contexts. */
+/* the feedback-phase IPM kernel: SEGMENTED runs every instance on one workgroup of four wavefronts with a
+ * partitioned (parallel-in-time) Riccati recursion (csrc/rti_qp_seg.hip); SERIAL on one wavefront
+ * (csrc/rti_qp.hip).  AUTO (default) = SEGMENTED for batches of at most SDFNMPC_QP_SEG_AUTO_MAX_B
+ * instances where it supports the horizon (7 <= N <= 63; the latency regime, 7-10 % faster at N = 40),
+ * SERIAL above (the throughput regime).  Both solve the same QP to the same stop test; their iterates
+ * agree to rounding, not bitwise.  SDFNMPC_QP_KERNEL=serial|segmented sets the default of new contexts. */
 #define SDFNMPC_QP_AUTO 0
 #define SDFNMPC_QP_SERIAL 1
 #define SDFNMPC_QP_SEGMENTED 2
+#define SDFNMPC_QP_SEG_AUTO_MAX_B 256
 int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel);
-/* the kernel a QP of horizon N runs on this context (SDFNMPC_QP_SERIAL or _SEGMENTED; -1 on bad arguments) */
-int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N);
+/* the kernel a QP batch of B instances at horizon N runs on this context (SDFNMPC_QP_SERIAL or
+ * _SEGMENTED; -1 on bad arguments) */
+int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B);
 /* LDS bytes one instance of the serial QP kernel holds at horizon N (-1: N < 1) */
 long long sdfnmpc_qp_lds_bytes(int N);
 /* the occupancy gate of SURVEY.md §8(e): instances the context's device solves in one wave of QP

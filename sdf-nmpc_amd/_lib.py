@@ -122,7 +122,7 @@ def load():
         "sdfnmpc_ctx_synchronize": (i, [vp]),
         "sdfnmpc_ctx_set_tile_rows": (i, [vp, i]),
         "sdfnmpc_ctx_set_qp_kernel": (i, [vp, i]),
-        "sdfnmpc_ctx_qp_kernel": (i, [vp, i]),
+        "sdfnmpc_ctx_qp_kernel": (i, [vp, i, i]),
         "sdfnmpc_qp_lds_bytes": (C.c_longlong, [i]),
         "sdfnmpc_qp_capacity": (C.c_longlong, [vp, i]),
         "sdfnmpc_ctx_enable_timing": (i, [vp, i]),
@@ -222,11 +222,13 @@ class Context:
     QP_KERNELS = {"auto": 0, "serial": 1, "segmented": 2}
 
     def set_qp_kernel(self, kind: str):
-        """'auto' (segmented where it supports N), 'serial' or 'segmented' (include/sdfnmpc.h)."""
+        """'auto' (segmented for B <= 256 where it supports N, else serial), 'serial' or 'segmented'
+        (include/sdfnmpc.h)."""
         _check(load().sdfnmpc_ctx_set_qp_kernel(self.h, self.QP_KERNELS[kind]))
 
-    def qp_kernel(self, N: int) -> str:
-        k = load().sdfnmpc_ctx_qp_kernel(self.h, N)
+    def qp_kernel(self, N: int, B: int) -> str:
+        """The kernel a QP batch of B instances at horizon N runs ('serial' or 'segmented')."""
+        k = load().sdfnmpc_ctx_qp_kernel(self.h, N, B)
         return {1: "serial", 2: "segmented"}.get(k, "invalid")
 
     def qp_capacity(self, N: int) -> int:

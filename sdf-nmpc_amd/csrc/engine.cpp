@@ -85,8 +85,6 @@ struct sdfnmpc_ctx {
     // host-pointer path (sdf_eval_host, the CasADi external): pinned staging, its own hoist buffer and
     // the latents it was computed for (consecutive acados calls share one latent: the hoist is reused)
     float* h_pin = nullptr;
-    float* h_pin_dev = nullptr;  // the same pinned block as the device sees it (zero-copy row path)
-    bool row_zc = true;          // SDFNMPC_ROW_ZC=0: the row path stages through device buffers instead
     size_t h_pin_bytes = 0;
     DevBuf hin, hout, hc13;
     std::vector<float> h_lat;
@@ -173,7 +171,6 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
     }
     const char* lf = getenv("SDFNMPC_LIN_FIRST");
     c->lin_first = lf && *lf == '1';
-    if (const char* zc = getenv("SDFNMPC_ROW_ZC")) c->row_zc = *zc != '0';
     const char* sp = getenv("SDFNMPC_SERIAL_PREP");
     c->serial_prep = sp && *sp == '1';
     if (const char* qk = getenv("SDFNMPC_QP_KERNEL")) {
@@ -280,10 +277,15 @@ extern "C" int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel) {
     return SDFNMPC_OK;
 }
 
-extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N) {
-    if (!ctx || N < 1) return -1;
-    if (ctx->qp_kernel != SDFNMPC_QP_SEGMENTED) return SDFNMPC_QP_SERIAL;  // AUTO: serial until the segmented is faster
-    return rti_qp_seg_supported(N) ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
+// AUTO: the segmented kernel for latency-sized batches (B <= SDFNMPC_QP_SEG_AUTO_MAX_B, one workgroup
+// of four wavefronts per instance: 7-10 % lower latency than the serial kernel at B <= 256, N = 40), the
+// serial one above (one wavefront per instance: at B = 1024 the serial kernel fills every SIMD once and
+// is 1.6x faster than four wavefronts per instance)
+extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B) {
+    if (!ctx || N < 1 || B < 0) return -1;
+    if (ctx->qp_kernel == SDFNMPC_QP_SERIAL || !rti_qp_seg_supported(N)) return SDFNMPC_QP_SERIAL;
+    if (ctx->qp_kernel == SDFNMPC_QP_SEGMENTED) return SDFNMPC_QP_SEGMENTED;
+    return B <= SDFNMPC_QP_SEG_AUTO_MAX_B ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
 }
 
 extern "C" long long sdfnmpc_qp_lds_bytes(int N) {
@@ -296,7 +298,8 @@ extern "C" long long sdfnmpc_qp_lds_bytes(int N) {
 extern "C" long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N) {
     if (!ctx || N < 1) return -1;
     if (ctx->n_cu <= 0 || ctx->lds_per_cu == 0) return -1;
-    const size_t per = sdfnmpc_ctx_qp_kernel(ctx, N) == SDFNMPC_QP_SEGMENTED ? qp_seg_lds_bytes(N) : qp_lds_bytes(N);
+    // a batch that fills the device: the kernel AUTO picks above SDFNMPC_QP_SEG_AUTO_MAX_B
+    const size_t per = sdfnmpc_ctx_qp_kernel(ctx, N, 1 << 30) == SDFNMPC_QP_SEGMENTED ? qp_seg_lds_bytes(N) : qp_lds_bytes(N);
     if (per == 0 || per > ctx->lds_per_cu) return 0;  // the horizon does not fit one CU's LDS
     return (long long)ctx->n_cu * (long long)(ctx->lds_per_cu / per);
 }
@@ -894,10 +897,8 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         if (ctx->h_pin) (void)hipHostFree(ctx->h_pin);
         ctx->h_pin = nullptr;
         ctx->h_pin_bytes = 0;
-        HIPCHK(hipHostMalloc((void**)&ctx->h_pin, bytes, hipHostMallocMapped));
+        HIPCHK(hipHostMalloc((void**)&ctx->h_pin, bytes, hipHostMallocDefault));
         ctx->h_pin_bytes = bytes;
-        ctx->h_pin_dev = nullptr;
-        if (hipHostGetDevicePointer((void**)&ctx->h_pin_dev, ctx->h_pin, 0) != hipSuccess) ctx->h_pin_dev = nullptr;
     }
     float* hp = ctx->h_pin;
     float* hl = hp + (size_t)rows * 4;
@@ -908,19 +909,9 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         for (int k = 0; k < L; ++k) hl[(size_t)r * L + k] = (float)in[(size_t)r * D + 3 + k];
     }
     const bool use_row = !net->wide && rows <= SDF_ROW_MAX;
-    if (use_row && ctx->row_zc && ctx->h_pin_dev) {  // the latency path: one launch on the pinned block itself (zero-copy:
-        // the kernel reads the ~0.5 KB input over PCIe and writes its result straight into host memory,
-        // no staging copies), no hoist (sdf_row.hip)
-        float* dp = ctx->h_pin_dev;
-        SdfRowArgs ra = net->row;
-        ra.pos = (const float4*)dp;
-        ra.latent = dp + (size_t)rows * 4;
-        ra.out = (float4*)(dp + nin);
-        ra.grad_latent = grad ? dp + nin + (size_t)rows * 4 : nullptr;
-        ra.rows = rows;
-        HIPCHK(timed(ctx, "sdf_row", [&] { return launch_sdf_row(ra, ctx->stream); }));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-    } else if (use_row) {  // pinned block not device-mapped: staging copies
+    if (use_row) {  // the latency path: one launch, no hoist (sdf_row.hip).  Zero-copy (the kernel reading
+        // and writing the pinned block over PCIe) was measured equal in wall time: the PCIe reads add
+        // ~2 us to the kernel, as much as the two staging copies cost.
         HIPCHK(ctx->hin.ensure(nin * sizeof(float)));
         HIPCHK(ctx->hout.ensure(nin * sizeof(float)));
         float* dpos = (float*)ctx->hin.p;
@@ -1131,7 +1122,7 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
 // the IPM kernel of this context and horizon: the segmented one (four wavefronts per instance,
 // rti_qp_seg.hip) where it supports N, unless the context asks for the serial one (rti_qp.hip)
 static hipError_t qp_launch(sdfnmpc_ctx* ctx, const QpArgs& q) {
-    if (sdfnmpc_ctx_qp_kernel(ctx, q.N) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
+    if (sdfnmpc_ctx_qp_kernel(ctx, q.N, q.B) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
     return launch_rti_qp(q, ctx->stream);
 }
 

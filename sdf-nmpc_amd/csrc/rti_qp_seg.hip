@@ -104,13 +104,12 @@ __device__ __forceinline__ void chol_cols(double (&col)[NX], double (&inv)[NX], 
         const double d = rdlane(col[j], j);
         const double iv = rsqrt_nr(d);
         inv[j] = iv;
-        const double lcj = col[j] * iv;  // L[c][j] (A symmetric: A[j][c] = A[c][j])
+        // A[i][c] -= L[i][j] L[c][j] = A[i][j] A[c][j] / d  (A symmetric: A[j][c] = A[c][j])
+        const double tcj = col[j] * (iv * iv);
 #pragma unroll
-        for (int i = j + 1; i < NX; ++i) {
-            const double lij = rdlane(col[i], j) * iv;
-            col[i] = lane > j ? fma(-lij, lcj, col[i]) : col[i];
-        }
-        // column j itself: L[i][j] = A[i][j] / L[j][j] for i >= j
+        for (int i = j + 1; i < NX; ++i) col[i] = lane > j ? fma(-rdlane(col[i], j), tcj, col[i]) : col[i];
+        // column j itself: L[i][j] = A[i][j] / L[j][j] for i >= j (a branch: as selects, 20 v_cndmask per
+        // column made the factorisation 20 % slower)
         if (lane == j) {
 #pragma unroll
             for (int i = 0; i < NX; ++i) col[i] = i < j ? 0.0 : col[i] * iv;
@@ -1357,8 +1356,10 @@ static size_t seg_lds_bytes(int P, int NMAX) {
     }
     (void)NMAX;
 }
-// segments per instance for horizon N (0: unsupported): three where they fit (168 registers per wave at
-// four instances per CU), else four.  SDFNMPC_QP_NSEG = 2, 3, 4 overrides (diagnostic).
+// segments per instance for horizon N (0: unsupported): four where they fit, else three, else two (the
+// kernel serves latency-sized batches -- one workgroup per CU -- where more segments mean a shorter
+// chain: B = 1 at N = 40 takes 0.583 ms with four, 0.599 ms with three).  SDFNMPC_QP_NSEG = 2, 3, 4
+// overrides (diagnostic).
 int rti_qp_seg_count(int N) {
     auto fits = [&](int P) {
         for (const SegCfg& c : SEG_CFGS)
@@ -1369,7 +1370,7 @@ int rti_qp_seg_count(int N) {
         const int P = atoi(e);
         return fits(P) ? P : 0;
     }
-    return fits(3) ? 3 : fits(4) ? 4 : 0;
+    return fits(4) ? 4 : fits(3) ? 3 : fits(2) ? 2 : 0;
 }
 
 bool rti_qp_seg_supported(int N) { return rti_qp_seg_count(N) > 0; }

@@ -95,7 +95,7 @@ def test_qp_exact_solution_64_c3_instances(gpu_ctx, oracle_lib, kernel):
     torch.cuda.synchronize()
     gpu_ctx.set_qp_kernel(kernel)
     try:
-        assert gpu_ctx.qp_kernel(N) == kernel
+        assert gpu_ctx.qp_kernel(N, B) == kernel
         _lib.qp_solve(gpu_ctx, _lib.qp_opts(model, tol=QP_TOL), B, N, t)
         gpu_ctx.synchronize()
     finally:

@@ -49,7 +49,7 @@ for B, N, seed in cases:
               WN=prob["WN"][:nb])
     cs = {mi: O.qp_ipm_batch(sub, pr, x0[:nb], model, nthreads=8, max_iter=mi, start=dict(seg=4)) for mi in (1, 100)}
     c1 = {mi: O.qp_ipm_batch(sub, pr, x0[:nb], model, nthreads=8, max_iter=mi) for mi in (1, 100)}
-    print(f"--- B={B} N={N} seed={seed}  kernel for N: {ctx.qp_kernel(N)}")
+    print(f"--- B={B} N={N} seed={seed}  auto kernel: {ctx.qp_kernel(N, B)}")
     for kind in ("serial", "segmented"):
         o = out[kind, 100]
         print(f"  {kind:10s} status {np.bincount(o['status'], minlength=3)} iters max {o['iters'].max()} mean {o['iters'].mean():.2f}")
