@@ -184,13 +184,14 @@ int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx);
 /* the feedback-phase IPM kernel: SEGMENTED runs every instance on one workgroup of four wavefronts with a
  * partitioned (parallel-in-time) Riccati recursion (csrc/rti_qp_seg.hip); SERIAL on one wavefront
  * (csrc/rti_qp.hip).  AUTO (default) = SEGMENTED for batches of at most SDFNMPC_QP_SEG_AUTO_MAX_B
- * instances where it supports the horizon (7 <= N <= 63; the latency regime, 7-10 % faster at N = 40),
- * SERIAL above (the throughput regime).  Both solve the same QP to the same stop test; their iterates
+ * instances at horizons SDFNMPC_QP_SEG_AUTO_MIN_N <= N <= 63 (the latency regime: 8-10 % faster at
+ * N = 40, 24 % at N = 60), SERIAL otherwise (large batches: the throughput regime; short horizons).  Both solve the same QP to the same stop test; their iterates
  * agree to rounding, not bitwise.  SDFNMPC_QP_KERNEL=serial|segmented sets the default of new contexts. */
 #define SDFNMPC_QP_AUTO 0
 #define SDFNMPC_QP_SERIAL 1
 #define SDFNMPC_QP_SEGMENTED 2
 #define SDFNMPC_QP_SEG_AUTO_MAX_B 256
+#define SDFNMPC_QP_SEG_AUTO_MIN_N 36
 int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel);
 /* the kernel a QP batch of B instances at horizon N runs on this context (SDFNMPC_QP_SERIAL or
  * _SEGMENTED; -1 on bad arguments) */

@@ -222,7 +222,7 @@ class Context:
     QP_KERNELS = {"auto": 0, "serial": 1, "segmented": 2}
 
     def set_qp_kernel(self, kind: str):
-        """'auto' (segmented for B <= 256 where it supports N, else serial), 'serial' or 'segmented'
+        """'auto' (segmented for B <= 256 at 36 <= N <= 63, else serial), 'serial' or 'segmented'
         (include/sdfnmpc.h)."""
         _check(load().sdfnmpc_ctx_set_qp_kernel(self.h, self.QP_KERNELS[kind]))
 

@@ -277,15 +277,16 @@ extern "C" int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel) {
     return SDFNMPC_OK;
 }
 
-// AUTO: the segmented kernel for latency-sized batches (B <= SDFNMPC_QP_SEG_AUTO_MAX_B, one workgroup
-// of four wavefronts per instance: 7-10 % lower latency than the serial kernel at B <= 256, N = 40), the
-// serial one above (one wavefront per instance: at B = 1024 the serial kernel fills every SIMD once and
-// is 1.6x faster than four wavefronts per instance)
+// AUTO: the segmented kernel for latency-sized batches of long horizons (B <= SDFNMPC_QP_SEG_AUTO_MAX_B,
+// N >= SDFNMPC_QP_SEG_AUTO_MIN_N; one workgroup of four wavefronts per instance: 8-10 % lower latency than
+// the serial kernel at N = 40, 24 % at N = 60, equal at N = 30, 30 % slower at N = 20 where the three
+// couplings outweigh five-node segments), the serial one otherwise (one wavefront per instance: at
+// B = 1024 it fills every SIMD once and is 1.6x faster than four wavefronts per instance)
 extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B) {
     if (!ctx || N < 1 || B < 0) return -1;
     if (ctx->qp_kernel == SDFNMPC_QP_SERIAL || !rti_qp_seg_supported(N)) return SDFNMPC_QP_SERIAL;
     if (ctx->qp_kernel == SDFNMPC_QP_SEGMENTED) return SDFNMPC_QP_SEGMENTED;
-    return B <= SDFNMPC_QP_SEG_AUTO_MAX_B ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
+    return (B <= SDFNMPC_QP_SEG_AUTO_MAX_B && N >= SDFNMPC_QP_SEG_AUTO_MIN_N) ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
 }
 
 extern "C" long long sdfnmpc_qp_lds_bytes(int N) {

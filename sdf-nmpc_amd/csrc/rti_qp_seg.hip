@@ -1358,7 +1358,7 @@ static size_t seg_lds_bytes(int P, int NMAX) {
 }
 // segments per instance for horizon N (0: unsupported): four where they fit, else three, else two (the
 // kernel serves latency-sized batches -- one workgroup per CU -- where more segments mean a shorter
-// chain: B = 1 at N = 40 takes 0.583 ms with four, 0.599 ms with three).  SDFNMPC_QP_NSEG = 2, 3, 4
+// chain: B = 1 at N = 40 takes 0.583 ms with four, 0.599 ms with three; at N = 60 only four fit).  SDFNMPC_QP_NSEG = 2, 3, 4
 // overrides (diagnostic).
 int rti_qp_seg_count(int N) {
     auto fits = [&](int P) {
