@@ -184,8 +184,9 @@ int sdfnmpc_ctx_synchronize(sdfnmpc_ctx* ctx);
 /* the feedback-phase IPM kernel: SEGMENTED runs every instance on one workgroup of four wavefronts with a
  * partitioned (parallel-in-time) Riccati recursion (csrc/rti_qp_seg.hip); SERIAL on one wavefront
  * (csrc/rti_qp.hip).  AUTO (default) = SEGMENTED for batches of at most SDFNMPC_QP_SEG_AUTO_MAX_B
- * instances at horizons SDFNMPC_QP_SEG_AUTO_MIN_N <= N <= 63 (the latency regime: 8-10 % faster at
- * N = 40, 24 % at N = 60), SERIAL otherwise (large batches: the throughput regime; short horizons).  Both solve the same QP to the same stop test; their iterates
+ * instances (twice that from N = 48) at horizons SDFNMPC_QP_SEG_AUTO_MIN_N <= N <= 63 (8-10 % faster
+ * at N = 40, 21-24 % at N = 60 up to B = 512), SERIAL otherwise (large batches at N < 48: one wavefront
+ * per SIMD is the throughput regime; short horizons, where the couplings outweigh the segments).  Both solve the same QP to the same stop test; their iterates
  * agree to rounding, not bitwise.  SDFNMPC_QP_KERNEL=serial|segmented sets the default of new contexts. */
 #define SDFNMPC_QP_AUTO 0
 #define SDFNMPC_QP_SERIAL 1

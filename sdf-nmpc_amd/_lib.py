@@ -222,8 +222,8 @@ class Context:
     QP_KERNELS = {"auto": 0, "serial": 1, "segmented": 2}
 
     def set_qp_kernel(self, kind: str):
-        """'auto' (segmented for B <= 256 at 36 <= N <= 63, else serial), 'serial' or 'segmented'
-        (include/sdfnmpc.h)."""
+        """'auto' (segmented for B <= 256 -- 512 from N = 48 -- at 36 <= N <= 63, else serial), 'serial' or
+        'segmented' (include/sdfnmpc.h)."""
         _check(load().sdfnmpc_ctx_set_qp_kernel(self.h, self.QP_KERNELS[kind]))
 
     def qp_kernel(self, N: int, B: int) -> str:

@@ -286,7 +286,11 @@ extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B) {
     if (!ctx || N < 1 || B < 0) return -1;
     if (ctx->qp_kernel == SDFNMPC_QP_SERIAL || !rti_qp_seg_supported(N)) return SDFNMPC_QP_SERIAL;
     if (ctx->qp_kernel == SDFNMPC_QP_SEGMENTED) return SDFNMPC_QP_SEGMENTED;
-    return (B <= SDFNMPC_QP_SEG_AUTO_MAX_B && N >= SDFNMPC_QP_SEG_AUTO_MIN_N) ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
+    // the batch bound doubles from N = 48: the serial kernel then holds two instances per CU instead of
+    // four (its LDS), and the segmented one still runs two per CU (measured at N = 60: 2.10 vs 2.67 ms at
+    // B = 512; at N = 40, 1.13 vs 1.08 ms at B = 512)
+    const int max_b = N >= 48 ? 2 * SDFNMPC_QP_SEG_AUTO_MAX_B : SDFNMPC_QP_SEG_AUTO_MAX_B;
+    return (B <= max_b && N >= SDFNMPC_QP_SEG_AUTO_MIN_N) ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
 }
 
 extern "C" long long sdfnmpc_qp_lds_bytes(int N) {

@@ -222,7 +222,10 @@ static_assert(F_NFIELD <= 26 && 8 * FRECS < 65536, "packed lane constants");
 #endif
 
 template <int NSEG, int NMAX>
-__global__ __launch_bounds__(64 * NSEG, NSEG) void rti_qp_seg_kernel(QpArgs A) {
+// occupancy targets: three or two (P = 2, 3) workgroups per CU; P = 4 at two (256 registers per lane: no
+// spill at 223 VGPRs; the 128-register target of four per CU spilled, and without a target the compiler
+// took 265 registers -- one workgroup per CU, half the instances of a B = 512 batch per round)
+__global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_kernel(QpArgs A) {
     __shared__ __align__(16) double lds_q[SegLds<NSEG, NMAX>::TOTAL];
     SSTAMP_DECL
     const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63;

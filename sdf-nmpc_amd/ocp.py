@@ -148,9 +148,14 @@ class Ocp:
             self.plan = shard.plan(B, c0.qp_capacity(N), len(devs))
         else:
             c0, self.plan = ctx, [(0, 0, B)]
+        # one QP kernel for the whole batch (AUTO picks by batch size: include/sdfnmpc.h), so the split over
+        # devices never changes a result -- every part runs what one part of B instances would
+        qp_kind = c0.qp_kernel(N, B) if len(self.plan) > 1 else None
         self.parts = []
         for slot, lo, hi in self.plan:
             c = c0 if slot == 0 else _lib.Context(devs[slot])
+            if qp_kind is not None:
+                c.set_qp_kernel(qp_kind)
             n = net if (net is not None and slot == 0) else load_net(c, cfg, weights)
             s = _lib.Solver(c, n, self.cmodel, self.qp_opts, hi - lo, N, model.np, model.ny, self.dt)
             self.parts.append(_Part(lo, hi, c, n, s, ctx is None, n is not net))
