@@ -480,6 +480,20 @@ def bench_c2(device, N, W, no_cpu, rtis=30):
     per_rti = float(np.median(ts))
     res = {"us_per_node": per_rti / (N + 1) * 1e6, "ms_per_rti": per_rti * 1e3, "nodes_per_rti": N + 1,
            "calls": "sdf_l4c + jac_sdf_l4c per node (ctypes, fp64 in/out, value and 1x131 Jacobian)"}
+    # the same calls from C (tools/c2_driver.c, a child process): acados's own call path, no Python per call
+    drv = os.path.join(ROOT, "tools", "_c2_driver")
+    if os.path.exists(drv):
+        import subprocess
+        with tempfile.NamedTemporaryFile(suffix=".sdfw", delete=False) as f:
+            f.write(W.pack(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed=0)))
+            wpath2 = f.name
+        try:
+            r = subprocess.run([drv, _lib.l4c_path(), wpath2, str(device), str(N + 1), str(rtis)],
+                               capture_output=True, text=True, timeout=120)
+            if r.returncode == 0:
+                res["c_driver"] = json.loads(r.stdout.strip().splitlines()[-1])
+        finally:
+            os.unlink(wpath2)
     if not no_cpu:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle as O

@@ -888,6 +888,10 @@ extern "C" int sdfnmpc_sdf_eval(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long l
                    grad_latent, grad_latent ? 32 : ctx->tile_rows);
 }
 
+// the host-pointer path's wait for its results (polling hipStreamQuery instead measured 3 us slower per
+// call; tools/launch_lat.hip: a bare launch + hipStreamSynchronize is 11 us on the box)
+static hipError_t host_wait(sdfnmpc_ctx* ctx) { return hipStreamSynchronize(ctx->stream); }
+
 extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const double* in,
                                      double* df, double* grad) {
     if (!ctx || !net || rows < 0 || (rows > 0 && (!in || !df))) return fail(SDFNMPC_E_ARG, "bad sdf_eval_host arguments");
@@ -931,7 +935,7 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         HIPCHK(timed(ctx, "sdf_row", [&] { return launch_sdf_row(ra, ctx->stream); }));
         HIPCHK(hipMemcpyAsync(ho, dout, (grad ? nin : (size_t)rows * 4) * sizeof(float), hipMemcpyDeviceToHost,
                               ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(host_wait(ctx));
     } else {
         HIPCHK(ctx->hin.ensure(nin * sizeof(float)));
         HIPCHK(ctx->hout.ensure(nin * sizeof(float)));
@@ -965,7 +969,7 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         }
         HIPCHK(hipMemcpyAsync(ho, dout, (grad ? nin : (size_t)rows * 4) * sizeof(float), hipMemcpyDeviceToHost,
                               ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
+        HIPCHK(host_wait(ctx));
     }
     const float* go = ho + (size_t)rows * 4;
     for (int r = 0; r < rows; ++r) {
