@@ -32,70 +32,82 @@ __device__ __forceinline__ float wave_sum(float v) {
     return v;
 }
 
-// out[j] = bias[j] + W[j][:K] . in  for j < J, from the transposed copy WT [K][J] (column j of WT is
-// row j of W): thread t owns output j = t % J over the K-slice t / J, so every weight load is one
-// coalesced 256-B wave access and no cross-lane reduction is needed; the S = 512 / J partial sums of
-// an output meet in LDS (`part`)
+// A layer at one row is a GEMV over ~0.25 MB of L2/MALL-resident weights: its time is the memory
+// latency unless every load of the layer is in flight at once.  Both directions therefore give each
+// thread one float4 column quad and a slice of the reduction dimension, issue the slice's loads
+// back to back into registers (up to 32 float4 = 128 VGPRs), then reduce; the slices' partial sums
+// meet in LDS (`part`).  Addresses are clamped and the padding multiplied by 0 (no divergent branch).
+
+// out[j] = bias[j] + W[j][:K] . in  for j < J, from the transposed copy WT [K][J] (row k of WT: the
+// k-th input's weights of every output, 16-byte aligned): thread t owns outputs 4q..4q+3, q = t % (J/4),
+// over the K-slice t / (J/4)
 template <int J, int K>
 __device__ __forceinline__ void fwd(const float* __restrict__ WT, const float* __restrict__ bias, const float* in,
                                     float* part, float* out) {
-    constexpr int S = 64 * RW / J, KS = (K + S - 1) / S;
-    static_assert(S >= 1 && S * J == 64 * RW, "J must divide the workgroup");
-    const int t = threadIdx.x, j = t % J, s = t / J;
-    const int k0 = s * KS, k1 = (k0 + KS < K) ? k0 + KS : K;
-    float a0 = 0.0f, a1 = 0.0f;
-    int k = k0;
-#pragma unroll 8
-    for (; k + 1 < k1; k += 2) {
-        a0 = fmaf(WT[(size_t)k * J + j], in[k], a0);
-        a1 = fmaf(WT[(size_t)(k + 1) * J + j], in[k + 1], a1);
+    constexpr int Q = J / 4, S = 64 * RW / Q, KS = (K + S - 1) / S;
+    static_assert(J % 4 == 0 && S >= 1 && S * Q == 64 * RW, "J / 4 must divide the workgroup");
+    const int t = threadIdx.x, q = t % Q, s = t / Q, k0 = s * KS;
+    const float4* W4 = (const float4*)WT;
+    float4 w[KS];
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+        const int k = k0 + i < K ? k0 + i : K - 1;
+        w[i] = W4[(size_t)k * Q + q];
     }
-    if (k < k1) a0 = fmaf(WT[(size_t)k * J + j], in[k], a0);
-    part[s * J + j] = a0 + a1;
+    float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+#pragma unroll
+    for (int i = 0; i < KS; ++i) {
+        const int k = k0 + i;
+        const float x = (k < K ? 1.0f : 0.0f) * in[k < K ? k : 0];
+        a.x = fmaf(w[i].x, x, a.x);
+        a.y = fmaf(w[i].y, x, a.y);
+        a.z = fmaf(w[i].z, x, a.z);
+        a.w = fmaf(w[i].w, x, a.w);
+    }
+    *(float4*)(part + s * J + 4 * q) = a;
     __syncthreads();
     if (t < J) {
         float v = 0.0f;
 #pragma unroll
-        for (int q = 0; q < S; ++q) v += part[q * J + t];
+        for (int r = 0; r < S; ++r) v += part[r * J + t];
         out[t] = v + bias[t];
     }
 }
 
-// out[k] = sum_j W[j][k] d[j]  for k < K (W row-major [J][K4], rows padded to K4 = 4 ceil(K / 4)); waves
-// own rows j (4 at a time), lanes own columns k and accumulate over j; partial sums reduced over the
-// waves through `part` [RW][K]
+// out[k] = sum_j W[j][k] d[j]  for k < K (W row-major [J][K4], rows padded to K4 = 4 ceil(K / 4)):
+// thread t owns columns 4q..4q+3, q = t % (K4/4), over the row slice t / (K4/4) (threads past the last
+// whole slice idle)
 template <int J, int K>
-__device__ __forceinline__ void bwd(const float* __restrict__ W, const float* d, float* part, float* out, int wave,
-                                    int lane) {
-    constexpr int T = (K + 63) / 64, K4 = (K + 3) / 4 * 4;
-    float acc[T];
+__device__ __forceinline__ void bwd(const float* __restrict__ W, const float* d, float* part, float* out) {
+    constexpr int K4 = (K + 3) / 4 * 4, Q = K4 / 4, S = 64 * RW / Q, JS = (J + S - 1) / S;
+    static_assert(S >= 1, "K too wide for the workgroup");
+    const int t = threadIdx.x, q = t % Q, s = t / Q, j0 = s * JS;
+    const bool act = s < S;
+    const float4* W4 = (const float4*)W;
+    float4 w[JS];
 #pragma unroll
-    for (int t = 0; t < T; ++t) acc[t] = 0.0f;
-    for (int j0 = 4 * wave; j0 < J; j0 += 4 * RW) {
-        float w[4][T], dj[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-            dj[r] = (j0 + r < J) ? d[j0 + r] : 0.0f;
-#pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const int k = lane + 64 * t;
-                w[r][t] = (j0 + r < J && k < K) ? W[(size_t)(j0 + r) * K4 + k] : 0.0f;
-            }
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r)
-#pragma unroll
-            for (int t = 0; t < T; ++t) acc[t] = fmaf(w[r][t], dj[r], acc[t]);
+    for (int i = 0; i < JS; ++i) {
+        const int j = (act && j0 + i < J) ? j0 + i : 0;
+        w[i] = W4[(size_t)j * Q + q];
     }
+    float4 a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
-    for (int t = 0; t < T; ++t)
-        if (lane + 64 * t < K) part[wave * K + lane + 64 * t] = acc[t];
+    for (int i = 0; i < JS; ++i) {
+        const int j = j0 + i;
+        const bool in = act && j < J;
+        const float x = (in ? 1.0f : 0.0f) * d[in ? j : 0];
+        a.x = fmaf(w[i].x, x, a.x);
+        a.y = fmaf(w[i].y, x, a.y);
+        a.z = fmaf(w[i].z, x, a.z);
+        a.w = fmaf(w[i].w, x, a.w);
+    }
+    if (act) *(float4*)(part + s * K4 + 4 * q) = a;
     __syncthreads();
-    for (int k = threadIdx.x; k < K; k += 64 * RW) {
-        float s = 0.0f;
+    for (int k = t; k < K; k += 64 * RW) {
+        float v = 0.0f;
 #pragma unroll
-        for (int w = 0; w < RW; ++w) s += part[w * K + k];
-        out[k] = s;
+        for (int r = 0; r < S; ++r) v += part[r * K4 + k];
+        out[k] = v;
     }
     __syncthreads();
 }
@@ -190,16 +202,16 @@ __global__ __launch_bounds__(64 * RW) void sdf_row_kernel(SdfRowArgs A) {
     // ---- backward: delta_a = (delta_h * cos(w0 a)) * w0 (torch SinBackward then MulBackward)
     for (int j = threadIdx.x; j < N4; j += 64 * RW) a4[j] = (A.w5[j] * c4[j]) * w0;
     __syncthreads();
-    bwd<N4, N3>(A.W4, a4, part, h3, wave, lane);             // d h3
+    bwd<N4, N3>(A.W4, a4, part, h3);             // d h3
     for (int j = threadIdx.x; j < N3; j += 64 * RW) a3[j] = (h3[j] * c3[j]) * w0;
     __syncthreads();
-    bwd<N3, C3>(A.W3, a3, part, g3, wave, lane);             // [d h2 | d e | d z]
+    bwd<N3, C3>(A.W3, a3, part, g3);             // [d h2 | d e | d z]
     for (int j = threadIdx.x; j < N2; j += 64 * RW) a2[j] = (g3[j] * c2[j]) * w0;
     __syncthreads();
-    bwd<N2, N1>(A.W2, a2, part, a1, wave, lane);             // d h1
+    bwd<N2, N1>(A.W2, a2, part, a1);             // d h1
     for (int j = threadIdx.x; j < N1; j += 64 * RW) a1[j] = (a1[j] * c1[j]) * w0;
     __syncthreads();
-    bwd<N1, C1>(A.W1, a1, part, g1, wave, lane);             // [d e | d z]
+    bwd<N1, C1>(A.W1, a1, part, g1);             // [d e | d z]
     // ---- outputs: df, d df / d pos (through the embedding), d df / d latent
     if (A.grad_latent)
         for (int k = threadIdx.x; k < L; k += 64 * RW) A.grad_latent[(size_t)r * L + k] = g3[N2 + E + k] + g1[E + k];
