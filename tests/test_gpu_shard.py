@@ -101,6 +101,25 @@ def test_qp_capacity_from_the_library():
         ctx.qp_capacity(0)
 
 
+def test_qp_kernel_auto_policy():
+    """AUTO (include/sdfnmpc.h): segmented at 36 <= N <= 63 for B <= 256 (512 from N = 48), serial
+    otherwise; an explicit choice overrides it; the capacity uses the kernel of a full batch."""
+    from sdf_nmpc_amd import _lib
+    ctx = _lib.Context(0)
+    assert ctx.qp_kernel(40, 1) == "segmented" and ctx.qp_kernel(40, 256) == "segmented"
+    assert ctx.qp_kernel(40, 257) == "serial" and ctx.qp_kernel(40, 1024) == "serial"
+    assert ctx.qp_kernel(60, 512) == "segmented" and ctx.qp_kernel(60, 513) == "serial"
+    assert ctx.qp_kernel(20, 1) == "serial" and ctx.qp_kernel(35, 1) == "serial" and ctx.qp_kernel(36, 1) == "segmented"
+    assert ctx.qp_kernel(64, 1) == "serial"  # beyond the segmented kernel's horizon
+    ctx.set_qp_kernel("serial")
+    assert ctx.qp_kernel(40, 1) == "serial"
+    ctx.set_qp_kernel("segmented")
+    assert ctx.qp_kernel(40, 1024) == "segmented" and ctx.qp_kernel(20, 1) == "segmented"
+    assert ctx.qp_kernel(80, 1) == "serial"  # unsupported horizon: serial whatever is asked
+    ctx.set_qp_kernel("auto")
+    assert ctx.qp_capacity(40) == 1024
+
+
 def test_ocp_occupancy_gate_parts_equal_one_part():
     """Ocp over two device slots (both cuda:0 here): a batch above one GPU's capacity at N = 60 (512
     instances) is split into two parts by shard.plan; the result equals a single-part solve bitwise."""
