@@ -30,4 +30,9 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format cs
 (cd $R && timeout -k 10 300 hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DQP_STAMPS -I sdf-nmpc_amd/csrc \
     tools/qp_stamps_drv.hip sdf-nmpc_amd/csrc/rti_qp.hip -o tools/_qp_stamps_drv)
 timeout -k 10 200 python3 $R/tools/qp_stamps.py > $O/qp_stamps.txt 2>&1
+# the segmented kernel: per-phase stamps (P = 4, B = 64 and 1024) and the serial / segmented sweep over B and N
+(cd $R && timeout -k 10 300 hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DSEG_STAMPS -I sdf-nmpc_amd/csrc \
+    tools/seg_stamps_drv.hip sdf-nmpc_amd/csrc/rti_qp_seg.hip sdf-nmpc_amd/csrc/rti_qp.hip -o tools/_qp_stamps_drv_seg)
+(cd $R && P=4 timeout -k 10 250 bash tools/_segrun.sh && cp gpurun_out/seg_stamps_b64.log $O/seg_stamps_b64.txt && cp gpurun_out/seg_stamps.log $O/seg_stamps_b1024.txt)
+(cd $R && for n in 40 60; do N=$n timeout -k 10 120 python3 tools/seg_sweep_b.py 1 8 64 256 512 1024 || exit 1; done) > $O/qp_kernel_sweep.txt 2>&1
 echo done
