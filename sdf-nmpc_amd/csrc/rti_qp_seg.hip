@@ -77,6 +77,12 @@ static_assert(CP_B + 10 <= CPL && CP_SC <= WIN && CP_PHI + 256 <= 2 * WIN, "coup
 __device__ __forceinline__ int trl(int i, int j) { return i * (i + 1) / 2 + j; }  // packed lower, j <= i
 // v[i] in the lanes with i == idx, as a chain of v_cndmask (a nested ?: of computed values compiles to a
 // divergent branch tree: exec save / restore per level)
+// an LDS read the source performs only where `ok` (0 elsewhere), as an unconditional read of a clamped
+// index: a conditional read compiles to a divergent branch around it
+__device__ __forceinline__ double ldsel(const sdfn::qpd::ldsd* base, int idx, bool ok) {
+    const double v = base[ok ? idx : 0];
+    return ok ? v : 0.0;
+}
 __device__ __forceinline__ double sel4(int i, double v0, double v1, double v2, double v3) {
     double r = v3;
     r = i == 2 ? v2 : r;
@@ -421,7 +427,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
                 const double d0 = rdlane(dv, 10), d1 = rdlane(dv, 11), d2_ = rdlane(dv, 12), d3 = rdlane(dv, 13);
                 const int bx = fx ? lane : 0;
                 const double bdv = cw[WF_B + bx] * d0 + cw[WF_B + 10 + bx] * d1 + cw[WF_B + 20 + bx] * d2_ + cw[WF_B + 30 + bx] * d3;
-                off -= fx ? bdv : fu ? dv : 0.0;
+                off -= (fx ? 1.0 : 0.0) * bdv + (fu ? 1.0 : 0.0) * dv;  // bdv used by every lane: its reads stay unconditional
             }
         }
         refill();
@@ -764,7 +770,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         double col[NX], inv[NX];
         // L = chol(P_b), one column per lane
 #pragma unroll
-        for (int i = 0; i < NX; ++i) col[i] = lane < NX ? Pb[i * NX + lane] : (i == (lane & 7) ? 1.0 : 0.0);
+        for (int i = 0; i < NX; ++i) {
+            const double v = Pb[i * NX + (lane < NX ? lane : 0)];
+            col[i] = lane < NX ? v : (i == (lane & 7) ? 1.0 : 0.0);
+        }
         chol_cols(col, inv, lane);
         SSTAMP(16);
         if (lane < NX) {
@@ -781,7 +790,8 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int row = g + 4 * r;
-            Lt[r] = (row < NX && c < NX && row >= c) ? win[CP_L + trl(row < NX ? row : 0, c < NX ? c : 0)] : 0.0;
+            const bool ok = row < NX && c < NX && row >= c;
+            Lt[r] = ldsel(win, CP_L + trl(ok ? row : 0, ok ? c : 0), ok);
         }
         d4 T = {0.0, 0.0, 0.0, 0.0};
         T = mfma(Cg[0], Lt[0], T);
@@ -802,7 +812,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         }
         wave_sync();
 #pragma unroll
-        for (int i = 0; i < NX; ++i) col[i] = lane < NX ? win[CP_V + i * NX + lane] : (i == (lane & 7) ? 1.0 : 0.0);
+        for (int i = 0; i < NX; ++i) {
+            const double v = win[CP_V + i * NX + (lane < NX ? lane : 0)];
+            col[i] = lane < NX ? v : (i == (lane & 7) ? 1.0 : 0.0);
+        }
         chol_cols(col, inv, lane);
         SSTAMP(18);
         if (lane < NX) {
@@ -817,7 +830,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         // row c of V = L U^-T: U^-1 (row c of L)^T in lane c, U[i][j] broadcast from lane j's column
         double y[NX];
 #pragma unroll
-        for (int j = 0; j < NX; ++j) y[j] = (lane < NX && j <= lane) ? win[CP_L + trl(lane < NX ? lane : 0, j)] : 0.0;
+        for (int j = 0; j < NX; ++j) {
+            const bool ok = lane < NX && j <= lane;
+            y[j] = ldsel(win, CP_L + trl(ok ? lane : 0, ok ? j : 0), ok);
+        }
 #pragma unroll
         for (int j = 0; j < NX; ++j) {
             y[j] *= inv[j];
@@ -843,9 +859,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         for (int r = 0; r < 4; ++r) {
             const int row = g + 4 * r, rc = row < NX ? row : 0, cc = c < NX ? c : 0;
             const bool in = row < NX && c < NX;
-            Ph[r] = in ? win[CP_X + cc * NX + rc] : (c == 14 && row < NX) ? vv[V_B + rc] : 0.0;
-            Vt[r] = in ? win[CP_V + rc * NX + cc] : 0.0;
-            VTt[r] = in ? win[CP_V + cc * NX + rc] : 0.0;
+            const double px = win[CP_X + cc * NX + rc], pbv = vv[V_B + rc];
+            Ph[r] = in ? px : (c == 14 && row < NX) ? pbv : 0.0;
+            Vt[r] = ldsel(win, CP_V + rc * NX + cc, in);
+            VTt[r] = ldsel(win, CP_V + cc * NX + rc, in);
         }
         d4 X = {0.0, 0.0, 0.0, 0.0};
         X = mfma(Vt[0], Ph[0], X);
@@ -888,8 +905,8 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
             const int row = g + 4 * r, rc = row < NX ? row : 0, cc = c < NX ? c : 0;
             const bool in = row < NX && c < NX;
             cPh[r] = win[CP_PHI + row * 16 + c];
-            cVTt[r] = in ? win[CP_V + cc * NX + rc] : 0.0;
-            cX[r] = in ? win[CP_X + rc * NX + cc] : 0.0;
+            cVTt[r] = ldsel(win, CP_V + cc * NX + rc, in);
+            cX[r] = ldsel(win, CP_X + rc * NX + cc, in);
         }
         d4 Lm = {0.0, 0.0, 0.0, 0.0};
         Lm = mfma(cVTt[0], cX[0], Lm);
@@ -927,13 +944,13 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         const double il = vv[V_IL + r], iu = vv[V_IU + r];
 #pragma unroll
         for (int j = 0; j < NX; ++j) {
-            const double lij = (lane > j && lane < NX) ? win[CP_L + trl(r, j)] : 0.0;
+            const double lij = ldsel(win, CP_L + trl(r, j), lane > j && lane < NX);
             qr = lane == j ? qr * il : qr;
             qr = fma(-lij, rdlane(qr, j), qr);
         }
 #pragma unroll
         for (int j = 0; j < NX; ++j) {
-            const double uij = (lane > j && lane < NX) ? win[CP_U + trl(r, j)] : 0.0;
+            const double uij = ldsel(win, CP_U + trl(r, j), lane > j && lane < NX);
             qr = lane == j ? qr * iu : qr;
             qr = fma(-uij, rdlane(qr, j), qr);
         }
