@@ -108,6 +108,10 @@ typedef struct {
                               -2 (1 - s/2)^3 J_h[2] are formed from h / J_h by the QP (yref, W: [B][N][ny]) */
     int lm_scaling;        /* 1: Levenberg-Marquardt term lm dt_k at stages k < N and lm at N (acados adds
                               Ts[k] * levenberg_marquardt); 0: lm at every node */
+    int warm_start;        /* qp_solver_warm_start (ocp.py:116, HPIPM's primal warm start): 1 = the IPM starts
+                              from the du found in sdfnmpc_qp_args.du on entry (the previous QP's solution --
+                              the solver object keeps it between steps; zero after init), dx rolled out from
+                              x0 under it, t / lambda by the cold start's rule; 0 = du = 0 (cold) */
 } sdfnmpc_qp_opts;
 
 /* Batched QP of the RTI feedback phase, built from sdfnmpc_linearize outputs. */

@@ -171,15 +171,16 @@ QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", 
 
 
 # IPM starting point / step fraction of csrc/rti_qp.hip (QP_T0, QP_L0, QP_LC, QP_TAU_LO, QP_TAU_HI)
-QP_START = dict(t0=0.5, l0=1.0, lc=0.5, tau_lo=0.995, tau_hi=0.995, seg=1, gk=0, ga=1.0, gd=0.1, gbmin=0.1, gbmax=10.0)
+QP_START = dict(t0=0.5, l0=1.0, lc=0.5, tau_lo=0.995, tau_hi=0.995, seg=1, gk=0, ga=1.0, gd=0.1, gbmin=0.1, gbmax=10.0, ws=0)
 
 
 def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_scaling=True, nthreads=1, lm_scaling=True,
-                 start=None):
+                 start=None, du_ws=None):
     """Structured Riccati IPM (qp_ipm.c) over a batch: the CPU restatement of the feedback-phase QP.
 
     lin: linearisation outputs (xn, AB, y, Jy, yN, JyN, h, Jh) with a leading batch dimension;
     prob: x, u, yref, W, yN (reference), WN, dt.  Returns dict(dx, du, slack, iters, status, res).
+    du_ws: primal warm start (B, N, 4), the previous QP's du (HPIPM's qp_solver_warm_start = 1, ocp.py:116).
     """
     B, N = lin["xn"].shape[0], lin["xn"].shape[1]
     arrs = dict(lin)
@@ -187,8 +188,9 @@ def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_sca
     arrs = {k: np.ascontiguousarray(arrs[k], dtype=np.float64) for k in QP_IN}
     dt = np.ascontiguousarray(prob["dt"], dtype=np.float64)
     opts = np.concatenate([model.lbu, model.ubu, model.lh, model.uh, model.zl, model.Zl, [lm, tol, float(bool(lm_scaling))],
-                           [v for v in {**QP_START, **(start or {})}.values()]]).astype(np.float64)
-    out = dict(dx=np.zeros((B, N + 1, 10)), du=np.zeros((B, N, 4)), slack=np.zeros((B, N + 1, 3, 2)),
+                           [v for v in {**QP_START, **(start or {}), "ws": float(du_ws is not None)}.values()]]).astype(np.float64)
+    du0 = np.zeros((B, N, 4)) if du_ws is None else np.array(du_ws, dtype=np.float64).reshape(B, N, 4)
+    out = dict(dx=np.zeros((B, N + 1, 10)), du=du0, slack=np.zeros((B, N + 1, 3, 2)),
                iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32), res=np.zeros((B, 4)))
     d = C.c_double
     ny = arrs["W"].shape[-1]

@@ -35,6 +35,10 @@ typedef struct {
      * onto [gbmin, gbmax] sigma mu; a corrector is kept when it lengthens the step by >= 0.1 gd */
     int gk;
     double ga, gd, gbmin, gbmax;
+    /* primal warm start (HPIPM's qp_solver_warm_start = 1, ocp.py:116): the start point takes du from the
+     * du buffer on entry (the previous QP's solution) instead of 0; dx is the dynamics rollout from x0 under
+     * that du, t / lambda follow the cold start's rule on the rows there */
+    int ws;
 } qp_opts_c;
 
 typedef struct {                  /* stage k < N, or the terminal node k = N (x part only) */
@@ -621,13 +625,16 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     }
     for (int i = 0; i < NX; ++i) Q.x0[i] = x0[i] - x[i];
 
-    /* ---- starting point (rti_qp.hip's): dynamics-feasible with du = sl = su = 0; t = max(row, 0.7);
-     * lambda = 0.5 on box rows, max(0.5, 0.5 s_k zl_j) on the rows of soft group (k, j) */
+    /* ---- starting point (rti_qp.hip's): dynamics-feasible with du = sl = su = 0 (o->ws: du = the du
+     * buffer's entry values); t = max(row, t0); lambda = l0 on box rows, max(l0, lc s_k zl_j) on the rows
+     * of soft group (k, j) */
     memcpy(zdx, Q.x0, sizeof(double) * NX);
+    if (o->ws) memcpy(zdu, du, sizeof(double) * N * NU);
     for (int k = 0; k < N; ++k)
         for (int a = 0; a < NX; ++a) {
             double s = Q.st[k].c[a];
             for (int l = 0; l < NX; ++l) s += Q.st[k].A[a][l] * zdx[k * NX + l];
+            for (int j = 0; j < NU; ++j) s += Q.st[k].Bm[a][j] * zdu[k * NU + j];
             zdx[(k + 1) * NX + a] = s;
         }
     rows_at(&Q, zdx, zdu, zsl, zsu, rv);
@@ -771,6 +778,7 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
     o.t0 = opts[23]; o.l0 = opts[24]; o.lc = opts[25]; o.tau_lo = opts[26]; o.tau_hi = opts[27];
     o.nseg = (int)opts[28];
     o.gk = (int)opts[29]; o.ga = opts[30]; o.gd = opts[31]; o.gbmin = opts[32]; o.gbmax = opts[33];
+    o.ws = opts[34] != 0.0;
     o.max_iter = max_iter;
     o.cost_scaling = cost_scaling;
     const int N1 = N + 1;

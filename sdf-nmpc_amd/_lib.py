@@ -60,7 +60,8 @@ class LinArgsC(C.Structure):
 class QpOptsC(C.Structure):
     _fields_ = [("lbu", C.c_double * 4), ("ubu", C.c_double * 4), ("lh", C.c_double * 3), ("uh", C.c_double * 3),
                 ("zl", C.c_double * 3), ("Zl", C.c_double * 3), ("lm", C.c_double), ("cost_scaling", C.c_int),
-                ("max_iter", C.c_int), ("tol", C.c_double), ("ny", C.c_int), ("lm_scaling", C.c_int)]
+                ("max_iter", C.c_int), ("tol", C.c_double), ("ny", C.c_int), ("lm_scaling", C.c_int),
+                ("warm_start", C.c_int)]
 
 
 class RefOptsC(C.Structure):
@@ -355,13 +356,14 @@ def linearize(ctx: Context, net: Net, model: QuadModelC, B: int, N: int, np_: in
     _check(load().sdfnmpc_linearize(ctx.h, net.h, C.byref(model), C.byref(a)))
 
 
-def qp_opts(model, lm=10.0, cost_scaling=True, max_iter=100, tol=1e-8, lm_scaling=True) -> QpOptsC:
+def qp_opts(model, lm=10.0, cost_scaling=True, max_iter=100, tol=1e-8, lm_scaling=True, warm_start=False) -> QpOptsC:
     """QP data of the 'att' model (model.Quad) + solver options (ocp.py:113-120 defaults).  lm_scaling: the
-    Levenberg-Marquardt term is lm dt_k at stages k < N and lm at N (acados' Ts-scaled term)."""
+    Levenberg-Marquardt term is lm dt_k at stages k < N and lm at N (acados' Ts-scaled term).  warm_start:
+    HPIPM's primal warm start (ocp.py:116) -- the IPM starts from the du buffer's entry values."""
     v = lambda a, n: (C.c_double * n)(*[float(x) for x in a])
     return QpOptsC(v(model.lbu, 4), v(model.ubu, 4), v(model.lh, 3), v(model.uh, 3), v(model.zl, 3),
                    v(model.Zl, 3), float(lm), int(bool(cost_scaling)), int(max_iter), float(tol), int(model.ny),
-                   int(bool(lm_scaling)))
+                   int(bool(lm_scaling)), int(bool(warm_start)))
 
 
 def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):

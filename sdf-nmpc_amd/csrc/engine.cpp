@@ -1125,6 +1125,7 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
     for (int i = 0; i < 3; ++i) { q.lh[i] = o->lh[i]; q.uh[i] = o->uh[i]; q.zl[i] = o->zl[i]; q.Zl[i] = o->Zl[i]; }
     q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling; q.ny = o->ny;
     q.lm_scaling = o->lm_scaling;
+    q.warm_start = o->warm_start ? 1 : 0;
     return SDFNMPC_OK;
 }
 

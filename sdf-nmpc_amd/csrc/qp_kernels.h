@@ -27,6 +27,7 @@ struct QpArgs {
     int pack_part;  // 0: whole stage records; 1: all but the sdf row of C^T (needs ny == 11), which
                     // rti_qp_kernel then copies from J_h itself (sdf_row_patch)
     int sdf_row_patch;  // rti_qp_kernel: copy J_h[.][2] into the records' C^T row 2 before the sweeps
+    int warm_start;     // 1: the IPM starts from the du found in du on entry (qp_solver_warm_start, ocp.py:116)
 };
 
 constexpr int QP_REC = 304;   // stage record: [A B | c | g | C^T | H upper | 0 ..] (128-B rows) (rti_qp.hip)

@@ -306,7 +306,7 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     // ------------------------------------------------------------ per-node constants into LDS
     for (int e = lane; e < N * NU; e += 64) {
         s.uu[e] = A.u[(size_t)b * N * NU + e];
-        s.du[e] = 0.0;
+        s.du[e] = A.warm_start ? A.du[(size_t)b * N * NU + e] : 0.0;  // primal warm start: the previous QP's du
     }
     for (int e = lane; e < N1 * NS; e += 64) s.hv[e] = A.h[(size_t)b * N1 * NS + e];
     {
@@ -391,6 +391,11 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
             for (int l = 0; l < NX; ++l) row[l] = rp[l * str];
             off = *(fx ? win + R_C + lane : s.zero);
+            // + B du_k of the start iterate (0 on a cold start): B[r][j] at R_AB + 10 (NX + j) + r
+            const int bx = fx ? lane : 0, ku = k < N ? k : N - 1;
+            const double bdu = win[R_AB + 100 + bx] * s.du[ku * NU] + win[R_AB + 110 + bx] * s.du[ku * NU + 1] +
+                               win[R_AB + 120 + bx] * s.du[ku * NU + 2] + win[R_AB + 130 + bx] * s.du[ku * NU + 3];
+            off += (fx ? 1.0 : 0.0) * bdu;
         } else {
             const ldsd* fk = k < PD ? s.fsave + k * F_FW : win;
             // 16-byte aligned rows: [A~ | b~] / [K | k_ff] row `lane`, C^T row lane - 14, zeros
@@ -656,14 +661,15 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     };
 
     // ------------------------------------------------------------ initial iterate (dynamics-feasible):
-    // du = sl = su = 0, dx_0 = x0 - xbar_0, dx_{k+1} = A dx_k + c_k (sweep 0), then the rows
+    // du = sl = su = 0 (warm start: du = the previous QP's), dx_0 = x0 - xbar_0, dx_{k+1} = A dx_k + B du_k + c_k
+    // (sweep 0), then the rows
     auto rows_init = [&]() -> double {
     double rp = 0.0;
     for (int r = lane; r < m; r += 64) {
         double v, l0 = L0;
         if (r < 8 * N) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
-            v = box_d(k, i, up);
+            v = box_d(k, i, up) + (up ? -s.du[k * NU + i] : s.du[k * NU + i]);
         } else {
             const int q = r - 8 * N, k = q / 12, w = q - 12 * k, j = w >> 2, kind = w & 3;
             const double h = s.hv[k * 3 + j];

@@ -295,6 +295,9 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     const double ubv = ownb ? A.u[((size_t)b * N + kbc) * NU + ib] : 0.0;
     const double hsv = owns ? A.h[((size_t)b * N1 + ksc) * NS + js] : 0.0;
     if (tid < NX) s.dxc[tid] = A.x0[(size_t)b * 10 + tid] - A.x[(size_t)b * N1 * 10 + tid];
+    // du of the start iterate into dua (free until the first forward sweep): 0, or on a primal warm start
+    // the previous QP's du as found in A.du (qp_solver_warm_start, ocp.py:116)
+    for (int e = tid; e < N * NU; e += 64 * NSEG) s.dua[e] = A.warm_start ? A.du[(size_t)b * N * NU + e] : 0.0;
     wg_sync();
     // row constants: box rows at du = 0 (dlo, dup), soft rows at C dx = 0 (hl0, hu0), slack weights
     auto dlo = [&]() { return ubv - s.cst[ib]; };
@@ -405,6 +408,11 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
 #pragma unroll
             for (int l = 0; l < NX; ++l) row[l] = rp[l * str];
             off = *(fx ? cw + R_C + lane : s.zero);
+            // + B du_k of the start iterate (dua; 0 on a cold start): B[r][j] at R_AB + 10 (NX + j) + r
+            const int bx = fx ? lane : 0, ku = k < N ? k : N - 1;
+            const double bdu = cw[R_AB + 100 + bx] * s.dua[ku * NU] + cw[R_AB + 110 + bx] * s.dua[ku * NU + 1] +
+                               cw[R_AB + 120 + bx] * s.dua[ku * NU + 2] + cw[R_AB + 130 + bx] * s.dua[ku * NU + 3];
+            off += (fx ? 1.0 : 0.0) * bdu;
         } else {
             const ldsd2* rp = (const ldsd2*)(lane < 14 ? cw + lane * FR : fc ? cw + WF_CT + fcj * 10 : s.zero);
 #pragma unroll
@@ -1063,12 +1071,14 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     wg_sync();
     for (int e = lane; e < nn * NX; e += 64) A.dx[((size_t)b * N1 + sa) * NX + e] = s.dxc[sa * NX + e];
     const int nu_ = (sb < N ? sb : N) - sa;
-    for (int e = lane; e < nu_ * NU; e += 64) A.du[((size_t)b * N + sa) * NU + e] = 0.0;
+    if (!A.warm_start)
+        for (int e = lane; e < nu_ * NU; e += 64) A.du[((size_t)b * N + sa) * NU + e] = 0.0;
     double rp = 0.0;
     {
         double rl = 0.0;
         if (ownb) {
-            const double d0 = dlo(), d1 = dup();
+            const double du = s.dua[kbc * NU + ib];  // the start iterate's
+            const double d0 = dlo() + du, d1 = dup() - du;
             tb0 = fmax(d0, T0); tb1 = fmax(d1, T0); lb0 = L0; lb1 = L0;
             rl = fmax(fabs(d0 - tb0), fabs(d1 - tb1));
         }

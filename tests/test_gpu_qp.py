@@ -240,3 +240,37 @@ def test_qp_sdf_cost_matches_riccati_oracle(gpu_ctx, oracle_lib, cfg):
     _, _, t2 = setup(gpu_ctx, cfg, B, N, 21, x0_noise=0.2)
     solve(gpu_ctx, cfg, t2, B, N, tol=QP_TOL)
     assert np.abs(t2["du"].cpu().numpy() - ref["du"]).max() > 1e-6
+
+
+@pytest.mark.parametrize("kernel", ["serial", "segmented"])
+def test_qp_warm_start_matches_riccati_oracle(gpu_ctx, oracle_lib, cfg, kernel):
+    """qp_solver_warm_start (ocp.py:116): the IPM starts from the du found in the du buffer.  Both kernels
+    against the C restatement started from the same du (same iteration counts up to a rounding tie, the
+    same solution); a zero du reproduces the cold start bit for bit."""
+    import torch
+    B, N = 32, 40
+    prob, x0, t = setup(gpu_ctx, cfg, B, N, 13, x0_noise=0.2)
+    du_ws = np.random.default_rng(14).normal(0, 0.1, (B, N, 4))
+    gpu_ctx.set_qp_kernel(kernel)
+    try:
+        solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL)
+        cold = {k: t[k].cpu().numpy().copy() for k in ("du", "dx", "iters")}
+        t["du"].zero_()
+        solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL, warm_start=True)
+        for k in ("du", "dx", "iters"):
+            assert np.array_equal(t[k].cpu().numpy(), cold[k]), k
+        t["du"].copy_(torch.from_numpy(du_ws))  # one iteration from the warm start: the start itself is pinned
+        solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL, warm_start=True, max_iter=1)
+        one = t["du"].cpu().numpy().copy()
+        t["du"].copy_(torch.from_numpy(du_ws))
+        model = solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL, warm_start=True)
+    finally:
+        gpu_ctx.set_qp_kernel("auto")
+    assert (t["status"].cpu().numpy() == 0).all()
+    lin = {k: t[k].cpu().numpy() for k in ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh")}
+    ref = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, nthreads=8, du_ws=du_ws)
+    assert (ref["status"] == 0).all() and np.abs(ref["du"] - cold["du"]).max() > 0  # another path, same optimum
+    ref1 = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, max_iter=1, nthreads=8, du_ws=du_ws)
+    np.testing.assert_allclose(one, ref1["du"], rtol=0, atol=1e-9)
+    _agree(prob, x0, lin, model, {k: t[k].cpu().numpy() for k in ("du", "dx", "slack")}, ref)
+    assert np.abs(t["iters"].cpu().numpy() - ref["iters"]).max() <= 1

@@ -108,6 +108,35 @@ def test_riccati_ipm_threads_and_batch_invariance(oracle_lib, cfg):
     assert full["iters"][b] == one["iters"][0]
 
 
+def test_riccati_ipm_warm_start(oracle_lib, cfg):
+    """qp_solver_warm_start (ocp.py:116, HPIPM's primal warm start): the IPM started from a given du.  A
+    zero du is the cold start bit for bit; a random one still reaches the unique solution (the exact one,
+    to SOL_ATOL) along a different path; the input du is not modified."""
+    import qp_oracle
+    model = Quad(cfg)
+    B, N = 4, 20
+    prob, x0, lin = _instance_set(oracle_lib, cfg, B, N, 17, 0.2)
+    cold = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL)
+    zero = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, du_ws=np.zeros((B, N, 4)))
+    for k in ("du", "dx", "slack", "iters"):
+        assert np.array_equal(cold[k], zero[k]), k
+    du_ws = np.random.default_rng(18).normal(0, 0.1, (B, N, 4))
+    keep = du_ws.copy()
+    warm = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, du_ws=du_ws)
+    assert np.array_equal(du_ws, keep)
+    assert (warm["status"] == 0).all()
+    # the start is live: one iteration from it lands elsewhere than one from the cold start
+    one_c = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, max_iter=1)
+    one_w = oracle_lib.qp_ipm_batch(lin, prob, x0, model, tol=QP_TOL, max_iter=1, du_ws=du_ws)
+    assert np.abs(one_c["du"] - one_w["du"]).max() > 1e-3
+    for b in range(B):
+        q = qp_oracle.stage_qp({k: v[b] for k, v in lin.items()}, prob["x"][b], prob["u"][b], x0[b], prob["yref"][b],
+                               prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], model, 10.0)
+        ref = _exact(q)
+        np.testing.assert_allclose(warm["du"][b], ref["du"], rtol=0, atol=SOL_ATOL)
+        np.testing.assert_allclose(warm["dx"][b], ref["dx"], rtol=0, atol=SOL_ATOL)
+
+
 def test_riccati_ipm_solution_is_feasible(oracle_lib, cfg):
     model = Quad(cfg)
     prob, x0, lin = _instance_set(oracle_lib, cfg, 4, 40, 11, 0.3)
