@@ -238,6 +238,18 @@ int sdfnmpc_sdf_eval(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, c
  * df[rows], grad[rows][3+128] (optional). Computed in fp32 on the device, returned as fp64. */
 int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const double* in, double* df,
                           double* grad);
+/* Calls of sdfnmpc_sdf_eval_host with at most 16 rows (the CasADi external's one row per node) are
+ * served by a resident server kernel: one persistent workgroup on its own stream polls a mailbox in
+ * pinned host memory, so a call costs no launch, no copies and no stream synchronisation.  It exits
+ * after SDFNMPC_SDF_SERVER_IDLE_MS (default 20) without a request, on sdfnmpc_ctx_destroy, or after 10 s
+ * (relaunched on the next call).  on = 0 stops it and returns to one launch per call (also
+ * SDFNMPC_SDF_SERVER=0); results are bitwise the same either way. */
+int sdfnmpc_ctx_set_sdf_server(sdfnmpc_ctx* ctx, int on);
+/* diagnostics: mean microseconds per served request since the last call -- out18[0] staging the request,
+ * [1] evaluating it, [2] the caller's wait from posting to the answer; out18[3] = requests;
+ * out18[4..17] the evaluation's phases (embedding, 4 x (layer GEMV, sine), the last sine, 4 backward
+ * GEMVs, outputs) */
+int sdfnmpc_ctx_sdf_server_stats(sdfnmpc_ctx* ctx, double* out18);
 
 /* ---- batched preparation phase ---- */
 int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* model,

@@ -23,7 +23,7 @@ L4C_PATH = os.path.join(LIB_DIR, "libsdf_l4c.so")
 SYMBOLS = [
     "sdfnmpc_abi_version", "sdfnmpc_last_error", "sdfnmpc_ctx_create", "sdfnmpc_ctx_destroy",
     "sdfnmpc_ctx_set_stream", "sdfnmpc_ctx_use_null_stream", "sdfnmpc_ctx_stream", "sdfnmpc_ctx_synchronize", "sdfnmpc_ctx_set_tile_rows",
-    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_qp_kernel", "sdfnmpc_qp_lds_bytes", "sdfnmpc_qp_capacity",
+    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_set_sdf_server", "sdfnmpc_ctx_sdf_server_stats", "sdfnmpc_ctx_qp_kernel", "sdfnmpc_qp_lds_bytes", "sdfnmpc_qp_capacity",
     "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
@@ -123,6 +123,8 @@ def load():
         "sdfnmpc_ctx_synchronize": (i, [vp]),
         "sdfnmpc_ctx_set_tile_rows": (i, [vp, i]),
         "sdfnmpc_ctx_set_qp_kernel": (i, [vp, i]),
+        "sdfnmpc_ctx_set_sdf_server": (i, [vp, i]),
+        "sdfnmpc_ctx_sdf_server_stats": (i, [vp, P(d)]),
         "sdfnmpc_ctx_qp_kernel": (i, [vp, i, i]),
         "sdfnmpc_qp_lds_bytes": (C.c_longlong, [i]),
         "sdfnmpc_qp_capacity": (C.c_longlong, [vp, i]),
@@ -226,6 +228,18 @@ class Context:
         """'auto' (segmented for B <= 256 -- 512 from N = 48 -- at 36 <= N <= 63, else serial), 'serial' or
         'segmented' (include/sdfnmpc.h)."""
         _check(load().sdfnmpc_ctx_set_qp_kernel(self.h, self.QP_KERNELS[kind]))
+
+    def set_sdf_server(self, on: bool):
+        """Serve the host-pointer SDF path (sdf_eval_host, <= 16 rows) from the resident server kernel
+        (default) or with one launch per call (include/sdfnmpc.h)."""
+        _check(load().sdfnmpc_ctx_set_sdf_server(self.h, int(bool(on))))
+
+    def sdf_server_stats(self) -> dict:
+        """Mean microseconds per served request since the last call (diagnostics)."""
+        o = (C.c_double * 18)()
+        _check(load().sdfnmpc_ctx_sdf_server_stats(self.h, o))
+        return {"stage_us": o[0], "eval_us": o[1], "wait_us": o[2], "requests": int(o[3]),
+                "phases_us": [round(v, 2) for v in o[4:18]]}
 
     def qp_kernel(self, N: int, B: int) -> str:
         """The kernel a QP batch of B instances at horizon N runs ('serial' or 'segmented')."""

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -89,6 +90,23 @@ struct sdfnmpc_ctx {
     DevBuf hin, hout, hc13;
     std::vector<float> h_lat;
     uint64_t h_net = 0;  // uid of the network the cached hoist belongs to
+    // resident SDF server of the host path (sdf_row.hip, SdfMbox): mailbox in pinned coherent memory, its
+    // own stream, the network it serves, the last request number, and whether it may still be running
+    struct {
+        int mode = -1;                // -1: from SDFNMPC_SDF_SERVER (default on), 0 off, 1 on
+        SdfMbox* mb = nullptr;
+        SdfMbox* mb_dev = nullptr;
+        hipStream_t stream = nullptr;
+        uint64_t net = 0;
+        unsigned long long seq = 0;
+        bool live = false;
+        long long idle_ticks = 0, life_ticks = 0;
+        double idle_s = 0.02;
+        double khz = 100000.0;
+        std::chrono::steady_clock::time_point last{};
+        double acc[4] = {0, 0, 0, 0};  // diagnostics: us staging, computing, host round trip; calls
+        double ph[14] = {};            // diagnostics: us per row_eval phase
+    } srv;
     std::map<std::string, KStat> stats;
     std::mutex mu;  // serialises the host-pointer path (CasADi externals may be called concurrently)
     // stage records packed by sdfnmpc_rti_prepare, consumed by the next sdfnmpc_qp_feedback
@@ -181,9 +199,22 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
     return SDFNMPC_OK;
 }
 
+static void srv_stop(sdfnmpc_ctx* ctx) {  // ask the resident SDF server to exit and wait for it
+    if (!ctx->srv.mb) return;
+    __atomic_store_n(&ctx->srv.mb->stop, 1ull, __ATOMIC_RELEASE);
+    (void)hipStreamSynchronize(ctx->srv.stream);
+    __atomic_store_n(&ctx->srv.mb->stop, 0ull, __ATOMIC_RELEASE);
+    ctx->srv.live = false;
+}
+
 extern "C" void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx) {
     if (!ctx) return;
     ScopedDevice sd(ctx->device);
+    if (ctx->srv.mb) {
+        srv_stop(ctx);
+        (void)hipStreamDestroy(ctx->srv.stream);
+        (void)hipHostFree(ctx->srv.mb);
+    }
     (void)hipStreamSynchronize(ctx->stream);
     for (auto& kv : ctx->stats)
         for (auto& ev : kv.second.pending) {
@@ -892,6 +923,117 @@ extern "C" int sdfnmpc_sdf_eval(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long l
 // call; tools/launch_lat.hip: a bare launch + hipStreamSynchronize is 11 us on the box)
 static hipError_t host_wait(sdfnmpc_ctx* ctx) { return hipStreamSynchronize(ctx->stream); }
 
+static bool srv_enabled(sdfnmpc_ctx* ctx) {
+    if (ctx->srv.mode < 0) {
+        const char* e = getenv("SDFNMPC_SDF_SERVER");
+        ctx->srv.mode = (e && *e == '0') ? 0 : 1;
+        if (const char* ms = getenv("SDFNMPC_SDF_SERVER_IDLE_MS")) {
+            const double v = atof(ms);
+            if (v > 0.0) ctx->srv.idle_s = v * 1e-3;
+        }
+    }
+    return ctx->srv.mode == 1;
+}
+
+// One request to the resident SDF server (sdf_row.hip): the staged fp32 request (hp [rows][4], hl
+// [rows][L]) goes into the mailbox, the results come back into ho in the staged path's layout.  The
+// server is (re)launched when it is not running -- first call, a different network, or after it left on
+// its idle timeout; a server that exits while a request is posted is relaunched and serves it (it
+// serves every seq_in above the seq_out it finds).
+static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const float* hp, const float* hl, bool grad,
+                    float* ho) {
+    using clk = std::chrono::steady_clock;
+    auto& S = ctx->srv;
+    if (!S.mb) {
+        HIPCHK(hipHostMalloc((void**)&S.mb, sizeof(SdfMbox), hipHostMallocCoherent | hipHostMallocMapped));
+        memset((void*)S.mb, 0, sizeof(SdfMbox));
+        HIPCHK(hipHostGetDevicePointer((void**)&S.mb_dev, S.mb, 0));
+        int lo = 0, hi = 0;
+        (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+        HIPCHK(hipStreamCreateWithPriority(&S.stream, hipStreamNonBlocking, hi));
+        int khz = 0;
+        HIPCHK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, ctx->device));
+        if (khz <= 0) khz = 100000;
+        S.khz = khz;
+        S.idle_ticks = (long long)(S.idle_s * khz * 1e3);
+        S.life_ticks = (long long)(10.0 * khz * 1e3);  // relaunched at most every 10 s
+        S.seq = 0;
+        S.live = false;
+    }
+    if (S.live && S.net != net->uid) srv_stop(ctx);
+    if (S.live && std::chrono::duration<double>(clk::now() - S.last).count() > 0.5 * S.idle_s) {
+        const hipError_t q = hipStreamQuery(S.stream);
+        if (q == hipSuccess) S.live = false;
+        else if (q != hipErrorNotReady) return fail(SDFNMPC_E_HIP, std::string("sdf server: ") + hipGetErrorString(q));
+    }
+    memcpy(S.mb->in, hp, (size_t)rows * 4 * sizeof(float));
+    memcpy(S.mb->in + (size_t)rows * 4, hl, (size_t)rows * L * sizeof(float));
+    S.mb->rows = rows;
+    S.mb->grad = grad ? 1 : 0;
+    const unsigned long long seq = ++S.seq;
+    __atomic_store_n(&S.mb->seq_in, seq, __ATOMIC_RELEASE);
+    SdfRowArgs ra = net->row;
+    if (!S.live) {
+        HIPCHK(launch_sdf_server(ra, S.mb_dev, S.idle_ticks, S.life_ticks, S.stream));
+        S.live = true;
+        S.net = net->uid;
+    }
+    const auto t0 = clk::now();
+    for (unsigned long spin = 1;; ++spin) {
+        if (__atomic_load_n(&S.mb->seq_out, __ATOMIC_ACQUIRE) == seq) break;
+        if ((spin & 1023) == 0) {
+            const hipError_t q = hipStreamQuery(S.stream);
+            if (q == hipSuccess) {  // the server left before it saw this request
+                if (__atomic_load_n(&S.mb->seq_out, __ATOMIC_ACQUIRE) == seq) break;
+                HIPCHK(launch_sdf_server(ra, S.mb_dev, S.idle_ticks, S.life_ticks, S.stream));
+            } else if (q != hipErrorNotReady) {
+                S.live = false;
+                return fail(SDFNMPC_E_HIP, std::string("sdf server: ") + hipGetErrorString(q));
+            }
+            if (std::chrono::duration<double>(clk::now() - t0).count() > 5.0) {
+                srv_stop(ctx);
+                return fail(SDFNMPC_E_HIP, "sdf server: no answer within 5 s");
+            }
+        }
+    }
+    const volatile float* o = S.mb->out;
+    const size_t n = (size_t)rows * (grad ? 4 + L : 4);
+    for (size_t i = 0; i < n; ++i) ho[i] = o[i];
+    S.last = clk::now();
+    const volatile SdfMbox* vm = S.mb;
+    S.acc[0] += (double)(vm->t_staged - vm->t_seen) * 1e3 / S.khz;
+    S.acc[1] += (double)(vm->t_done - vm->t_staged) * 1e3 / S.khz;
+    S.acc[2] += std::chrono::duration<double>(S.last - t0).count() * 1e6;
+    S.acc[3] += 1.0;
+    for (int i = 0; i < 14; ++i)
+        S.ph[i] += (double)(vm->t_phase[i] - (i ? vm->t_phase[i - 1] : vm->t_staged)) * 1e3 / S.khz;
+    return SDFNMPC_OK;
+}
+
+// mean microseconds per served request since the last call: [0] staging the request into LDS, [1] the
+// evaluation, [2] the host's wait from posting to the answer; [3] requests; [4..17] the evaluation's
+// phases (row_eval's ROW_STAMPs) (diagnostics, tools/c2_server_probe.py)
+extern "C" int sdfnmpc_ctx_sdf_server_stats(sdfnmpc_ctx* ctx, double* out18) {
+    if (!ctx || !out18) return fail(SDFNMPC_E_ARG, "bad sdfnmpc_ctx_sdf_server_stats arguments");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    const double n = ctx->srv.acc[3];
+    for (int i = 0; i < 3; ++i) out18[i] = n > 0 ? ctx->srv.acc[i] / n : 0.0;
+    out18[3] = n;
+    for (int i = 0; i < 14; ++i) out18[4 + i] = n > 0 ? ctx->srv.ph[i] / n : 0.0;
+    for (double& a : ctx->srv.acc) a = 0.0;
+    for (double& a : ctx->srv.ph) a = 0.0;
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_ctx_set_sdf_server(sdfnmpc_ctx* ctx, int on) {
+    if (!ctx || on < 0 || on > 1) return fail(SDFNMPC_E_ARG, "bad sdfnmpc_ctx_set_sdf_server arguments");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    ScopedDevice sd(ctx->device);
+    if (!on) srv_stop(ctx);
+    ctx->srv.mode = on;
+    return SDFNMPC_OK;
+}
+
 extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const double* in,
                                      double* df, double* grad) {
     if (!ctx || !net || rows < 0 || (rows > 0 && (!in || !df))) return fail(SDFNMPC_E_ARG, "bad sdf_eval_host arguments");
@@ -918,7 +1060,10 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         for (int k = 0; k < L; ++k) hl[(size_t)r * L + k] = (float)in[(size_t)r * D + 3 + k];
     }
     const bool use_row = !net->wide && rows <= SDF_ROW_MAX;
-    if (use_row) {  // the latency path: one launch, no hoist (sdf_row.hip).  Zero-copy (the kernel reading
+    if (use_row && srv_enabled(ctx)) {  // the resident server: no launch, no copies, no synchronisation
+        const int rc = srv_call(ctx, net, rows, hp, hl, grad != nullptr, ho);
+        if (rc) return rc;
+    } else if (use_row) {  // the latency path: one launch, no hoist (sdf_row.hip).  Zero-copy (the kernel reading
         // and writing the pinned block over PCIe) was measured equal in wall time: the PCIe reads add
         // ~2 us to the kernel, as much as the two staging copies cost.
         HIPCHK(ctx->hin.ensure(nin * sizeof(float)));

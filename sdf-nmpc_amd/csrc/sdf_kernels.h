@@ -83,9 +83,30 @@ struct SdfRowArgs {
     int np, rows_per_inst;
     double *h, *Jh;         // [rows][3], [rows][10][3]: the sdf row
     double max_df;
+    long long* stamps;      // diagnostics: phase wall-clock stamps (the server), or NULL
 };
 constexpr int SDF_ROW_MAX = 16;       // host-path calls with at most this many rows use sdf_row_kernel
 constexpr int SDF_ROW_PREP_MAX = 64;  // and preparation phases with at most this many rows (B=1 at N <= 63)
+
+// Resident SDF server (the C2 latency path, sdf_row.hip): one persistent workgroup polls this mailbox in
+// pinned, coherent host memory, so a CasADi-external call costs no kernel launch and no copies.  The host
+// writes rows / grad / in, then seq_in (release); the server stages the request into LDS, evaluates the
+// rows with sdf_row's arithmetic, writes out, then seq_out = seq_in (release).  The server exits on
+// `stop`, after `idle` wall-clock ticks without a request, or after `life` ticks in total; the host
+// relaunches it when it finds it gone.  Sequence words sit on their own 128-byte lines.
+struct alignas(128) SdfMbox {
+    unsigned long long seq_in;
+    unsigned long long pad0[15];
+    unsigned long long seq_out;
+    unsigned long long pad1[15];
+    unsigned long long stop;
+    int rows, grad;
+    long long t_seen, t_staged, t_done;  // server wall-clock stamps of the last request (diagnostics)
+    unsigned long long pad2[11];
+    long long t_phase[16];               // row_eval's phase stamps of the last request (diagnostics)
+    float in[SDF_ROW_MAX * (4 + 128)];   // [rows][4] Co_p_B | [rows][L] latent
+    float out[SDF_ROW_MAX * (4 + 128)];  // [rows][4] (df, d df / d pos) | [rows][L] d df / d latent
+};
 
 template <typename T>
 struct HoistArgs {
@@ -141,6 +162,8 @@ size_t sdf_lds_bytes(int M);
 hipError_t sdf_set_lds_limits();
 hipError_t launch_sdf_mlp(const SdfArgs& a, int M, bool latent_grad, hipStream_t s);
 hipError_t launch_sdf_row(const SdfRowArgs& a, hipStream_t s);
+hipError_t launch_sdf_server(const SdfRowArgs& a, SdfMbox* mb_dev, long long idle_ticks, long long life_ticks,
+                             hipStream_t s);
 template <typename T>
 hipError_t launch_hoist(const HoistArgs<T>& a, hipStream_t s);
 

@@ -216,3 +216,27 @@ def test_l4c_shim_reconfigure_invalidates_every_thread(tmp_path):
     out = np.zeros(1)
     lib.sdf_l4c((D * 1)(x.ctypes.data_as(D)), (D * 1)(out.ctypes.data_as(D)), None, None, 0)
     assert results["after"] == out[0] and results["after"] != results["before"]
+
+
+def test_sdf_server_matches_per_call_launch(golden, gpu_ctx):
+    """The resident SDF server (sdf_row.hip sdf_server_kernel, include/sdfnmpc.h sdfnmpc_ctx_set_sdf_server)
+    returns bitwise what one sdf_row launch per call returns, for 1..16 rows, across networks, and after it
+    left on its idle timeout (the next call relaunches it)."""
+    import time
+    g = golden["sdf"]
+    net0, net1 = _lib.Net.siren(gpu_ctx, 0), _lib.Net.siren(gpu_ctx, 1)
+    cases = [(net0, g["input"][0:1]), (net0, g["input"][5:21]), (net1, g["input"][30:31]), (net0, g["input"][40:43])]
+    gpu_ctx.set_sdf_server(False)
+    want = [net.eval_host(x.astype(np.float64)) for net, x in cases]
+    gpu_ctx.set_sdf_server(True)
+    for _ in range(2):
+        for (net, x), (df, gr) in zip(cases, want):
+            d2, g2 = net.eval_host(x.astype(np.float64))
+            np.testing.assert_array_equal(d2, df)
+            np.testing.assert_array_equal(g2, gr)
+        time.sleep(0.1)  # > the 20 ms idle timeout: the server has left, the next call relaunches it
+    for i in range(200):  # a burst of calls as acados makes them, one node at a time
+        net, x = cases[i % 4]
+        d2, g2 = net.eval_host(x.astype(np.float64))
+        np.testing.assert_array_equal(d2, want[i % 4][0])
+    gpu_ctx.set_sdf_server(False)
