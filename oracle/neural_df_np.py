@@ -1,0 +1,80 @@
+"""TEST INFRASTRUCTURE (the checker, never the product): fp64 numpy restatement of the reference NeuralDF
+for every architecture variant -- df and d df / d pos.
+
+It follows, line for line in meaning:
+  * PositionEmbedding.forward  sdf_nmpc/utils/embeddings.py:106-111  (e = [x, sin(xb), sin(xb + pi/2)],
+    xb direction-major / frequency-minor; embed 'none' is the identity, neural_df.py:50-52)
+  * NeuralDF.forward           sdf_nmpc/network/neural_df.py:91-103   (res 'full' | 'state' | 'latent' decides
+    what layer 3 sees besides h2, :97-100; dropout is the identity in eval mode)
+  * activations                neural_df.py:40-47 (Sine(w0) activation.py:12-13, torch ReLU, torch Softplus
+    with beta 1 and threshold 20)
+and the reverse-mode derivative torch's autograd takes through them.  The weights are fp32 values used in
+fp64; the embedding directions are weights.embedding_dirs (pinned to the reference's own buffers by
+tests/golden/variants_golden.npz).  Pinned to the reference's fp64 outputs on the same inputs
+(tests/test_oracle.py::test_neural_df_np_matches_reference_variants).
+"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import sdf_nmpc_amd  # noqa: E402,F401
+from sdf_nmpc_amd import weights as W  # noqa: E402
+
+
+def _act(spec, a):
+    """(act(a), act'(a)) of the spec's activation (neural_df.py:40-47)."""
+    if spec.act == "sin":
+        return np.sin(spec.w0 * a), spec.w0 * np.cos(spec.w0 * a)
+    if spec.act == "relu":
+        return np.maximum(a, 0.0), (a > 0.0).astype(a.dtype)
+    ez = np.exp(np.minimum(a, 20.0))
+    return np.where(a > 20.0, a, np.log1p(ez)), np.where(a > 20.0, 1.0, ez / (ez + 1.0))
+
+
+def forward_grad(spec, params, inp):
+    """inp [n, 3 + L] -> (df [n], d df / d pos [n, 3]) in fp64."""
+    x = np.asarray(inp, dtype=np.float64)
+    pos, z = x[:, :3], x[:, 3:]
+    p = {k: np.asarray(v, dtype=np.float64) for k, v in params.items()}
+    W1, b1 = p["layers.main1.0.weight"], p["layers.main1.0.bias"]
+    W2, b2 = p["layers.main1.3.weight"], p["layers.main1.3.bias"]
+    W3, b3 = p["layers.main2.0.weight"], p["layers.main2.0.bias"]
+    W4, b4 = p["layers.main2.3.weight"], p["layers.main2.3.bias"]
+    W5, b5 = p["layers.df.0.weight"], p["layers.df.0.bias"]
+    dirs = W.embedding_dirs(spec.embed).astype(np.float64)
+    nd = dirs.shape[1]
+    if nd:
+        freqs = (2.0 ** np.linspace(0, spec.nb_freqs - 1, spec.nb_freqs)).astype(np.float32).astype(np.float64)
+        proj = pos @ dirs                                        # [n, nd]
+        xb = (proj[..., None] * freqs).reshape(len(x), -1)       # [n, nd * nf], direction-major
+        dxb = (dirs[:, :, None] * freqs).reshape(3, -1)          # d xb / d pos [3, nb]
+        e = np.concatenate([pos, np.sin(xb), np.sin(xb + 0.5 * np.pi)], 1)
+    else:
+        e = pos
+    E = e.shape[1]
+    n2 = W2.shape[0]
+    a1 = np.concatenate([e, z], 1) @ W1.T + b1
+    h1, d1 = _act(spec, a1)
+    a2 = h1 @ W2.T + b2
+    h2, d2 = _act(spec, a2)
+    parts = [h2] + ([e] if spec.res in ("full", "state") else []) + ([z] if spec.res in ("full", "latent") else [])
+    a3 = np.concatenate(parts, 1) @ W3.T + b3
+    h3, d3 = _act(spec, a3)
+    a4 = h3 @ W4.T + b4
+    h4, d4 = _act(spec, a4)
+    df = (h4 @ W5.T + b5)[:, 0]
+    g4 = W5[0] * d4
+    g3 = (g4 @ W4) * d3
+    gx3 = g3 @ W3
+    ge = gx3[:, n2:n2 + E] if spec.res in ("full", "state") else np.zeros_like(e)
+    g2 = gx3[:, :n2] * d2
+    g1 = (g2 @ W2) * d1
+    ge = ge + (g1 @ W1)[:, :E]
+    grad = ge[:, :3].copy()
+    if nd:
+        nb = xb.shape[1]
+        gs = ge[:, 3:3 + nb] * np.cos(xb) + ge[:, 3 + nb:3 + 2 * nb] * np.cos(xb + 0.5 * np.pi)
+        grad += gs @ dxb.T
+    return df, grad

@@ -395,10 +395,15 @@ namespace {
 
 struct HostNet {
     int nb_states = 3, L = 0, n1 = 0, n2 = 0, n3 = 0, n4 = 0, nf = 0, nd = 0;
+    int res = 0;  // 0 'full' [h2 | e | z], 1 'state' [h2 | e], 2 'latent' [h2 | z] into layer 3 (neural_df.py:76-78)
+    int act = 0;  // 0 sin(w0 .), 1 relu, 2 softplus (neural_df.py:40-47)
     float w0 = 0, max_df = 1;
     std::vector<float> dirs, freqs;                           // [3][nd], [nf]
     std::vector<float> W1, b1, W2, b2, W3, b3, W4, b4, W5, b5;  // torch order / shapes
     int E() const { return 3 + 2 * nd * nf; }
+    bool e3() const { return res != 2; }  // layer 3 sees the embedding
+    bool z3() const { return res != 1; }  // layer 3 sees the latent
+    int c3() const { return n2 + (e3() ? E() : 0) + (z3() ? L : 0); }  // W3 row length
 };
 
 uint64_t mix64(uint64_t z) {
@@ -419,7 +424,7 @@ std::vector<float*> param_list(HostNet& h) {
 }
 std::vector<std::pair<int, int>> param_shapes(const HostNet& h) {
     const int E = h.E(), L = h.L;
-    return {{h.n1, E + L}, {h.n1, 1}, {h.n2, h.n1}, {h.n2, 1}, {h.n3, h.n2 + E + L},
+    return {{h.n1, E + L}, {h.n1, 1}, {h.n2, h.n1}, {h.n2, 1}, {h.n3, h.c3()},
             {h.n3, 1},     {h.n4, h.n3}, {h.n4, 1}, {1, h.n4}, {1, 1}};
 }
 void alloc_params(HostNet& h) {
@@ -428,37 +433,49 @@ void alloc_params(HostNet& h) {
     for (size_t i = 0; i < v.size(); ++i) v[i]->assign((size_t)sh[i].first * sh[i].second, 0.0f);
 }
 
-// wide networks (every layer a multiple of 128, e.g. config C5's [1024,1024,512,256]) run the
-// layer-by-layer GEMM schedule of sdf_wide.hip; the deployed [256,256,128,64] the fused sdf_mlp.hip
-bool is_wide(const HostNet& h) {
-    return !(h.n1 == N1 && h.n2 == N2 && h.n3 == N3 && h.n4 == N4) && h.n1 % 128 == 0 && h.n2 % 128 == 0 &&
-           h.n3 % 128 == 0 && h.n4 % 128 == 0;
+// The deployed NeuralDF (layers [256,256,128,64], 'oct' x 5 frequencies, res 'full', sin) runs the fused
+// sdf_mlp.hip / sdf_row.hip kernels.  Every other architecture -- config C5's [1024,1024,512,256], and the
+// reference's variants: any layer sizes (zero-padded to multiples of 128: the padded units' outgoing
+// weights are zero, so they change nothing), embeddings none / pos / cube / oct / dod / ico with any
+// frequency count, res full / state / latent, activations sin / relu / softplus -- runs the layer-by-layer
+// GEMM schedule of sdf_wide.hip ("wide" below means exactly that: not the deployed net).
+bool is_deployed(const HostNet& h) {
+    return h.n1 == N1 && h.n2 == N2 && h.n3 == N3 && h.n4 == N4 && h.nd == EMB_ND && h.nf == EMB_NF && h.res == 0 &&
+           h.act == 0 && h.L == L;
 }
+bool is_wide(const HostNet& h) { return !is_deployed(h); }
+int pad128(int n) { return (n + 127) / 128 * 128; }
 
 int check_supported(const HostNet& h) {
-    const bool arch_ok = (h.n1 == N1 && h.n2 == N2 && h.n3 == N3 && h.n4 == N4) || is_wide(h);
-    if (h.nb_states != 3 || h.L != L || !arch_ok || h.nd != EMB_ND || h.nf != EMB_NF) {
+    if (h.nb_states != 3 || h.L != L || h.E() > 256 || h.res < 0 || h.res > 2 || h.act < 0 || h.act > 2) {
         char buf[256];
         snprintf(buf, sizeof buf,
-                 "network architecture (states %d, latent %d, layers [%d,%d,%d,%d], dirs %d, freqs %d) is not "
-                 "built for; this build supports latent 128, 'oct' embedding, 5 freqs and layers [256,256,128,64] or "
-                 "all multiples of 128 (e.g. [1024,1024,512,256])",
-                 h.nb_states, h.L, h.n1, h.n2, h.n3, h.n4, h.nd, h.nf);
+                 "network architecture (states %d, latent %d, embedding features %d, res %d, act %d) is not built "
+                 "for; this build supports 3 states, latent 128, at most 256 embedding features",
+                 h.nb_states, h.L, h.E(), h.res, h.act);
         return fail(SDFNMPC_E_UNSUPPORTED, buf);
     }
     return SDFNMPC_OK;
 }
 
 int parse_sdfw(const void* blob, size_t bytes, HostNet& h) {
+    // version 1: magic, version, nb_states, L, n1..n4, nb_freqs, n_dirs, res (0), w0, max_df;
+    // version 2 adds the activation after res (sdf_nmpc_amd/weights.py)
     const unsigned char* p = (const unsigned char*)blob;
-    const size_t HDR = 8 + 10 * 4 + 2 * 4;
-    if (!blob || bytes < HDR || memcmp(p, "SDFNMPCW", 8) != 0) return fail(SDFNMPC_E_FORMAT, "not an .sdfw blob");
-    uint32_t u[10];
-    memcpy(u, p + 8, sizeof u);
+    if (!blob || bytes < 12 || memcmp(p, "SDFNMPCW", 8) != 0) return fail(SDFNMPC_E_FORMAT, "not an .sdfw blob");
+    uint32_t ver = 0;
+    memcpy(&ver, p + 8, 4);
+    if (ver != 1 && ver != 2) return fail(SDFNMPC_E_FORMAT, "unsupported .sdfw version");
+    const int nu = ver == 1 ? 10 : 11;
+    const size_t HDR = 8 + nu * 4 + 2 * 4;
+    if (bytes < HDR) return fail(SDFNMPC_E_FORMAT, "truncated .sdfw header");
+    uint32_t u[11] = {};
+    memcpy(u, p + 8, (size_t)nu * 4);
     float f[2];
-    memcpy(f, p + 48, sizeof f);
-    if (u[0] != 1) return fail(SDFNMPC_E_FORMAT, "unsupported .sdfw version");
-    if (u[9] != 0) return fail(SDFNMPC_E_UNSUPPORTED, "only res='full' networks are supported");
+    memcpy(f, p + 8 + nu * 4, sizeof f);
+    if (ver == 1 && u[9] != 0) return fail(SDFNMPC_E_FORMAT, "version-1 .sdfw blobs are res='full'");
+    h.res = (int)u[9];
+    h.act = ver == 2 ? (int)u[10] : 0;
     h.nb_states = (int)u[1];
     h.L = (int)u[2];
     h.n1 = (int)u[3]; h.n2 = (int)u[4]; h.n3 = (int)u[5]; h.n4 = (int)u[6];
@@ -466,7 +483,8 @@ int parse_sdfw(const void* blob, size_t bytes, HostNet& h) {
     h.nd = (int)u[8];
     h.w0 = f[0];
     h.max_df = f[1];
-    if (h.nd <= 0 || h.nf <= 0 || h.nd > 64 || h.nf > 64 || h.L < 0 || h.n1 <= 0 || h.n2 <= 0 || h.n3 <= 0 || h.n4 <= 0)
+    if (h.nd < 0 || h.nf < 0 || h.nd > 64 || h.nf > 64 || (h.nd == 0) != (h.nf == 0) || h.L < 0 || h.n1 <= 0 ||
+        h.n2 <= 0 || h.n3 <= 0 || h.n4 <= 0 || h.n1 > 65536 || h.n2 > 65536 || h.n3 > 65536 || h.n4 > 65536)
         return fail(SDFNMPC_E_FORMAT, "bad .sdfw header");
     size_t off = HDR;
     auto take = [&](std::vector<float>& v, size_t n) -> bool {
@@ -535,6 +553,11 @@ struct WideDev {  // plain row-major [N][K] fp32 operands of the wide schedule (
     const float *B4 = nullptr, *B3h = nullptr, *B3e = nullptr, *B2 = nullptr, *B1e = nullptr;
     const float *Hz = nullptr, *bz = nullptr, *b2 = nullptr, *b4 = nullptr, *w5 = nullptr;
     const float4* emb_tab = nullptr;
+    int P1 = 0, P2 = 0, P3 = 0, P4 = 0;  // layer widths padded to multiples of 128
+    int NEK = NE, NEB = 128;             // embedding width as a K segment / as the d e GEMMs' output
+    int nb = 0;                          // projected frequencies (n_dirs x nb_freqs)
+    bool e3 = true;                      // layer 3 sees the embedding (res 'full' / 'state')
+    int act = 0;                         // 0 sin, 1 relu, 2 softplus
 };
 
 struct sdfnmpc_net {
@@ -557,15 +580,18 @@ struct sdfnmpc_net {
     }
 };
 
-static void emb_table(const HostNet& h, std::vector<float>& blob) {
-    for (int m = 0; m < NE; ++m) {
+// [width] float4 (dir * 2^f, 0) of embedding feature m: the projected frequencies in the reference's order
+// (embeddings.py:108-109: direction-major, frequency-minor; the sin half, then the same for the shifted half)
+static void emb_table(const HostNet& h, std::vector<float>& blob, int width = NE) {
+    const int nb = h.nd * h.nf, E = h.E();
+    for (int m = 0; m < width; ++m) {
         float v[4] = {0, 0, 0, 0};
         int j = -1;
-        if (m >= 3 && m < 3 + EMB_NB) j = m - 3;
-        else if (m >= 3 + EMB_NB && m < E) j = m - 3 - EMB_NB;
+        if (m >= 3 && m < 3 + nb) j = m - 3;
+        else if (m >= 3 + nb && m < E) j = m - 3 - nb;
         if (j >= 0) {
-            const int d = j / EMB_NF, f = j % EMB_NF;
-            for (int c = 0; c < 3; ++c) v[c] = h.dirs[c * EMB_ND + d] * h.freqs[f];  // freq = 2^f: exact
+            const int d = j / h.nf, f = j % h.nf;
+            for (int c = 0; c < 3; ++c) v[c] = h.dirs[c * h.nd + d] * h.freqs[f];  // freq = 2^f: exact
         }
         blob.insert(blob.end(), v, v + 4);
     }
@@ -584,7 +610,13 @@ static uint64_t net_fingerprint(HostNet& h) {  // FNV-1a over the parameters in 
 }
 
 static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
-    const int n1 = h.n1, n2 = h.n2, n3 = h.n3, n4 = h.n4, c1 = E + L, c3 = n2 + E + L;
+    // layer widths zero-padded to multiples of 128 (the GEMM's column tile), the embedding to NEK (a
+    // multiple of 32) as a K segment and to NEB (a multiple of 128) as the d e GEMMs' output width
+    const int n1 = h.n1, n2 = h.n2, n3 = h.n3, n4 = h.n4, E = h.E(), c1 = E + L, c3 = h.c3();
+    const int P1 = pad128(n1), P2 = pad128(n2), P3 = pad128(n3), P4 = pad128(n4);
+    const int NEK = std::max(96, (E + 31) / 32 * 32), NEB = pad128(E);
+    const bool e3 = h.e3(), z3 = h.z3();
+    const int z3off = n2 + (e3 ? E : 0);  // first latent column of W3
     const float *W1 = h.W1.data(), *W2 = h.W2.data(), *W3 = h.W3.data(), *W4 = h.W4.data();
     std::vector<float> blob;
     std::vector<size_t> off;
@@ -593,30 +625,39 @@ static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
         for (int j = 0; j < N; ++j)
             for (int k = 0; k < K; ++k) blob.push_back(f(j, k));
     };
-    mat(n1, NE, [&](int j, int k) { return k < E ? W1[(size_t)j * c1 + k] : 0.0f; });                      // F1
-    mat(n2, n1, [&](int j, int k) { return W2[(size_t)j * n1 + k]; });                                      // F2
-    mat(n3, n2 + NE, [&](int j, int k) { return k < n2 + E ? W3[(size_t)j * c3 + k] : 0.0f; });            // F3
-    mat(n4, n3, [&](int j, int k) { return W4[(size_t)j * n3 + k]; });                                      // F4
-    mat(n3, n4, [&](int j, int k) { return W4[(size_t)k * n3 + j]; });                                      // B4
-    mat(n2, n3, [&](int j, int k) { return W3[(size_t)k * c3 + j]; });                                      // B3h
-    mat(128, n3, [&](int j, int k) { return j < E ? W3[(size_t)k * c3 + n2 + j] : 0.0f; });                 // B3e
-    mat(n1, n2, [&](int j, int k) { return W2[(size_t)k * n1 + j]; });                                      // B2
-    mat(128, n1, [&](int j, int k) { return j < E ? W1[(size_t)k * c1 + j] : 0.0f; });                      // B1e
-    mat(n1 + n3, L, [&](int j, int k) {                                                                     // Hz
-        return j < n1 ? W1[(size_t)j * c1 + E + k] : W3[(size_t)(j - n1) * c3 + n2 + E + k];
+    auto vec = [&](const std::vector<float>& v, int P) {
+        off.push_back(blob.size());
+        blob.insert(blob.end(), v.begin(), v.end());
+        blob.insert(blob.end(), (size_t)(P - (int)v.size()), 0.0f);
+    };
+    mat(P1, NEK, [&](int j, int k) { return j < n1 && k < E ? W1[(size_t)j * c1 + k] : 0.0f; });                // F1
+    mat(P2, P1, [&](int j, int k) { return j < n2 && k < n1 ? W2[(size_t)j * n1 + k] : 0.0f; });                 // F2
+    mat(P3, P2 + (e3 ? NEK : 0), [&](int j, int k) {                                                             // F3
+        if (j >= n3) return 0.0f;
+        if (k < P2) return k < n2 ? W3[(size_t)j * c3 + k] : 0.0f;
+        return k - P2 < E ? W3[(size_t)j * c3 + n2 + (k - P2)] : 0.0f;
     });
-    off.push_back(blob.size());  // bz
+    mat(P4, P3, [&](int j, int k) { return j < n4 && k < n3 ? W4[(size_t)j * n3 + k] : 0.0f; });                 // F4
+    mat(P3, P4, [&](int j, int k) { return j < n3 && k < n4 ? W4[(size_t)k * n3 + j] : 0.0f; });                 // B4
+    mat(P2, P3, [&](int j, int k) { return j < n2 && k < n3 ? W3[(size_t)k * c3 + j] : 0.0f; });                 // B3h
+    mat(NEB, P3, [&](int j, int k) { return e3 && j < E && k < n3 ? W3[(size_t)k * c3 + n2 + j] : 0.0f; });      // B3e
+    mat(P1, P2, [&](int j, int k) { return j < n1 && k < n2 ? W2[(size_t)k * n1 + j] : 0.0f; });                 // B2
+    mat(NEB, P1, [&](int j, int k) { return j < E && k < n1 ? W1[(size_t)k * c1 + j] : 0.0f; });                 // B1e
+    mat(P1 + P3, L, [&](int j, int k) {                                                                          // Hz
+        if (j < P1) return j < n1 ? W1[(size_t)j * c1 + E + k] : 0.0f;
+        return z3 && j - P1 < n3 ? W3[(size_t)(j - P1) * c3 + z3off + k] : 0.0f;
+    });
+    off.push_back(blob.size());  // bz = [b1 | b3], padded
     blob.insert(blob.end(), h.b1.begin(), h.b1.end());
+    blob.insert(blob.end(), (size_t)(P1 - n1), 0.0f);
     blob.insert(blob.end(), h.b3.begin(), h.b3.end());
-    off.push_back(blob.size());
-    blob.insert(blob.end(), h.b2.begin(), h.b2.end());
-    off.push_back(blob.size());
-    blob.insert(blob.end(), h.b4.begin(), h.b4.end());
-    off.push_back(blob.size());
-    blob.insert(blob.end(), h.W5.begin(), h.W5.end());
+    blob.insert(blob.end(), (size_t)(P3 - n3), 0.0f);
+    vec(h.b2, P2);
+    vec(h.b4, P4);
+    vec(h.W5, P4);
     while (blob.size() % 4) blob.push_back(0.0f);
     off.push_back(blob.size());
-    emb_table(h, blob);
+    emb_table(h, blob, NEK);
     for (size_t o : off)
         if (o % 4) return fail(SDFNMPC_E_FORMAT, "internal: misaligned wide operand");
     auto* net = new sdfnmpc_net();
@@ -636,6 +677,8 @@ static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     w.B4 = d + off[i++]; w.B3h = d + off[i++]; w.B3e = d + off[i++]; w.B2 = d + off[i++]; w.B1e = d + off[i++];
     w.Hz = d + off[i++]; w.bz = d + off[i++]; w.b2 = d + off[i++]; w.b4 = d + off[i++]; w.w5 = d + off[i++];
     w.emb_tab = (const float4*)(d + off[i++]);
+    w.P1 = P1; w.P2 = P2; w.P3 = P3; w.P4 = P4; w.NEK = NEK; w.NEB = NEB;
+    w.nb = h.nd * h.nf; w.e3 = e3; w.act = h.act;
     net->args.b5 = h.b5[0];
     net->args.w0 = h.w0;
     net->fingerprint = net_fingerprint(h);
@@ -833,18 +876,18 @@ static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, co
                     const double* zd, long long zstride, int n_inst, int rows_per_inst, float4* out4,
                     const SdfArgs* cons) {
     if (rows > 0x7fffffffLL / 2) return fail(SDFNMPC_E_ARG, "too many rows");
-    const HostNet& hn = net->host;
     const WideDev& w = net->wd;
-    const int n1 = hn.n1, n2 = hn.n2, n3 = hn.n3, n4 = hn.n4, nz = n1 + n3, R = (int)rows;
-    const size_t per_row = 2 * NE + 2 * (size_t)(n1 + n2 + n3 + n4) + 2 * 128;
+    const int n1 = w.P1, n2 = w.P2, n3 = w.P3, n4 = w.P4, nz = n1 + n3, R = (int)rows;
+    const int NEK = w.NEK, NEB = w.NEB;
+    const size_t per_row = 2 * (size_t)NEK + 2 * (size_t)(n1 + n2 + n3 + n4) + 2 * (size_t)NEB;
     const size_t nfl = per_row * rows + (size_t)n_inst * (L + nz);
     HIPCHK(ctx->wws.ensure(nfl * sizeof(float)));
     float* q = (float*)ctx->wws.p;
     auto take = [&](size_t n) { float* r = q; q += n; return r; };
-    float *Eb = take((size_t)R * NE), *Gb = take((size_t)R * NE);
+    float *Eb = take((size_t)R * NEK), *Gb = take((size_t)R * NEK);
     float *H1 = take((size_t)R * n1), *D1 = take((size_t)R * n1), *H2 = take((size_t)R * n2), *D2 = take((size_t)R * n2);
     float *H3 = take((size_t)R * n3), *D3 = take((size_t)R * n3), *H4 = take((size_t)R * n4), *D4 = take((size_t)R * n4);
-    float *GE3 = take((size_t)R * 128), *GE1 = take((size_t)R * 128);
+    float *GE3 = take((size_t)R * NEB), *GE1 = take((size_t)R * NEB);
     float* z = take((size_t)n_inst * L);
     float* c13 = take((size_t)n_inst * nz);
     hipStream_t st = ctx->stream;
@@ -862,27 +905,32 @@ static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, co
         g.W = W; g.M = M; g.N = N;
         g.bias = bias; g.c = c; g.ldc = nz; g.rows_per_inst = rows_per_inst;
         g.d = d; g.ldd = ldd; g.w5 = w.w5;
-        g.out1 = o1; g.ld1 = N; g.out2 = o2; g.ld2 = N; g.w0 = w0;
+        g.out1 = o1; g.ld1 = N; g.out2 = o2; g.ld2 = N; g.w0 = w0; g.act = w.act;
         return timed(ctx, name, [&] { return launch_wide_gemm(g, epi, st); });
     };
     HIPCHK(gemm(zf, L, nullptr, 0, w.Hz, n_inst, nz, WIDE_EPI_STORE, w.bz, nullptr, nullptr, 0, c13, nullptr,
                 "sdf_wide_hoist"));
     WideSdfArgs ea{};
     ea.rows = R; ea.n4 = n4; ea.pos = pos4; ea.emb_tab = w.emb_tab; ea.E = Eb; ea.G = Gb;
+    ea.nb = w.nb; ea.nek = NEK; ea.neb = NEB;
     if (cons) { ea.x = cons->x; ea.p = cons->p; ea.np = cons->np; ea.h = cons->h; ea.Jh = cons->Jh; ea.max_df = cons->max_df; }
     HIPCHK(timed(ctx, "sdf_wide_emb", [&] { return launch_wide_emb(ea, st); }));
-    // forward: L1..L4
-    HIPCHK(gemm(Eb, NE, nullptr, 0, w.F1, R, n1, WIDE_EPI_SIN, nullptr, c13, nullptr, 0, H1, D1, "sdf_wide_gemm"));
+    // forward: L1..L4 (layer 3 sees [h2 | e] for res full / state; its latent part is in c13)
+    HIPCHK(gemm(Eb, NEK, nullptr, 0, w.F1, R, n1, WIDE_EPI_SIN, nullptr, c13, nullptr, 0, H1, D1, "sdf_wide_gemm"));
     HIPCHK(gemm(H1, n1, nullptr, 0, w.F2, R, n2, WIDE_EPI_SIN, w.b2, nullptr, nullptr, 0, H2, D2, "sdf_wide_gemm"));
-    HIPCHK(gemm(H2, n2, Eb, NE, w.F3, R, n3, WIDE_EPI_SIN, nullptr, c13 + n1, nullptr, 0, H3, D3, "sdf_wide_gemm"));
+    HIPCHK(gemm(H2, n2, w.e3 ? Eb : nullptr, w.e3 ? NEK : 0, w.F3, R, n3, WIDE_EPI_SIN, nullptr, c13 + n1, nullptr, 0,
+                H3, D3, "sdf_wide_gemm"));
     HIPCHK(gemm(H3, n3, nullptr, 0, w.F4, R, n4, WIDE_EPI_SIN_L4, w.b4, nullptr, nullptr, 0, H4, D4, "sdf_wide_gemm"));
     // backward (deltas overwrite the consumed activations): delta3 -> H3, delta2 -> H2, delta1 -> H1
     HIPCHK(gemm(D4, n4, nullptr, 0, w.B4, R, n3, WIDE_EPI_BWD, nullptr, nullptr, D3, n3, H3, nullptr, "sdf_wide_gemm"));
     HIPCHK(gemm(H3, n3, nullptr, 0, w.B3h, R, n2, WIDE_EPI_BWD, nullptr, nullptr, D2, n2, H2, nullptr, "sdf_wide_gemm"));
-    HIPCHK(gemm(H3, n3, nullptr, 0, w.B3e, R, 128, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, GE3, nullptr,
-                "sdf_wide_gemm"));
+    if (w.e3)
+        HIPCHK(gemm(H3, n3, nullptr, 0, w.B3e, R, NEB, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, GE3, nullptr,
+                    "sdf_wide_gemm"));
+    else  // res 'latent': layer 3 does not see the embedding
+        HIPCHK(hipMemsetAsync(GE3, 0, (size_t)R * NEB * sizeof(float), st));
     HIPCHK(gemm(H2, n2, nullptr, 0, w.B2, R, n1, WIDE_EPI_BWD, nullptr, nullptr, D1, n1, H1, nullptr, "sdf_wide_gemm"));
-    HIPCHK(gemm(H1, n1, nullptr, 0, w.B1e, R, 128, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, GE1, nullptr,
+    HIPCHK(gemm(H1, n1, nullptr, 0, w.B1e, R, NEB, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, GE1, nullptr,
                 "sdf_wide_gemm"));
     ea.H4 = H4; ea.GE3 = GE3; ea.GE1 = GE1; ea.w5 = w.w5; ea.b5 = net->args.b5; ea.out = out4;
     HIPCHK(timed(ctx, "sdf_wide_final", [&] { return launch_wide_final(ea, st); }));

@@ -136,18 +136,20 @@ struct WideGemmArgs {
     const float* d; int ldd;         // BWD: cos(w0 a) of the layer
     const float* w5;                 // SIN_L4: final-layer weights
     float* out1; int ld1;            // SIN: sin(w0 a) | BWD: ((acc * d) * w0) | STORE: acc + bias
-    float* out2; int ld2;            // SIN: cos(w0 a) | SIN_L4: (w5 * cos(w0 a)) * w0
+    float* out2; int ld2;            // SIN: cos(w0 a) | SIN_L4: (w5 * cos(w0 a)) * w0  (act' for relu / softplus)
     float w0;
+    int act;                         // 0 sin(w0 .), 1 relu, 2 softplus (neural_df.py:40-47)
 };
 
 struct WideSdfArgs {
     int rows, n4, np;
+    int nb, nek, neb;                 // projected frequencies; E / G row stride; GE3 / GE1 row stride
     const double* x; const double* p;  // Co_p_B from the iterate (or pos when x == NULL)
     const float4* pos;
     const float4* emb_tab;
-    float* E; float* G;               // [rows][NE]
+    float* E; float* G;               // [rows][nek]
     const float* H4;                  // [rows][n4]
-    const float* GE3; const float* GE1;  // [rows][128]
+    const float* GE3; const float* GE1;  // [rows][neb]
     const float* w5; float b5;
     float4* out;                      // [rows] (df, d df / d pos) or NULL
     double* h; double* Jh; double max_df;

@@ -63,6 +63,9 @@ __device__ __forceinline__ void gemm(f32x16 (&acc)[RB][NCB], const float* lds, i
     constexpr int PF = (NG < SDF_PF) ? NG : SDF_PF;
     static_assert(0 <= G0 && G0 < G1 && G1 <= G, "group range");
     static_assert(K % 8 == 0, "K must be a multiple of 8");
+#ifdef SDF_PRIO_GEMM  // diagnostic: raise the wave's issue priority over its matrix phase
+    __builtin_amdgcn_s_setprio(2);
+#endif
     const int r = lane & 31, h = lane >> 5;
     const float* abase = lds + r * stride + h * (K / 2);
     const float4* bbase = wpk + (size_t)cb0 * G * 64 + lane;
@@ -106,6 +109,9 @@ __device__ __forceinline__ void gemm(f32x16 (&acc)[RB][NCB], const float* lds, i
             for (int rb = 0; rb < RB; ++rb) a[rb] = an[rb];
         }
     }
+#ifdef SDF_PRIO_GEMM
+    __builtin_amdgcn_s_setprio(0);
+#endif
 }
 
 template <int RB, int NCB>

@@ -7,9 +7,13 @@
 // from L2 once per group of 8 row tiles:
 //   wide_latent  z (fp64 stage parameters) -> fp32 [n_inst][L]
 //   wide_gemm    hoist  c13 = z [W1z | W3z]^T + [b1 | b3]            (per instance)
-//   wide_emb     Co_p_B (fp64 -> fp32), e [R][96], d e / d xb factors g [R][96]
-//   wide_gemm    L1..L4 forward: sin(w0 (A W^T + bias / c13)), keeping cos(w0 a) for the backward pass
-//   wide_gemm    backward: delta_{l-1} = ((delta_l W_l) * cos) * w0, d e = delta3 W3e + delta1 W1e
+//   wide_emb     Co_p_B (fp64 -> fp32), e [R][nek], d e / d xb factors g [R][nek]
+//   wide_gemm    L1..L4 forward: act(A W^T + bias / c13) -- sin(w0 .), relu or softplus -- keeping act'
+//                for the backward pass
+//   wide_gemm    backward: delta_{l-1} = (delta_l W_l) * act' (* w0 for sin), d e = delta3 W3e + delta1 W1e
+// The same schedule serves every NeuralDF other than the deployed one (engine.cpp is_deployed): layer
+// widths zero-padded to multiples of 128, any embedding (none / pos / cube / oct / dod / ico), res
+// full / state / latent (neural_df.py:40-103).
 //   wide_final   df = w5 h4 + b5, d df / d pos from d e, and the fused sdf constraint row h[2], J_h
 // wide_gemm is an fp32 MFMA (v_mfma_f32_32x32x2_f32, exact fp32 products) GEMM: 128 x 128 tile per
 // 256-thread workgroup (2 x 2 waves of 64 x 64), K staged 16 at a time through double-buffered LDS
@@ -135,16 +139,27 @@ __global__ __launch_bounds__(256) void wide_gemm_kernel(WideGemmArgs a) {
             if (m >= a.M) break;
             const float v = T[row * 33 + lr];
             if constexpr (EPI == WIDE_EPI_BWD) {
-                // torch's SinBackward then MulBackward: (delta_h * cos(t)) * w0
-                a.out1[(size_t)m * a.ld1 + n] = (v * a.d[(size_t)m * a.ldd + n]) * a.w0;
+                // torch's SinBackward then MulBackward: (delta_h * cos(t)) * w0; relu / softplus: delta_h * act'(t)
+                const float dd = v * a.d[(size_t)m * a.ldd + n];
+                a.out1[(size_t)m * a.ld1 + n] = a.act == 0 ? dd * a.w0 : dd;
             } else if constexpr (EPI == WIDE_EPI_STORE) {
                 a.out1[(size_t)m * a.ld1 + n] = v + bias;
             } else {
                 const float c0 = a.c ? a.c[(size_t)(m / a.rows_per_inst) * a.ldc + n] : bias;
-                float sn, co;
-                sdfn_sincosf(a.w0 * (v + c0), &sn, &co);
-                a.out1[(size_t)m * a.ld1 + n] = sn;
-                a.out2[(size_t)m * a.ld2 + n] = (EPI == WIDE_EPI_SIN_L4) ? (w5 * co) * a.w0 : co;
+                const float t = v + c0;
+                float hv, dv;
+                if (a.act == 0) {
+                    sdfn_sincosf(a.w0 * t, &hv, &dv);
+                } else if (a.act == 1) {  // torch ReLU; ReluBackward passes where the output is > 0
+                    hv = t > 0.0f ? t : 0.0f;
+                    dv = hv > 0.0f ? 1.0f : 0.0f;
+                } else {  // torch Softplus(beta 1, threshold 20) and SoftplusBackward: z / (z + 1), z = exp(t)
+                    const float ez = expf(t);
+                    hv = t > 20.0f ? t : log1pf(ez);
+                    dv = t > 20.0f ? 1.0f : ez / (ez + 1.0f);
+                }
+                a.out1[(size_t)m * a.ld1 + n] = hv;
+                a.out2[(size_t)m * a.ld2 + n] = (EPI == WIDE_EPI_SIN_L4) ? (a.act == 0 ? (w5 * dv) * a.w0 : w5 * dv) : dv;
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -179,12 +194,14 @@ __global__ void wide_latent_kernel(const double* lat, long long stride, int n_in
     z[i] = (float)lat[inst * stride + k];
 }
 
-// positional embedding e (embeddings.py:106-111) and its derivative factors, 96 features per row
-// (m < 3: pos, then sin(xb), sin(xb + pi/2), zero pad) -- the same arithmetic as sdf_mlp.hip
+// positional embedding e (embeddings.py:106-111) and its derivative factors, nek features per row
+// (m < 3: pos, then sin(xb), sin(xb + pi/2) over the nb projected frequencies, zero pad; embed 'none':
+// nb = 0) -- the same arithmetic as sdf_mlp.hip
 __global__ __launch_bounds__(256) void wide_emb_kernel(WideSdfArgs a) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (long long)a.rows * NE) return;
-    const int r = (int)(i / NE), m = (int)(i - (long long)r * NE);
+    const int NEK = a.nek, NB = a.nb;
+    if (i >= (long long)a.rows * NEK) return;
+    const int r = (int)(i / NEK), m = (int)(i - (long long)r * NEK);
     float px, py, pz;
     if (a.x) {  // Co_p_B = W_R_Co^T (W_p_B - W_p_Co) in fp64, handed over as fp32 (gen_model.py:46-51)
         const double* xr = a.x + (size_t)r * 10;
@@ -202,10 +219,10 @@ __global__ __launch_bounds__(256) void wide_emb_kernel(WideSdfArgs a) {
     if (m < 3) {
         e = (m == 0) ? px : (m == 1 ? py : pz);
         g = 1.0f;
-    } else if (m < 3 + 2 * EMB_NB) {
+    } else if (m < 3 + 2 * NB) {
         const float4 t = a.emb_tab[m];
         float xb = px * t.x + py * t.y + pz * t.z;
-        if (m >= 3 + EMB_NB) xb = xb + 1.57079637050628662109375f;
+        if (m >= 3 + NB) xb = xb + 1.57079637050628662109375f;
         float s, c;
         sdfn_sincosf(xb, &s, &c);
         e = s;
@@ -214,8 +231,8 @@ __global__ __launch_bounds__(256) void wide_emb_kernel(WideSdfArgs a) {
         e = 0.0f;
         g = 0.0f;
     }
-    a.E[(size_t)r * NE + m] = e;
-    a.G[(size_t)r * NE + m] = g;
+    a.E[(size_t)r * NEK + m] = e;
+    a.G[(size_t)r * NEK + m] = g;
 }
 
 // df, d df / d pos and the constraint epilogue, one thread per row (sequential sums: deterministic)
@@ -226,11 +243,11 @@ __global__ __launch_bounds__(256) void wide_final_kernel(WideSdfArgs a) {
     float acc = 0.0f;
     for (int n = 0; n < a.n4; ++n) acc += a.w5[n] * h4[n];
     const float df = acc + a.b5;
-    const float* ge3 = a.GE3 + (size_t)r * 128;
-    const float* ge1 = a.GE1 + (size_t)r * 128;
-    const float* gg = a.G + (size_t)r * NE;
+    const float* ge3 = a.GE3 + (size_t)r * a.neb;
+    const float* ge1 = a.GE1 + (size_t)r * a.neb;
+    const float* gg = a.G + (size_t)r * a.nek;
     float s0 = 0.f, s1 = 0.f, s2 = 0.f;
-    for (int m = 0; m < NE; ++m) {
+    for (int m = 0; m < a.nek; ++m) {
         const float u = (ge3[m] + ge1[m]) * gg[m];
         if (m < 3) {
             s0 += (m == 0) ? u : 0.0f;
@@ -266,7 +283,7 @@ hipError_t launch_wide_latent(const double* lat, long long stride, int n_inst, f
 
 hipError_t launch_wide_emb(const WideSdfArgs& a, hipStream_t s) {
     if (a.rows <= 0) return hipSuccess;
-    const long long n = (long long)a.rows * NE;
+    const long long n = (long long)a.rows * a.nek;
     hipLaunchKernelGGL(wide_emb_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, a);
     return hipGetLastError();
 }

@@ -25,30 +25,52 @@ from typing import Dict, List, Tuple
 import numpy as np
 
 MAGIC = b"SDFNMPCW"
-VERSION = 1
+VERSION = 1  # res='full', act='sin' networks (every deployed / C5 blob); version 2 adds the activation
 _HDR = struct.Struct("<8s10I2f")  # magic, version, nb_states, L, n1..n4, nb_freqs, n_dirs, res, w0, max_df
+_HDR2 = struct.Struct("<8s11I2f")  # version 2: ... n_dirs, res, act, w0, max_df
+RES_CODES = {"full": 0, "state": 1, "latent": 2}   # neural_df.py:76-78, 97-100
+ACT_CODES = {"sin": 0, "relu": 1, "softplus": 2}   # neural_df.py:40-47
 
 # embedding projection directions, one row per direction (embeddings.py:20-100)
 _OCT = [(-1, -1, -1), (-1, -1, +1), (-1, +1, -1), (-1, +1, +1),
         (+1, -1, -1), (+1, -1, +1), (+1, +1, -1), (+1, +1, +1)]
 _CUBE = [(-1, 0, 0), (+1, 0, 0), (0, -1, 0), (0, +1, 0), (0, 0, -1), (0, 0, +1)]
+_PHI = (1 + np.sqrt(5)) / 2
+_DOD = [(0, -1, -_PHI), (0, +1, -_PHI), (0, -1, +_PHI), (0, +1, +_PHI), (-1, 0, -_PHI), (+1, 0, -_PHI),
+        (-1, 0, +_PHI), (+1, 0, +_PHI), (-1, -_PHI, 0), (+1, -_PHI, 0), (-1, +_PHI, 0), (+1, +_PHI, 0)]
+_H = 1 / _PHI
+_ICO = [(+1, +1, +1), (+1, +1, -1), (+1, -1, +1), (+1, -1, -1), (-1, +1, +1), (-1, +1, -1), (-1, -1, +1),
+        (-1, -1, -1), (0, +_PHI, +_H), (0, +_PHI, -_H), (0, -_PHI, +_H), (0, -_PHI, -_H), (+_H, 0, +_PHI),
+        (+_H, 0, -_PHI), (-_H, 0, +_PHI), (-_H, 0, -_PHI), (+_PHI, +_H, 0), (+_PHI, -_H, 0), (-_PHI, +_H, 0),
+        (-_PHI, -_H, 0)]
+EMBED_BY_DIRS = {0: "none", 3: "pos", 6: "cube", 8: "oct", 12: "dod", 20: "ico"}
 
 
 def embedding_dirs(embed: str) -> np.ndarray:
-    """fp32 [3, n_dirs] projection matrix exactly as torch builds it (embeddings.py:20-51).
+    """fp32 [3, n_dirs] projection matrix exactly as torch builds it (embeddings.py:20-100); 'none' (no
+    embedding, neural_df.py:50-52) has no directions.
 
-    torch normalises each column with ``vector_norm`` in fp32: sqrt of a fp32 sum, then a
-    correctly-rounded fp32 division, which numpy reproduces bit for bit.
+    The reference lists the directions as Python floats and builds an fp32 tensor (each value rounded
+    once), then normalises each column with ``vector_norm`` in fp32: torch accumulates the squares with
+    fused multiply-adds (acc = fma(x, x, acc), one rounding per component -- the dod / ico columns with a
+    zero in the middle tell it from a sum of rounded squares), takes an fp32 sqrt and divides with one
+    rounding; numpy reproduces that bit for bit (fp32 products are exact in fp64).
     """
+    if embed == "none":
+        return np.zeros((3, 0), dtype=np.float32)
     if embed == "pos":
         return np.eye(3, dtype=np.float32)
     if embed == "cube":  # not normalised in the reference (embeddings.py:26-36)
         return np.array(_CUBE, dtype=np.float32).T.copy()
-    if embed == "oct":
-        d = np.array(_OCT, dtype=np.float32).T.copy()
-        n = np.sqrt((d * d).sum(axis=0, dtype=np.float32)).astype(np.float32)
-        return (d / n[None, :]).astype(np.float32)
-    raise ValueError(f"embedding '{embed}' is not supported by this build (supported: oct, pos, cube)")
+    tab = {"oct": _OCT, "dod": _DOD, "ico": _ICO}.get(embed)
+    if tab is None:
+        raise ValueError(f"unknown embedding '{embed}' (none, pos, cube, oct, dod, ico)")
+    d = np.array(tab, dtype=np.float64).astype(np.float32).T.copy()
+    acc = np.zeros(d.shape[1], dtype=np.float32)
+    for c in range(3):
+        acc = (d[c].astype(np.float64) * d[c].astype(np.float64) + acc.astype(np.float64)).astype(np.float32)
+    n = np.sqrt(acc).astype(np.float32)
+    return (d / n[None, :]).astype(np.float32)
 
 
 @dataclasses.dataclass(frozen=True)
@@ -61,6 +83,8 @@ class NetSpec:
     w0: float = 20.0
     max_df: float = 1.0
     nb_states: int = 3
+    act: str = "sin"    # 'sin' | 'relu' | 'softplus' (neural_df.py:40-47)
+    res: str = "full"   # 'full' | 'state' | 'latent': what layer 3 sees besides h2 (neural_df.py:76-78)
 
     @property
     def n_dirs(self) -> int:
@@ -71,13 +95,14 @@ class NetSpec:
         return self.nb_freqs * self.n_dirs * 2 + 3
 
     def param_shapes(self) -> List[Tuple[str, Tuple[int, ...]]]:
-        """Parameter names/shapes in torch ``state_dict`` order (neural_df.py:61-89, res='full')."""
+        """Parameter names/shapes in torch ``state_dict`` order (neural_df.py:61-89)."""
         E, L = self.n_embed, self.size_latent
         n1, n2, n3, n4 = self.layer_sizes
+        c3 = n2 + {"full": E + L, "state": E, "latent": L}[self.res]
         return [
             ("layers.main1.0.weight", (n1, E + L)), ("layers.main1.0.bias", (n1,)),
             ("layers.main1.3.weight", (n2, n1)), ("layers.main1.3.bias", (n2,)),
-            ("layers.main2.0.weight", (n3, n2 + E + L)), ("layers.main2.0.bias", (n3,)),
+            ("layers.main2.0.weight", (n3, c3)), ("layers.main2.0.bias", (n3,)),
             ("layers.main2.3.weight", (n4, n3)), ("layers.main2.3.bias", (n4,)),
             ("layers.df.0.weight", (1, n4)), ("layers.df.0.bias", (1,)),
         ]
@@ -150,9 +175,14 @@ def siren_weights(spec: NetSpec = DEFAULT_SPEC, seed: int = 0, weight_gain: floa
 def pack(spec: NetSpec, params: Dict[str, np.ndarray]) -> bytes:
     """Serialise to the `.sdfw` layout read by ``sdfnmpc_net_load_file`` (include/sdfnmpc.h)."""
     dirs = embedding_dirs(spec.embed)
-    freqs = (2.0 ** np.linspace(0, spec.nb_freqs - 1, spec.nb_freqs)).astype(np.float32)
-    hdr = _HDR.pack(MAGIC, VERSION, spec.nb_states, spec.size_latent, *spec.layer_sizes,
-                    spec.nb_freqs, dirs.shape[1], 0, spec.w0, spec.max_df)
+    nf = spec.nb_freqs if dirs.shape[1] else 0  # embed 'none': no frequencies
+    freqs = (2.0 ** np.linspace(0, nf - 1, nf)).astype(np.float32)
+    if spec.act == "sin" and spec.res == "full":  # version 1: byte-identical to every earlier blob
+        hdr = _HDR.pack(MAGIC, VERSION, spec.nb_states, spec.size_latent, *spec.layer_sizes,
+                        nf, dirs.shape[1], 0, spec.w0, spec.max_df)
+    else:
+        hdr = _HDR2.pack(MAGIC, 2, spec.nb_states, spec.size_latent, *spec.layer_sizes, nf, dirs.shape[1],
+                         RES_CODES[spec.res], ACT_CODES[spec.act], spec.w0, spec.max_df)
     body = [dirs.astype("<f4").tobytes(), freqs.astype("<f4").tobytes()]
     for name, shape in spec.param_shapes():
         a = np.asarray(params[name], dtype=np.float32)
@@ -163,13 +193,21 @@ def pack(spec: NetSpec, params: Dict[str, np.ndarray]) -> bytes:
 
 
 def unpack(blob: bytes) -> Tuple[NetSpec, Dict[str, np.ndarray]]:
-    magic, ver, ns, L, n1, n2, n3, n4, nf, nd, res, w0, max_df = _HDR.unpack_from(blob, 0)
-    if magic != MAGIC or ver != VERSION or res != 0:
-        raise ValueError("not a version-1 res='full' .sdfw blob")
-    embed = {8: "oct", 3: "pos", 6: "cube"}[nd]
-    spec = NetSpec(size_latent=L, layer_sizes=(n1, n2, n3, n4), nb_freqs=nf, embed=embed,
-                   w0=float(w0), max_df=float(max_df), nb_states=ns)
-    off = _HDR.size + 4 * (3 * nd + nf)
+    magic, ver = struct.unpack_from("<8sI", blob, 0)
+    if magic != MAGIC or ver not in (1, 2):
+        raise ValueError("not a version-1/2 .sdfw blob")
+    if ver == 1:
+        _, _, ns, L, n1, n2, n3, n4, nf, nd, res, w0, max_df = _HDR.unpack_from(blob, 0)
+        act, hsize = 0, _HDR.size
+        if res != 0:
+            raise ValueError("version-1 .sdfw blobs are res='full'")
+    else:
+        _, _, ns, L, n1, n2, n3, n4, nf, nd, res, act, w0, max_df = _HDR2.unpack_from(blob, 0)
+        hsize = _HDR2.size
+    spec = NetSpec(size_latent=L, layer_sizes=(n1, n2, n3, n4), nb_freqs=nf if nd else 5, embed=EMBED_BY_DIRS[nd],
+                   w0=float(w0), max_df=float(max_df), nb_states=ns,
+                   act={v: k for k, v in ACT_CODES.items()}[act], res={v: k for k, v in RES_CODES.items()}[res])
+    off = hsize + 4 * (3 * nd + nf)
     params = {}
     for name, shape in spec.param_shapes():
         n = int(np.prod(shape))
@@ -203,14 +241,15 @@ def from_torchscript(path: str) -> Tuple[NetSpec, Dict[str, np.ndarray]]:
     n2 = sd["layers.main1.3.weight"].shape[0]
     n3 = sd["layers.main2.0.weight"].shape[0]
     n4 = sd["layers.main2.3.weight"].shape[0]
-    nd = sd["embed.dirs"].shape[1]
-    nf = sd["embed.freq_bands"].shape[0]
+    nd = sd["embed.dirs"].shape[1] if "embed.dirs" in sd else 0
+    nf = sd["embed.freq_bands"].shape[0] if nd else 5
     E = 3 + 2 * nf * nd
     L = sd["layers.main1.0.weight"].shape[1] - E
-    embed = {8: "oct", 3: "pos", 6: "cube"}[nd]
+    embed = EMBED_BY_DIRS[nd]
     spec = NetSpec(size_latent=L, layer_sizes=(n1, n2, n3, n4), nb_freqs=nf, embed=embed,
-                   w0=float(m.w0), max_df=float(m.max_df))
-    if not np.array_equal(sd["embed.dirs"], embedding_dirs(embed)):
+                   w0=float(m.w0), max_df=float(m.max_df), act=str(getattr(m, "activation", "sin")),
+                   res=str(getattr(m, "res", "full")))
+    if nd and not np.array_equal(sd["embed.dirs"], embedding_dirs(embed)):
         raise ValueError("unexpected embedding directions")
     return spec, {k: sd[k] for k, _ in spec.param_shapes()}
 

@@ -6,6 +6,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "oracle"))  # test infrastructure: the CPU checker
+sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))  # variant_specs (fixture specs)
 
 
 def pytest_configure(config):
@@ -29,7 +30,8 @@ def oracle_lib():
 def golden():
     import numpy as np
     d = os.path.join(ROOT, "tests", "golden")
-    return {k: np.load(os.path.join(d, f"{k}_golden.npz")) for k in ("sdf", "lin", "grid", "params", "sdfc3")}
+    return {k: np.load(os.path.join(d, f"{k}_golden.npz")) for k in ("sdf", "lin", "grid", "params", "sdfc3",
+                                                                                  "variants")}
 
 
 @pytest.fixture(scope="session")

@@ -79,7 +79,7 @@ VARIANTS = {  # name -> (seed, weight_gain, bias_gain)
 
 def ref_net(spec, params, dtype):
     net = NeuralDF(nb_states=3, size_latent=spec.size_latent, signed=True, max_df=spec.max_df,
-                   res="full", w0=spec.w0, embed=spec.embed, act="sin",
+                   res=spec.res, w0=spec.w0, embed=spec.embed, act=spec.act,
                    layer_sizes=list(spec.layer_sizes), dropout_rate=0.1, nb_freqs=spec.nb_freqs)
     sd = net.state_dict()
     for k, v in params.items():
@@ -499,6 +499,33 @@ def wide_golden(n=128):
     print("wide_golden.npz", {k: v.shape for k, v in out.items()})
 
 
+from variant_specs import BIAS_GAIN, NET_VARIANTS, SEED  # noqa: E402
+
+
+def variants_golden(n=48):
+    """The reference's own NeuralDF for each NET_VARIANTS spec (variant_specs.py; SIREN-init weights from
+    our PRNG, biases drawn so the bias path is live): df and d df / d pos in fp32 and fp64, plus the embedding
+    directions the reference builds (pins weights.embedding_dirs for every projection)."""
+    out = {}
+    rng = np.random.default_rng(777)
+    inp = sample_inputs(rng, n, 128)
+    out["input"] = inp
+    for name, spec in NET_VARIANTS.items():
+        params = W.siren_weights(spec, seed=SEED, bias_gain=BIAS_GAIN)
+        out[f"{name}/sha256"] = np.frombuffer(hashlib.sha256(W.pack(spec, params)).digest(), dtype=np.uint8)
+        for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+            net = ref_net(spec, params, dt)
+            x = torch.from_numpy(inp).to(dt).requires_grad_(True)
+            df = net(x)
+            (g,) = torch.autograd.grad(df.sum(), x)
+            out[f"{name}/df_{tag}"] = df.detach().numpy()[:, 0]
+            out[f"{name}/grad_{tag}"] = g.numpy()[:, :3]
+        if spec.embed != "none":
+            out[f"{name}/dirs"] = ref_net(spec, params, torch.float32).embed.dirs.numpy()
+    np.savez_compressed(os.path.join(HERE, "variants_golden.npz"), **out)
+    print("variants_golden.npz", len(out))
+
+
 def sdfc3_golden(stride=32):
     """The reference's own NeuralDF (SIREN-init, seed 0) in fp32 and fp64 on every `stride`-th SDF row of
     the bench workload C3 (1024 instances x 41 nodes, synthetic seed 1000): body positions in the
@@ -591,6 +618,7 @@ def vae_golden():
 if __name__ == "__main__":
     only = sys.argv[1:]
     for name, fn in (("sdf", sdf_golden), ("lin", lin_golden), ("grid", grid_golden), ("params", params_golden),
-                     ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden), ("wide", wide_golden), ("sdfc3", sdfc3_golden)):
+                     ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden), ("wide", wide_golden), ("sdfc3", sdfc3_golden),
+                     ("variants", variants_golden)):
         if not only or name in only:
             fn()

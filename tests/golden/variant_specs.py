@@ -1,0 +1,19 @@
+"""NeuralDF variants beyond the deployed net (sdf_nmpc/network/neural_df.py:13-103): activation, embedding,
+residual input of layer 3, layer sizes (non-multiples of 128 exercise the padded schedule) and frequency
+count.  Shared by make_golden.py (variants_golden.npz, from the reference's own NeuralDF) and the tests."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import sdf_nmpc_amd  # noqa: E402,F401
+from sdf_nmpc_amd import weights as W  # noqa: E402
+
+NET_VARIANTS = {
+    "relu_pos_full": W.NetSpec(act="relu", embed="pos", res="full", layer_sizes=(256, 256, 256, 256), w0=1.0),
+    "softplus_cube_state": W.NetSpec(act="softplus", embed="cube", res="state", w0=1.0),
+    "sin_dod_latent": W.NetSpec(act="sin", embed="dod", res="latent"),
+    "sin_ico_full": W.NetSpec(act="sin", embed="ico", res="full", layer_sizes=(128, 128, 128, 128)),
+    "relu_none_state": W.NetSpec(act="relu", embed="none", res="state", layer_sizes=(192, 160, 100, 50), w0=1.0),
+    "sin_oct6_full": W.NetSpec(act="sin", embed="oct", res="full", nb_freqs=6, w0=30.0),
+}
+SEED, BIAS_GAIN = 7, 0.5  # variants_golden.npz weights: W.siren_weights(spec, SEED, bias_gain=BIAS_GAIN)

@@ -124,3 +124,26 @@ def test_oracle_batch_equals_per_node_calls(oracle_lib, cfg):
             if k < N:
                 xn, AB = oracle_lib.rk4(m, x, prob["u"][b, k], prob["dt"][k])
                 assert np.array_equal(out["xn"][b, k], xn) and np.array_equal(out["AB"][b, k], AB.T)
+
+
+# ---- NeuralDF variants (neural_df.py:13-103): act / embed / res / layer sizes / frequencies
+from variant_specs import BIAS_GAIN, NET_VARIANTS, SEED  # noqa: E402
+
+
+@pytest.mark.parametrize("name", sorted(NET_VARIANTS))
+def test_neural_df_np_matches_reference_variants(golden, name):
+    """oracle/neural_df_np.py (the variants' checker) against the reference's own NeuralDF in fp64 on the
+    same weights and inputs; the blob round trip and the embedding directions, bit for bit."""
+    import neural_df_np
+    g, spec = golden["variants"], NET_VARIANTS[name]
+    params = W.siren_weights(spec, seed=SEED, bias_gain=BIAS_GAIN)
+    blob = W.pack(spec, params)
+    assert hashlib.sha256(blob).digest() == g[f"{name}/sha256"].tobytes()
+    spec2, params2 = W.unpack(blob)
+    assert spec2 == spec and all(np.array_equal(params[k], params2[k]) for k in params)
+    if f"{name}/dirs" in g.files:  # weights.embedding_dirs == the buffer the reference builds
+        assert np.array_equal(W.embedding_dirs(spec.embed), g[f"{name}/dirs"])
+    df, gr = neural_df_np.forward_grad(spec, params, g["input"])
+    ref_df, ref_g = g[f"{name}/df_f64"], g[f"{name}/grad_f64"]
+    assert np.abs(df - ref_df).max() <= 1e-12 * max(1.0, np.abs(ref_df).max())
+    assert np.abs(gr - ref_g).max() <= 1e-12 * max(1.0, np.abs(ref_g).max())
