@@ -132,9 +132,11 @@ def test_weight_blob_roundtrip_and_fingerprint(gpu_ctx):
     assert _lib.Net.siren(gpu_ctx, 1).fingerprint != a.fingerprint
     with pytest.raises(_lib.SdfnmpcError):
         _lib.Net.from_blob(gpu_ctx, b"SDFNMPCW" + b"\0" * 40)
-    odd = W.NetSpec(layer_sizes=(200, 200, 100, 50))  # neither the deployed nor a 128-multiple net
+    odd = W.NetSpec(layer_sizes=(200, 200, 100, 50))  # padded to multiples of 128 (sdf_wide.hip)
+    _lib.Net.from_blob(gpu_ctx, W.pack(odd, W.siren_weights(odd, 0))).close()
+    small = W.NetSpec(size_latent=64)  # the kernels are built for the reference's 128-wide latent
     with pytest.raises(_lib.SdfnmpcError, match="not built for"):
-        _lib.Net.from_blob(gpu_ctx, W.pack(odd, W.siren_weights(odd, 0)))
+        _lib.Net.from_blob(gpu_ctx, W.pack(small, W.siren_weights(small, 0)))
 
 
 def test_l4c_shim_casadi_calls(golden, tmp_path):
