@@ -33,8 +33,9 @@ def _act(spec, a):
     return np.where(a > 20.0, a, np.log1p(ez)), np.where(a > 20.0, 1.0, ez / (ez + 1.0))
 
 
-def forward_grad(spec, params, inp):
-    """inp [n, 3 + L] -> (df [n], d df / d pos [n, 3]) in fp64."""
+def forward_grad(spec, params, inp, latent_grad=False):
+    """inp [n, 3 + L] -> (df [n], d df / d pos [n, 3]) in fp64; with latent_grad also d df / d z [n, L]
+    (the latent columns of L4CasADi's 1 x 131 jac_sdf_l4c)."""
     x = np.asarray(inp, dtype=np.float64)
     pos, z = x[:, :3], x[:, 3:]
     p = {k: np.asarray(v, dtype=np.float64) for k, v in params.items()}
@@ -77,4 +78,9 @@ def forward_grad(spec, params, inp):
         nb = xb.shape[1]
         gs = ge[:, 3:3 + nb] * np.cos(xb) + ge[:, 3 + nb:3 + 2 * nb] * np.cos(xb + 0.5 * np.pi)
         grad += gs @ dxb.T
-    return df, grad
+    if not latent_grad:
+        return df, grad
+    gz = (g1 @ W1)[:, E:]
+    if spec.res in ("full", "latent"):
+        gz = gz + gx3[:, W3.shape[1] - z.shape[1]:]
+    return df, grad, gz

@@ -551,7 +551,7 @@ void pack_operand(std::vector<float>& dst, int N, int K, F&& W) {
 struct WideDev {  // plain row-major [N][K] fp32 operands of the wide schedule (sdf_wide.hip)
     const float *F1 = nullptr, *F2 = nullptr, *F3 = nullptr, *F4 = nullptr;
     const float *B4 = nullptr, *B3h = nullptr, *B3e = nullptr, *B2 = nullptr, *B1e = nullptr;
-    const float *Hz = nullptr, *bz = nullptr, *b2 = nullptr, *b4 = nullptr, *w5 = nullptr;
+    const float *Bz = nullptr, *Hz = nullptr, *bz = nullptr, *b2 = nullptr, *b4 = nullptr, *w5 = nullptr;
     const float4* emb_tab = nullptr;
     int P1 = 0, P2 = 0, P3 = 0, P4 = 0;  // layer widths padded to multiples of 128
     int NEK = NE, NEB = 128;             // embedding width as a K segment / as the d e GEMMs' output
@@ -643,6 +643,10 @@ static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     mat(NEB, P3, [&](int j, int k) { return e3 && j < E && k < n3 ? W3[(size_t)k * c3 + n2 + j] : 0.0f; });      // B3e
     mat(P1, P2, [&](int j, int k) { return j < n1 && k < n2 ? W2[(size_t)k * n1 + j] : 0.0f; });                 // B2
     mat(NEB, P1, [&](int j, int k) { return j < E && k < n1 ? W1[(size_t)k * c1 + j] : 0.0f; });                 // B1e
+    mat(L, P1 + P3, [&](int j, int k) {  // Bz: d z = [delta1 | delta3] . [W1z ; W3z] (the 131-wide jac_sdf_l4c)
+        if (k < P1) return k < n1 ? W1[(size_t)k * c1 + E + j] : 0.0f;
+        return z3 && k - P1 < n3 ? W3[(size_t)(k - P1) * c3 + z3off + j] : 0.0f;
+    });
     mat(P1 + P3, L, [&](int j, int k) {                                                                          // Hz
         if (j < P1) return j < n1 ? W1[(size_t)j * c1 + E + k] : 0.0f;
         return z3 && j - P1 < n3 ? W3[(size_t)(j - P1) * c3 + z3off + k] : 0.0f;
@@ -675,6 +679,7 @@ static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     int i = 0;
     w.F1 = d + off[i++]; w.F2 = d + off[i++]; w.F3 = d + off[i++]; w.F4 = d + off[i++];
     w.B4 = d + off[i++]; w.B3h = d + off[i++]; w.B3e = d + off[i++]; w.B2 = d + off[i++]; w.B1e = d + off[i++];
+    w.Bz = d + off[i++];
     w.Hz = d + off[i++]; w.bz = d + off[i++]; w.b2 = d + off[i++]; w.b4 = d + off[i++]; w.w5 = d + off[i++];
     w.emb_tab = (const float4*)(d + off[i++]);
     w.P1 = P1; w.P2 = P2; w.P3 = P3; w.P4 = P4; w.NEK = NEK; w.NEB = NEB;
@@ -874,7 +879,7 @@ static int run_sdf(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, con
 // x / p (then also the constraint epilogue when cons->h is set).
 static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, const float4* pos4, const float* zf,
                     const double* zd, long long zstride, int n_inst, int rows_per_inst, float4* out4,
-                    const SdfArgs* cons) {
+                    const SdfArgs* cons, float* glat = nullptr) {
     if (rows > 0x7fffffffLL / 2) return fail(SDFNMPC_E_ARG, "too many rows");
     const WideDev& w = net->wd;
     const int n1 = w.P1, n2 = w.P2, n3 = w.P3, n4 = w.P4, nz = n1 + n3, R = (int)rows;
@@ -932,6 +937,9 @@ static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, co
     HIPCHK(gemm(H2, n2, nullptr, 0, w.B2, R, n1, WIDE_EPI_BWD, nullptr, nullptr, D1, n1, H1, nullptr, "sdf_wide_gemm"));
     HIPCHK(gemm(H1, n1, nullptr, 0, w.B1e, R, NEB, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, GE1, nullptr,
                 "sdf_wide_gemm"));
+    if (glat)  // d df / d z = delta1 W1z + delta3 W3z: one GEMM over the two K segments [delta1 | delta3]
+        HIPCHK(gemm(H1, n1, H3, n3, w.Bz, R, L, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, glat, nullptr,
+                    "sdf_wide_gemm"));
     ea.H4 = H4; ea.GE3 = GE3; ea.GE1 = GE1; ea.w5 = w.w5; ea.b5 = net->args.b5; ea.out = out4;
     HIPCHK(timed(ctx, "sdf_wide_final", [&] { return launch_wide_final(ea, st); }));
     return SDFNMPC_OK;
@@ -954,12 +962,9 @@ extern "C" int sdfnmpc_sdf_eval(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long l
     if (rows == 0) return SDFNMPC_OK;
     ScopedDevice sd(ctx->device);
     const int n_inst = (int)((rows + rows_per_inst - 1) / rows_per_inst);
-    if (net->wide) {
-        if (grad_latent)
-            return fail(SDFNMPC_E_UNSUPPORTED, "latent gradient (the 131-wide jac_sdf_l4c) is not built for wide networks");
+    if (net->wide)
         return run_wide(ctx, net, rows, (const float4*)pos4, latent, nullptr, 0, n_inst, rows_per_inst, (float4*)out4,
-                        nullptr);
-    }
+                        nullptr, grad_latent);
     HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
     int rc = run_hoist<float>(ctx, net, latent, L, n_inst, (float*)ctx->c13.p);
     if (rc) return rc;

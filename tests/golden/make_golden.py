@@ -502,7 +502,7 @@ def wide_golden(n=128):
 from variant_specs import BIAS_GAIN, NET_VARIANTS, SEED  # noqa: E402
 
 
-def variants_golden(n=48):
+def variants_golden(n=32):
     """The reference's own NeuralDF for each NET_VARIANTS spec (variant_specs.py; SIREN-init weights from
     our PRNG, biases drawn so the bias path is live): df and d df / d pos in fp32 and fp64, plus the embedding
     directions the reference builds (pins weights.embedding_dirs for every projection)."""
@@ -519,7 +519,7 @@ def variants_golden(n=48):
             df = net(x)
             (g,) = torch.autograd.grad(df.sum(), x)
             out[f"{name}/df_{tag}"] = df.detach().numpy()[:, 0]
-            out[f"{name}/grad_{tag}"] = g.numpy()[:, :3]
+            out[f"{name}/grad_{tag}"] = g.numpy()  # the full 1 x 131 Jacobian (jac_sdf_l4c)
         if spec.embed != "none":
             out[f"{name}/dirs"] = ref_net(spec, params, torch.float32).embed.dirs.numpy()
     np.savez_compressed(os.path.join(HERE, "variants_golden.npz"), **out)

@@ -30,7 +30,7 @@ def test_variant_vs_reference_golden(gpu_ctx, golden, name):
         net.close()
     assert np.isfinite(o).all()
     df64, df32 = g[f"{name}/df_f64"], g[f"{name}/df_f32"]
-    g64, g32 = g[f"{name}/grad_f64"], g[f"{name}/grad_f32"]
+    g64, g32 = g[f"{name}/grad_f64"][:, :3], g[f"{name}/grad_f32"][:, :3]
     err_df, err_g = np.abs(o[:, 0] - df64).max(), np.abs(o[:, 1:] - g64).max()
     assert err_df <= _bar(df64, df32), (err_df, np.abs(df32 - df64).max())
     assert err_g <= _bar(g64, g32), (err_g, np.abs(g32 - g64).max())
@@ -76,3 +76,23 @@ def test_variant_in_the_preparation_phase(gpu_ctx, cfg, name):
     assert np.abs(h[:, 2] - h_ref).max() <= 1e-5 * scale
     assert np.abs(J[:, :3, 2] - J_ref).max() <= 1e-5 * max(1.0, np.abs(J_ref).max())
     assert np.all(J[:, 3:, 2] == 0.0)
+
+
+@pytest.mark.parametrize("name", sorted(NET_VARIANTS))
+def test_variant_full_jacobian_host_path(gpu_ctx, golden, name):
+    """sdfnmpc_sdf_eval_host on a variant net: the full 1 x 131 Jacobian L4CasADi's jac_sdf_l4c returns
+    (position and latent columns) against the reference's own autograd Jacobian, and through the CasADi
+    external ABI's rows (one row per call, as acados calls it)."""
+    g, spec = golden["variants"], NET_VARIANTS[name]
+    net = _lib.Net.from_blob(gpu_ctx, W.pack(spec, W.siren_weights(spec, SEED, bias_gain=BIAS_GAIN)))
+    try:
+        inp = g["input"].astype(np.float64)
+        df, gr = net.eval_host(inp)
+        df1, gr1 = net.eval_host(inp[5:6])
+    finally:
+        net.close()
+    g64, g32 = g[f"{name}/grad_f64"], g[f"{name}/grad_f32"]
+    assert np.abs(df - g[f"{name}/df_f64"]).max() <= _bar(g[f"{name}/df_f64"], g[f"{name}/df_f32"])
+    assert np.abs(gr - g64).max() <= _bar(g64, g32), (np.abs(gr - g64).max(), np.abs(g32 - g64).max())
+    assert np.abs(gr1[0] - g64[5]).max() <= _bar(g64, g32)
+    assert abs(df1[0] - g[f"{name}/df_f64"][5]) <= _bar(g[f"{name}/df_f64"], g[f"{name}/df_f32"])

@@ -57,9 +57,16 @@ def test_wide_rows_independent_bitwise(gpu_ctx, wide_net):
     assert np.array_equal(a[perm], b)
 
 
-def test_wide_latent_gradient_is_refused(gpu_ctx, wide_net):
-    with pytest.raises(_lib.SdfnmpcError, match="not built for wide"):
-        wide_net.eval_host(np.zeros((2, 131)), want_grad=True)
+def test_wide_full_jacobian_vs_oracle(gpu_ctx, wide_net, oracle_lib, wg):
+    """The 1 x 131 Jacobian (jac_sdf_l4c's latent columns included) of the C5 net through the host path,
+    against the fp64 C oracle."""
+    inp = wg["input"][:40].astype(np.float64)
+    df, gr = wide_net.eval_host(inp, want_grad=True)
+    onet = oracle_lib.Net(W.WIDE_SPEC, W.siren_weights(W.WIDE_SPEC, 0))
+    df64, _, g64 = onet.f64(inp)
+    assert sdf_df_ok(df, df64), sdf_df_err(df, df64)
+    assert sdf_grad_ok(gr[:, :3], g64[:, :3]), sdf_grad_err(gr[:, :3], g64[:, :3])
+    assert np.abs(gr[:, 3:] - g64[:, 3:]).max() <= 1e-5 * max(1.0, np.abs(g64[:, 3:]).max())
 
 
 def test_wide_linearize_matches_oracle(gpu_ctx, cfg, oracle_lib):

@@ -143,7 +143,8 @@ def test_neural_df_np_matches_reference_variants(golden, name):
     assert spec2 == spec and all(np.array_equal(params[k], params2[k]) for k in params)
     if f"{name}/dirs" in g.files:  # weights.embedding_dirs == the buffer the reference builds
         assert np.array_equal(W.embedding_dirs(spec.embed), g[f"{name}/dirs"])
-    df, gr = neural_df_np.forward_grad(spec, params, g["input"])
+    df, gr, gz = neural_df_np.forward_grad(spec, params, g["input"], latent_grad=True)
     ref_df, ref_g = g[f"{name}/df_f64"], g[f"{name}/grad_f64"]
     assert np.abs(df - ref_df).max() <= 1e-12 * max(1.0, np.abs(ref_df).max())
-    assert np.abs(gr - ref_g).max() <= 1e-12 * max(1.0, np.abs(ref_g).max())
+    assert np.abs(gr - ref_g[:, :3]).max() <= 1e-12 * max(1.0, np.abs(ref_g).max())
+    assert np.abs(gz - ref_g[:, 3:]).max() <= 1e-12 * max(1.0, np.abs(ref_g).max())
