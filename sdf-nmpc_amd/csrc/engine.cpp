@@ -1014,10 +1014,16 @@ static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const fl
         S.live = false;
     }
     if (S.live && S.net != net->uid) srv_stop(ctx);
-    if (S.live && std::chrono::duration<double>(clk::now() - S.last).count() > 0.5 * S.idle_s) {
+    if (S.live && (S.mb->stop || std::chrono::duration<double>(clk::now() - S.last).count() > 0.5 * S.idle_s)) {
         const hipError_t q = hipStreamQuery(S.stream);
-        if (q == hipSuccess) S.live = false;
-        else if (q != hipErrorNotReady) return fail(SDFNMPC_E_HIP, std::string("sdf server: ") + hipGetErrorString(q));
+        if (q == hipSuccess) {
+            S.live = false;
+            __atomic_store_n(&S.mb->stop, 0ull, __ATOMIC_RELEASE);
+        } else if (q == hipErrorNotReady && S.mb->stop) {
+            return fail(SDFNMPC_E_HIP, "sdf server: the previous server has not left yet");
+        } else if (q != hipErrorNotReady) {
+            return fail(SDFNMPC_E_HIP, std::string("sdf server: ") + hipGetErrorString(q));
+        }
     }
     memcpy(S.mb->in, hp, (size_t)rows * 4 * sizeof(float));
     memcpy(S.mb->in + (size_t)rows * 4, hl, (size_t)rows * L * sizeof(float));
@@ -1044,7 +1050,9 @@ static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const fl
                 return fail(SDFNMPC_E_HIP, std::string("sdf server: ") + hipGetErrorString(q));
             }
             if (std::chrono::duration<double>(clk::now() - t0).count() > 5.0) {
-                srv_stop(ctx);
+                // ask it to leave, but do not wait on a server that stopped answering; a later call
+                // queries the stream and relaunches only once it has gone
+                __atomic_store_n(&S.mb->stop, 1ull, __ATOMIC_RELEASE);
                 return fail(SDFNMPC_E_HIP, "sdf server: no answer within 5 s");
             }
         }
