@@ -22,6 +22,32 @@
 namespace sdfn {
 
 typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// fp32 -> three bf16 by truncation: x = hi + mid + lo EXACTLY (each takes the next 8 significant bits of
+// the 24; the remainders are exact fp32 differences).  Eight values -> three 8-lane bf16 operands.
+__device__ __forceinline__ void split3(const float (&x)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
+    unsigned hw[4], mw[4], lw[4];
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+        unsigned hb[2], mb[2], lb[2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const float v = x[2 * p + q];
+            hb[q] = __float_as_uint(v) & 0xffff0000u;
+            const float r1 = v - __uint_as_float(hb[q]);
+            mb[q] = __float_as_uint(r1) & 0xffff0000u;
+            const float r2 = r1 - __uint_as_float(mb[q]);
+            lb[q] = __float_as_uint(r2) & 0xffff0000u;
+        }
+        hw[p] = (hb[0] >> 16) | hb[1];
+        mw[p] = (mb[0] >> 16) | mb[1];
+        lw[p] = (lb[0] >> 16) | lb[1];
+    }
+    h = __builtin_bit_cast(bf16x8, hw);
+    m = __builtin_bit_cast(bf16x8, mw);
+    l = __builtin_bit_cast(bf16x8, lw);
+}
 
 // ------------------------------------------------------------------------------------------------
 // preprocessing: ToDevice (float32), Reshape (bilinear, align_corners=False), ClipDistance,
@@ -230,6 +256,7 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
             bv[i][0] = b0.x; bv[i][1] = b0.y; bv[i][2] = b0.z; bv[i][3] = b0.w;
             bv[i][4] = b1.x; bv[i][5] = b1.y; bv[i][6] = b1.z; bv[i][7] = b1.w;
         }
+#ifdef VAE_F32_MFMA  // diagnostic: the exact-fp32 MFMA (eight 32x32x2 steps per K-tile)
 #pragma unroll
         for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -237,6 +264,30 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
 #pragma unroll
                 for (int j = 0; j < 2; ++j)
                     acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[j][s], acc[i][j], 0, 0, 0);
+#else
+        // fp32 products on the bf16 matrix pipe: a = ah + am + al, b = bh + bm + bl exactly, and the six
+        // products down to 2^-16 relative (al.bh, ah.bl, am.bm, am.bh, ah.bm, ah.bh; smallest first)
+        // are accumulated in fp32 -- the dropped ones (am.bl, al.bm, al.bl) are <= 2^-24 relative, the
+        // fp32 rounding level.  One 32x32x16 K-step covers the K-tile (lane half h: k = 8h .. 8h + 7,
+        // the same permutation for A and B).  6 x 32 cycles of the matrix pipe per block and K-tile
+        // against 8 x 64 for the fp32 MFMA.
+        bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            split3(av[i], ah[i], am[i], al[i]);
+            split3(bv[i], bh[i], bm[i], bl[i]);
+        }
+#define VAE_MM(X, Y)                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)         \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[i], Y[j], acc[i][j], 0, 0, 0);
+        VAE_MM(al, bh)
+        VAE_MM(ah, bl)
+        VAE_MM(am, bm)
+        VAE_MM(am, bh)
+        VAE_MM(ah, bm)
+        VAE_MM(ah, bh)
+#undef VAE_MM
+#endif
         if (kt + 1 < KT) VAE_STASH(buf ^ 1);
         __syncthreads();
     }

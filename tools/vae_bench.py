@@ -13,6 +13,8 @@ from sdf_nmpc_amd.config import Config  # noqa: E402
 
 
 def main(B=512, steps=10):
+    if os.environ.get("SDFNMPC_LIB"):  # a diagnostic build (tools/build_variant.sh)
+        _lib.LIB_PATH = os.environ["SDFNMPC_LIB"]
     cfg = Config()
     ctx = _lib.Context(0, stream=torch.cuda.current_stream().cuda_stream)
     spec = V.DEFAULT_ENCODER
@@ -32,7 +34,7 @@ def main(B=512, steps=10):
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t) / steps
     fl = spec.n_flops() * B
-    print(f"B={B}: {dt*1e3:.3f} ms/encode  {fl/dt/1e12:.1f} TFLOP/s  ({B/dt:.0f} images/s)")
+    print(f"{_lib.LIB_PATH[-32:]} B={B}: {dt*1e3:.3f} ms/encode  {fl/dt/1e12:.1f} TFLOP/s  ({B/dt:.0f} images/s)")
     for k in ("vae_pre", "vae_stem", "vae_conv", "vae_head"):
         ms, n = ctx.kernel_stats(k)
         print(f"  {k:10s} {ms/steps:.3f} ms/encode ({n//steps} launches)")
