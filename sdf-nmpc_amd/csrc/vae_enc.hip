@@ -24,30 +24,7 @@ namespace sdfn {
 typedef float floatx16 __attribute__((ext_vector_type(16)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
-// fp32 -> three bf16 by truncation: x = hi + mid + lo EXACTLY (each takes the next 8 significant bits of
-// the 24; the remainders are exact fp32 differences).  Eight values -> three 8-lane bf16 operands.
-__device__ __forceinline__ void split3(const float (&x)[8], bf16x8& h, bf16x8& m, bf16x8& l) {
-    unsigned hw[4], mw[4], lw[4];
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-        unsigned hb[2], mb[2], lb[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const float v = x[2 * p + q];
-            hb[q] = __float_as_uint(v) & 0xffff0000u;
-            const float r1 = v - __uint_as_float(hb[q]);
-            mb[q] = __float_as_uint(r1) & 0xffff0000u;
-            const float r2 = r1 - __uint_as_float(mb[q]);
-            lb[q] = __float_as_uint(r2) & 0xffff0000u;
-        }
-        hw[p] = (hb[0] >> 16) | hb[1];
-        mw[p] = (mb[0] >> 16) | mb[1];
-        lw[p] = (lb[0] >> 16) | lb[1];
-    }
-    h = __builtin_bit_cast(bf16x8, hw);
-    m = __builtin_bit_cast(bf16x8, mw);
-    l = __builtin_bit_cast(bf16x8, lw);
-}
+
 
 // ------------------------------------------------------------------------------------------------
 // preprocessing: ToDevice (float32), Reshape (bilinear, align_corners=False), ClipDistance,
@@ -167,6 +144,26 @@ hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s) {
 // 16-byte slots (conflict-free).  Within a K-tile, MFMA step s feeds lane half h with k = 8h + s
 // (the same permutation for A and B), so each lane reads its 8 k-values with two ds_read_b128.
 constexpr int CV_BM = 128, CV_BN = 128, CV_BK = 16, CV_LD = 20;
+constexpr int CV_SLD = 24;  // bf16 plane row stride (48 bytes)
+
+// fp32 -> three bf16 by truncation: x = hi + mid + lo EXACTLY (each takes the next 8 significant bits of
+// the 24; the remainders are exact fp32 differences).  A float4 of one row -> its 4-bf16 pieces of the
+// hi / mid / lo planes (8-byte stores).
+__device__ __forceinline__ void split3_store(float4 v, unsigned short (*planes)[CV_BM * CV_SLD], int off) {
+    const float x[4] = {v.x, v.y, v.z, v.w};
+    unsigned hb[4], mb[4], lb[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        hb[q] = __float_as_uint(x[q]) & 0xffff0000u;
+        const float r1 = x[q] - __uint_as_float(hb[q]);
+        mb[q] = __float_as_uint(r1) & 0xffff0000u;
+        const float r2 = r1 - __uint_as_float(mb[q]);
+        lb[q] = __float_as_uint(r2) & 0xffff0000u;
+    }
+    *(uint2*)&planes[0][off] = make_uint2((hb[0] >> 16) | hb[1], (hb[2] >> 16) | hb[3]);
+    *(uint2*)&planes[1][off] = make_uint2((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3]);
+    *(uint2*)&planes[2][off] = make_uint2((lb[0] >> 16) | lb[1], (lb[2] >> 16) | lb[3]);
+}
 
 // component-wise select (a ?: on the float4 struct goes through a stack slot)
 __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
@@ -176,8 +173,15 @@ __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
 template <int KS, int S>
 __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
     constexpr int P = KS / 2;
+#ifdef VAE_F32_MFMA
     __shared__ float As[2][CV_BM * CV_LD];
     __shared__ float Bs[2][CV_BN * CV_LD];
+#else
+    // the K-tile split ONCE, by the thread that loads it, into bf16 hi / mid / lo planes: rows of 16 bf16
+    // at a 24-bf16 (48-byte) stride, so the lane groups of a ds_read_b128 hit distinct 16-byte slots
+    __shared__ __align__(16) unsigned short As3[2][3][CV_BM * CV_SLD];
+    __shared__ __align__(16) unsigned short Bs3[2][3][CV_BN * CV_SLD];
+#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
     const int M = a.B * a.Ho * a.Wo, MT = (M + CV_BM - 1) / CV_BM;
@@ -222,6 +226,7 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
             }                                                                                                 \
         }                                                                                                     \
     } while (0)
+#ifdef VAE_F32_MFMA
 #define VAE_STASH(buf)                                        \
     do {                                                      \
         *(float4*)(&As[buf][srow0]) = ra0;                    \
@@ -229,6 +234,16 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
         *(float4*)(&Bs[buf][srow0]) = rb0;                    \
         *(float4*)(&Bs[buf][srow1]) = rb1;                    \
     } while (0)
+#else
+    const int hrow0 = (tid >> 2) * CV_SLD + 4 * kq, hrow1 = hrow0 + 64 * CV_SLD;
+#define VAE_STASH(buf)                                        \
+    do {                                                      \
+        split3_store(ra0, As3[buf], hrow0);                   \
+        split3_store(ra1, As3[buf], hrow1);                   \
+        split3_store(rb0, Bs3[buf], hrow0);                   \
+        split3_store(rb1, Bs3[buf], hrow1);                   \
+    } while (0)
+#endif
 
     floatx16 acc[2][2];
 #pragma unroll
@@ -244,6 +259,7 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
     for (int kt = 0; kt < KT; ++kt) {
         const int buf = kt & 1;
         if (kt + 1 < KT) VAE_LOAD(kt + 1);
+#ifdef VAE_F32_MFMA
         float av[2][8], bv[2][8];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -256,7 +272,7 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
             bv[i][0] = b0.x; bv[i][1] = b0.y; bv[i][2] = b0.z; bv[i][3] = b0.w;
             bv[i][4] = b1.x; bv[i][5] = b1.y; bv[i][6] = b1.z; bv[i][7] = b1.w;
         }
-#ifdef VAE_F32_MFMA  // diagnostic: the exact-fp32 MFMA (eight 32x32x2 steps per K-tile)
+        // diagnostic: the exact-fp32 MFMA (eight 32x32x2 steps per K-tile)
 #pragma unroll
         for (int s = 0; s < 8; ++s)
 #pragma unroll
@@ -274,8 +290,13 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
         bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            split3(av[i], ah[i], am[i], al[i]);
-            split3(bv[i], bh[i], bm[i], bl[i]);
+            const int ao = (wm * 64 + 32 * i + lr) * CV_SLD + 8 * lh, bo = (wn * 64 + 32 * i + lr) * CV_SLD + 8 * lh;
+            ah[i] = *(const bf16x8*)&As3[buf][0][ao];
+            am[i] = *(const bf16x8*)&As3[buf][1][ao];
+            al[i] = *(const bf16x8*)&As3[buf][2][ao];
+            bh[i] = *(const bf16x8*)&Bs3[buf][0][bo];
+            bm[i] = *(const bf16x8*)&Bs3[buf][1][bo];
+            bl[i] = *(const bf16x8*)&Bs3[buf][2][bo];
         }
 #define VAE_MM(X, Y)                                                                                   \
     _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)         \
