@@ -204,9 +204,10 @@ int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B);
 /* LDS bytes one instance of the serial QP kernel holds at horizon N (-1: N < 1) */
 long long sdfnmpc_qp_lds_bytes(int N);
 /* the occupancy gate of SURVEY.md §8(e): instances the context's device solves in one wave of QP
- * workgroups at horizon N = CUs x (LDS per CU / LDS per instance), from hipDeviceProp_t and the LDS
- * footprint of the kernel sdfnmpc_ctx_qp_kernel picks (1024 at N = 40 on an MI355X); 0 when N does
- * not fit one CU, -1 on bad arguments.  Replaces the reference's single acados solver per process
+ * workgroups at horizon N = CUs x min(LDS per CU / LDS per instance, the runtime's occupancy of the
+ * kernel sdfnmpc_ctx_qp_kernel picks -- registers and waves included), from hipDeviceProp_t and
+ * hipOccupancyMaxActiveBlocksPerMultiprocessor (1024 at N = 20 and 40 on an MI355X: the serial kernel's
+ * registers allow four instances per CU); 0 when N does not fit one CU, -1 on bad arguments.  Replaces the reference's single acados solver per process
  * (controller.py:16 builds one Ocp): a batch larger than this is split over devices (shard.plan). */
 long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N);
 /* rows per SDF workgroup: 32 (2 workgroups / CU) or 64 (1 workgroup / CU); default 32 */

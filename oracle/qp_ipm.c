@@ -626,10 +626,16 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     for (int i = 0; i < NX; ++i) Q.x0[i] = x0[i] - x[i];
 
     /* ---- starting point (rti_qp.hip's): dynamics-feasible with du = sl = su = 0 (o->ws: du = the du
-     * buffer's entry values); t = max(row, t0); lambda = l0 on box rows, max(l0, lc s_k zl_j) on the rows
+     * buffer's entry values, if all finite); t = max(row, t0); lambda = l0 on box rows, max(l0, lc s_k zl_j) on the rows
      * of soft group (k, j) */
     memcpy(zdx, Q.x0, sizeof(double) * NX);
-    if (o->ws) memcpy(zdu, du, sizeof(double) * N * NU);
+    if (o->ws) {
+        /* a du with a non-finite entry (the output of a failed QP) gives a cold start: a failure must not
+         * stick to the instance through the warm start */
+        int fin = 1;
+        for (int e = 0; e < N * NU; ++e) fin &= isfinite(du[e]) != 0;
+        if (fin) memcpy(zdu, du, sizeof(double) * N * NU);
+    }
     for (int k = 0; k < N; ++k)
         for (int a = 0; a < NX; ++a) {
             double s = Q.st[k].c[a];

@@ -108,7 +108,7 @@ static void bnorm(double* x, int C, long HW, const float* g, const float* b, con
 }
 
 static void relu(double* x, long n) {
-    for (long i = 0; i < n; ++i) x[i] = x[i] > 0.0 ? x[i] : 0.0;
+    for (long i = 0; i < n; ++i) x[i] = x[i] < 0.0 ? 0.0 : x[i];  /* torch.relu keeps a NaN */
 }
 
 /* ResBlock(size_in, stride), non-bottleneck (resnet.py:27-56) */
@@ -177,7 +177,7 @@ void orc_vae_encode(const float* pre, int B, int H, int W, const float* params, 
                             const int iy = oy * 2 - 1 + ky, ix = ox * 2 - 1 + kx;
                             if (iy < 0 || iy >= H1 || ix < 0 || ix >= W1) continue;
                             const double v = c1[((long)c * H1 + iy) * W1 + ix];
-                            m = v > m ? v : m;
+                            m = (v > m || v != v) ? v : m;  /* torch max_pool2d propagates a NaN */
                         }
                     mp[((long)c * H2 + oy) * W2 + ox] = m;
                 }

@@ -323,6 +323,10 @@ class Net:
         return float(load().sdfnmpc_net_max_df(self.h))
 
     @property
+    def size_latent(self) -> int:
+        return int(load().sdfnmpc_net_size_latent(self.h))
+
+    @property
     def fingerprint(self) -> int:
         return int(load().sdfnmpc_net_fingerprint(self.h))
 
@@ -332,7 +336,8 @@ class Net:
                                        _ptr(out4), _ptr(grad_latent)))
 
     def eval_host(self, inp: np.ndarray, want_grad=True):
-        """Host-pointer synchronous evaluation: inp [rows, 131] fp64 -> (df [rows], grad [rows,131])."""
+        """Host-pointer synchronous evaluation: inp [rows, 3 + L] fp64 -> (df [rows], grad [rows, 3 + L])
+        (L = size_latent, 128 for the deployed net: the 131 of jac_sdf_l4c)."""
         inp = np.ascontiguousarray(inp, dtype=np.float64)
         rows = inp.shape[0]
         df = np.empty(rows)

@@ -250,17 +250,41 @@ class Nmpc:
 
     def set_latent_device(self, latent, W_p_Bo, W_R_Bo, flag=None):
         """set_latent (+ set_sdf_flag) on the device buffers for every instance (controller.py:45-54);
-        latent: host array or a device array [B][L] fp64 (e.g. VaeWrapper's latents, no host round trip)."""
+        latent: host array or a device array [B][L] fp64 (e.g. VaeWrapper's latents, no host round trip).
+        With the batch split over devices (Ocp(devices=...), shard.plan) each part packs its own instance
+        rows on its own device: a device array on that device is read in place (a view at the part's first
+        row), one on another device goes through the host once."""
         from . import _lib
         Bn = max(self.B, 1)
         L = int(self.cfg.nn.size_latent)
-        lat = latent if hasattr(latent, "data_ptr") else np.reshape(latent, (Bn, L))
-        args = {"latent": self._dev(lat), "W_p_Bo": self._dev(np.reshape(W_p_Bo, (Bn, 3))),
-                "W_R_Bo": self._dev(np.reshape(W_R_Bo, (Bn, 9))), "p": self.ocp.field("p")}
+        cols = {"latent": L, "W_p_Bo": 3, "W_R_Bo": 9, "flag": 1}
+        given = {"latent": latent, "W_p_Bo": W_p_Bo, "W_R_Bo": W_R_Bo}
         if flag is not None:
-            args["flag"] = self._dev(np.broadcast_to(np.asarray(flag, float), (Bn,)))
-        _lib.pack_refs(self.ocp.ctx, _lib.ref_opts(self.cfg, -1), Bn, self.N, self.model.np, self.model.ny, args, L=L)
-        self.ocp.ctx.synchronize()
+            given["flag"] = flag if hasattr(flag, "data_ptr") else np.broadcast_to(np.asarray(flag, float), (Bn,))
+        host = {}
+        for k, v in given.items():
+            if not hasattr(v, "data_ptr"):
+                host[k] = np.reshape(np.asarray(v, dtype=np.float64), (Bn, cols[k]))
+            elif np.dtype(str(v.dtype).replace("torch.", "")) != np.float64:
+                raise TypeError(f"device input must be float64, got {v.dtype}")
+        parts = self.ocp.parts
+        for part in parts:
+            lo, nb = part.lo, part.hi - part.lo
+            args = {"p": part.solver.field("p")}
+            for k, v in given.items():
+                if k in host:
+                    args[k] = _lib.DeviceArray.from_numpy(part.ctx, np.ascontiguousarray(host[k][lo:part.hi]))
+                elif len(parts) == 1:
+                    args[k] = _lib.sync_producer(v)
+                elif _device_of(v) == part.ctx.device:  # a view of the part's rows, in place
+                    args[k] = _lib.FieldView(_lib.sync_producer(v).data_ptr() + lo * cols[k] * 8, (nb, cols[k]),
+                                             np.float64)
+                else:  # another device: through the host, once per array
+                    host[k] = _download(v, Bn, cols[k])
+                    args[k] = _lib.DeviceArray.from_numpy(part.ctx, np.ascontiguousarray(host[k][lo:part.hi]))
+            _lib.pack_refs(part.ctx, _lib.ref_opts(self.cfg, -1), nb, self.N, self.model.np, self.model.ny, args, L=L)
+        for part in parts:
+            part.ctx.synchronize()
         self._clean("pose", "latent", *(("flag",) if flag is not None else ()))
 
     def set_ref(self, ref, k, b=None):
@@ -280,3 +304,19 @@ class Nmpc:
             self.yN[sel] = y[: self.model.nyN]
             self._mark("yNref", b)
             self._mark("WN", b)
+
+
+def _device_of(a) -> int:
+    """HIP device of a device array: DeviceArray (its context's), torch tensor (its own), else 0."""
+    ctx = getattr(a, "ctx", None)
+    if ctx is not None:
+        return int(ctx.device)
+    dev = getattr(a, "device", None)
+    return int(getattr(dev, "index", 0) or 0)
+
+
+def _download(a, rows, cols):
+    """Host copy [rows][cols] fp64 of a device array (DeviceArray or torch tensor)."""
+    if hasattr(a, "numpy") and not type(a).__module__.startswith("torch"):
+        return np.reshape(a.numpy(), (rows, cols))
+    return np.reshape(a.detach().cpu().numpy(), (rows, cols))

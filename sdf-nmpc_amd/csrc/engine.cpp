@@ -14,6 +14,7 @@
 #include <cstring>
 #include <map>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -101,7 +102,9 @@ struct sdfnmpc_ctx {
         unsigned long long seq = 0;
         bool live = false;
         long long idle_ticks = 0, life_ticks = 0;
-        double idle_s = 0.02;
+        double idle_s = 0.001, life_s = 0.0008;  // SDFNMPC_SDF_SERVER_IDLE_MS / _LIFE_MS
+        unsigned long long epoch = 0;           // launches so far; the live server's is in `gone` once it left
+        bool abandoned = false;                 // a server that would not stop: its mailbox is never reused
         double khz = 100000.0;
         std::chrono::steady_clock::time_point last{};
         double acc[4] = {0, 0, 0, 0};  // diagnostics: us staging, computing, host round trip; calls
@@ -199,19 +202,36 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
     return SDFNMPC_OK;
 }
 
-static void srv_stop(sdfnmpc_ctx* ctx) {  // ask the resident SDF server to exit and wait for it
-    if (!ctx->srv.mb) return;
-    __atomic_store_n(&ctx->srv.mb->stop, 1ull, __ATOMIC_RELEASE);
-    (void)hipStreamSynchronize(ctx->srv.stream);
-    __atomic_store_n(&ctx->srv.mb->stop, 0ull, __ATOMIC_RELEASE);
-    ctx->srv.live = false;
+// Ask the resident SDF server to exit and wait for it, polling with a deadline (a server that stopped
+// answering must not hang destroy / reconfigure while the shim's lock is held): on timeout the mailbox
+// and stream are abandoned -- never freed or reused, since the server may still write to them -- and
+// the host path falls back to one launch per call.  Returns false on timeout.
+static bool srv_stop(sdfnmpc_ctx* ctx) {
+    auto& S = ctx->srv;
+    if (!S.mb || S.abandoned) return !S.abandoned;
+    __atomic_store_n(&S.mb->stop, 1ull, __ATOMIC_RELEASE);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t q = hipStreamQuery(S.stream);
+        if (q != hipErrorNotReady) break;
+        if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > 2.0) {
+            S.abandoned = true;
+            S.live = false;
+            S.mode = 0;
+            fail(SDFNMPC_E_HIP, "sdf server: did not stop within 2 s; abandoned (one launch per call from now on)");
+            return false;
+        }
+        std::this_thread::yield();
+    }
+    __atomic_store_n(&S.mb->stop, 0ull, __ATOMIC_RELEASE);
+    S.live = false;
+    return true;
 }
 
 extern "C" void sdfnmpc_ctx_destroy(sdfnmpc_ctx* ctx) {
     if (!ctx) return;
     ScopedDevice sd(ctx->device);
-    if (ctx->srv.mb) {
-        srv_stop(ctx);
+    if (ctx->srv.mb && srv_stop(ctx)) {
         (void)hipStreamDestroy(ctx->srv.stream);
         (void)hipHostFree(ctx->srv.mb);
     }
@@ -335,9 +355,16 @@ extern "C" long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N) {
     if (!ctx || N < 1) return -1;
     if (ctx->n_cu <= 0 || ctx->lds_per_cu == 0) return -1;
     // a batch that fills the device: the kernel AUTO picks above SDFNMPC_QP_SEG_AUTO_MAX_B
-    const size_t per = sdfnmpc_ctx_qp_kernel(ctx, N, 1 << 30) == SDFNMPC_QP_SEGMENTED ? qp_seg_lds_bytes(N) : qp_lds_bytes(N);
+    const bool seg = sdfnmpc_ctx_qp_kernel(ctx, N, 1 << 30) == SDFNMPC_QP_SEGMENTED;
+    const size_t per = seg ? qp_seg_lds_bytes(N) : qp_lds_bytes(N);
     if (per == 0 || per > ctx->lds_per_cu) return 0;  // the horizon does not fit one CU's LDS
-    return (long long)ctx->n_cu * (long long)(ctx->lds_per_cu / per);
+    // the runtime's occupancy of the kernel (LDS, registers and waves at once): the serial kernel's 375
+    // registers allow one wave per SIMD, four instances per CU, whatever the LDS would admit; the segmented
+    // kernel's __launch_bounds__ two or three workgroups per CU
+    ScopedDevice sd(ctx->device);
+    const int occ = seg ? rti_qp_seg_blocks_per_cu(N) : rti_qp_blocks_per_cu(N);
+    const long long by_lds = (long long)(ctx->lds_per_cu / per);
+    return (long long)ctx->n_cu * std::min<long long>(by_lds, occ > 0 ? occ : 0);
 }
 
 extern "C" int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows) {
@@ -395,14 +422,15 @@ namespace {
 
 struct HostNet {
     int nb_states = 3, L = 0, n1 = 0, n2 = 0, n3 = 0, n4 = 0, nf = 0, nd = 0;
-    int res = 0;  // 0 'full' [h2 | e | z], 1 'state' [h2 | e], 2 'latent' [h2 | z] into layer 3 (neural_df.py:76-78)
+    int res = 0;  // 0 'full' [h2 | e | z], 1 'state' [h2 | e], 2 'latent' [h2 | z], 3 plain MLP [h2] into layer 3
+                  // (neural_df.py:76-78: any other `res` value)
     int act = 0;  // 0 sin(w0 .), 1 relu, 2 softplus (neural_df.py:40-47)
     float w0 = 0, max_df = 1;
     std::vector<float> dirs, freqs;                           // [3][nd], [nf]
     std::vector<float> W1, b1, W2, b2, W3, b3, W4, b4, W5, b5;  // torch order / shapes
     int E() const { return 3 + 2 * nd * nf; }
-    bool e3() const { return res != 2; }  // layer 3 sees the embedding
-    bool z3() const { return res != 1; }  // layer 3 sees the latent
+    bool e3() const { return res == 0 || res == 1; }  // layer 3 sees the embedding
+    bool z3() const { return res == 0 || res == 2; }  // layer 3 sees the latent
     int c3() const { return n2 + (e3() ? E() : 0) + (z3() ? L : 0); }  // W3 row length
 };
 
@@ -437,7 +465,8 @@ void alloc_params(HostNet& h) {
 // sdf_mlp.hip / sdf_row.hip kernels.  Every other architecture -- config C5's [1024,1024,512,256], and the
 // reference's variants: any layer sizes (zero-padded to multiples of 128: the padded units' outgoing
 // weights are zero, so they change nothing), embeddings none / pos / cube / oct / dod / ico with any
-// frequency count, res full / state / latent, activations sin / relu / softplus -- runs the layer-by-layer
+// frequency count, res full / state / latent / none (a plain MLP), any size_latent, activations sin / relu /
+// softplus -- runs the layer-by-layer
 // GEMM schedule of sdf_wide.hip ("wide" below means exactly that: not the deployed net).
 bool is_deployed(const HostNet& h) {
     return h.n1 == N1 && h.n2 == N2 && h.n3 == N3 && h.n4 == N4 && h.nd == EMB_ND && h.nf == EMB_NF && h.res == 0 &&
@@ -446,13 +475,14 @@ bool is_deployed(const HostNet& h) {
 bool is_wide(const HostNet& h) { return !is_deployed(h); }
 int pad128(int n) { return (n + 127) / 128 * 128; }
 
+constexpr int L_MAX = 1024;  // size_latent bound (the wide schedule pads it to a multiple of 128)
 int check_supported(const HostNet& h) {
-    if (h.nb_states != 3 || h.L != L || h.E() > 256 || h.res < 0 || h.res > 2 || h.act < 0 || h.act > 2) {
+    if (h.nb_states != 3 || h.L < 1 || h.L > L_MAX || h.E() > 256 || h.res < 0 || h.res > 3 || h.act < 0 || h.act > 2) {
         char buf[256];
         snprintf(buf, sizeof buf,
                  "network architecture (states %d, latent %d, embedding features %d, res %d, act %d) is not built "
-                 "for; this build supports 3 states, latent 128, at most 256 embedding features",
-                 h.nb_states, h.L, h.E(), h.res, h.act);
+                 "for; this build supports 3 states, latent 1..%d, at most 256 embedding features",
+                 h.nb_states, h.L, h.E(), h.res, h.act, L_MAX);
         return fail(SDFNMPC_E_UNSUPPORTED, buf);
     }
     return SDFNMPC_OK;
@@ -556,6 +586,7 @@ struct WideDev {  // plain row-major [N][K] fp32 operands of the wide schedule (
     int P1 = 0, P2 = 0, P3 = 0, P4 = 0;  // layer widths padded to multiples of 128
     int NEK = NE, NEB = 128;             // embedding width as a K segment / as the d e GEMMs' output
     int nb = 0;                          // projected frequencies (n_dirs x nb_freqs)
+    int LH = L, LZ = L;                  // size_latent, and padded to a multiple of 128 (the GEMMs' K / N)
     bool e3 = true;                      // layer 3 sees the embedding (res 'full' / 'state')
     int act = 0;                         // 0 sin, 1 relu, 2 softplus
 };
@@ -612,7 +643,7 @@ static uint64_t net_fingerprint(HostNet& h) {  // FNV-1a over the parameters in 
 static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     // layer widths zero-padded to multiples of 128 (the GEMM's column tile), the embedding to NEK (a
     // multiple of 32) as a K segment and to NEB (a multiple of 128) as the d e GEMMs' output width
-    const int n1 = h.n1, n2 = h.n2, n3 = h.n3, n4 = h.n4, E = h.E(), c1 = E + L, c3 = h.c3();
+    const int n1 = h.n1, n2 = h.n2, n3 = h.n3, n4 = h.n4, E = h.E(), Lh = h.L, LZ = pad128(Lh), c1 = E + Lh, c3 = h.c3();
     const int P1 = pad128(n1), P2 = pad128(n2), P3 = pad128(n3), P4 = pad128(n4);
     const int NEK = std::max(96, (E + 31) / 32 * 32), NEB = pad128(E);
     const bool e3 = h.e3(), z3 = h.z3();
@@ -643,11 +674,13 @@ static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     mat(NEB, P3, [&](int j, int k) { return e3 && j < E && k < n3 ? W3[(size_t)k * c3 + n2 + j] : 0.0f; });      // B3e
     mat(P1, P2, [&](int j, int k) { return j < n1 && k < n2 ? W2[(size_t)k * n1 + j] : 0.0f; });                 // B2
     mat(NEB, P1, [&](int j, int k) { return j < E && k < n1 ? W1[(size_t)k * c1 + j] : 0.0f; });                 // B1e
-    mat(L, P1 + P3, [&](int j, int k) {  // Bz: d z = [delta1 | delta3] . [W1z ; W3z] (the 131-wide jac_sdf_l4c)
+    mat(LZ, P1 + P3, [&](int j, int k) {  // Bz: d z = [delta1 | delta3] . [W1z ; W3z] (the 131-wide jac_sdf_l4c)
+        if (j >= Lh) return 0.0f;
         if (k < P1) return k < n1 ? W1[(size_t)k * c1 + E + j] : 0.0f;
         return z3 && k - P1 < n3 ? W3[(size_t)(k - P1) * c3 + z3off + j] : 0.0f;
     });
-    mat(P1 + P3, L, [&](int j, int k) {                                                                          // Hz
+    mat(P1 + P3, LZ, [&](int j, int k) {                                                                         // Hz
+        if (k >= Lh) return 0.0f;
         if (j < P1) return j < n1 ? W1[(size_t)j * c1 + E + k] : 0.0f;
         return z3 && j - P1 < n3 ? W3[(size_t)(j - P1) * c3 + z3off + k] : 0.0f;
     });
@@ -683,7 +716,7 @@ static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     w.Hz = d + off[i++]; w.bz = d + off[i++]; w.b2 = d + off[i++]; w.b4 = d + off[i++]; w.w5 = d + off[i++];
     w.emb_tab = (const float4*)(d + off[i++]);
     w.P1 = P1; w.P2 = P2; w.P3 = P3; w.P4 = P4; w.NEK = NEK; w.NEB = NEB;
-    w.nb = h.nd * h.nf; w.e3 = e3; w.act = h.act;
+    w.nb = h.nd * h.nf; w.e3 = e3; w.act = h.act; w.LH = Lh; w.LZ = LZ;
     net->args.b5 = h.b5[0];
     net->args.w0 = h.w0;
     net->fingerprint = net_fingerprint(h);
@@ -883,9 +916,11 @@ static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, co
     if (rows > 0x7fffffffLL / 2) return fail(SDFNMPC_E_ARG, "too many rows");
     const WideDev& w = net->wd;
     const int n1 = w.P1, n2 = w.P2, n3 = w.P3, n4 = w.P4, nz = n1 + n3, R = (int)rows;
-    const int NEK = w.NEK, NEB = w.NEB;
-    const size_t per_row = 2 * (size_t)NEK + 2 * (size_t)(n1 + n2 + n3 + n4) + 2 * (size_t)NEB;
-    const size_t nfl = per_row * rows + (size_t)n_inst * (L + nz);
+    const int NEK = w.NEK, NEB = w.NEB, LH = w.LH, LZ = w.LZ;
+    const bool zpad = LH != LZ;  // size_latent not a multiple of 128: padded latent and d z staging
+    const size_t per_row = 2 * (size_t)NEK + 2 * (size_t)(n1 + n2 + n3 + n4) + 2 * (size_t)NEB +
+                           (zpad && glat ? (size_t)LZ : 0);
+    const size_t nfl = per_row * rows + (size_t)n_inst * (LZ + nz);
     HIPCHK(ctx->wws.ensure(nfl * sizeof(float)));
     float* q = (float*)ctx->wws.p;
     auto take = [&](size_t n) { float* r = q; q += n; return r; };
@@ -893,11 +928,15 @@ static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, co
     float *H1 = take((size_t)R * n1), *D1 = take((size_t)R * n1), *H2 = take((size_t)R * n2), *D2 = take((size_t)R * n2);
     float *H3 = take((size_t)R * n3), *D3 = take((size_t)R * n3), *H4 = take((size_t)R * n4), *D4 = take((size_t)R * n4);
     float *GE3 = take((size_t)R * NEB), *GE1 = take((size_t)R * NEB);
-    float* z = take((size_t)n_inst * L);
+    float* z = take((size_t)n_inst * LZ);
     float* c13 = take((size_t)n_inst * nz);
+    float* gz = (zpad && glat) ? take((size_t)R * LZ) : glat;  // d df / d z before its padding is cut off
     hipStream_t st = ctx->stream;
     if (zd) {
-        HIPCHK(timed(ctx, "sdf_wide_hoist", [&] { return launch_wide_latent(zd, zstride, n_inst, z, st); }));
+        HIPCHK(timed(ctx, "sdf_wide_hoist", [&] { return launch_wide_latent<double>(zd, zstride, n_inst, LH, LZ, z, st); }));
+        zf = z;
+    } else if (zpad) {  // fp32 [n_inst][LH] -> [n_inst][LZ]
+        HIPCHK(timed(ctx, "sdf_wide_hoist", [&] { return launch_wide_latent<float>(zf, LH, n_inst, LH, LZ, z, st); }));
         zf = z;
     }
     const float w0 = net->args.w0;
@@ -913,7 +952,7 @@ static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, co
         g.out1 = o1; g.ld1 = N; g.out2 = o2; g.ld2 = N; g.w0 = w0; g.act = w.act;
         return timed(ctx, name, [&] { return launch_wide_gemm(g, epi, st); });
     };
-    HIPCHK(gemm(zf, L, nullptr, 0, w.Hz, n_inst, nz, WIDE_EPI_STORE, w.bz, nullptr, nullptr, 0, c13, nullptr,
+    HIPCHK(gemm(zf, LZ, nullptr, 0, w.Hz, n_inst, nz, WIDE_EPI_STORE, w.bz, nullptr, nullptr, 0, c13, nullptr,
                 "sdf_wide_hoist"));
     WideSdfArgs ea{};
     ea.rows = R; ea.n4 = n4; ea.pos = pos4; ea.emb_tab = w.emb_tab; ea.E = Eb; ea.G = Gb;
@@ -937,9 +976,13 @@ static int run_wide(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, long long rows, co
     HIPCHK(gemm(H2, n2, nullptr, 0, w.B2, R, n1, WIDE_EPI_BWD, nullptr, nullptr, D1, n1, H1, nullptr, "sdf_wide_gemm"));
     HIPCHK(gemm(H1, n1, nullptr, 0, w.B1e, R, NEB, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, GE1, nullptr,
                 "sdf_wide_gemm"));
-    if (glat)  // d df / d z = delta1 W1z + delta3 W3z: one GEMM over the two K segments [delta1 | delta3]
-        HIPCHK(gemm(H1, n1, H3, n3, w.Bz, R, L, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, glat, nullptr,
+    if (glat) {  // d df / d z = delta1 W1z + delta3 W3z: one GEMM over the two K segments [delta1 | delta3]
+        HIPCHK(gemm(H1, n1, H3, n3, w.Bz, R, LZ, WIDE_EPI_STORE, nullptr, nullptr, nullptr, 0, gz, nullptr,
                     "sdf_wide_gemm"));
+        if (zpad)
+            HIPCHK(hipMemcpy2DAsync(glat, (size_t)LH * sizeof(float), gz, (size_t)LZ * sizeof(float),
+                                    (size_t)LH * sizeof(float), (size_t)R, hipMemcpyDeviceToDevice, st));
+    }
     ea.H4 = H4; ea.GE3 = GE3; ea.GE1 = GE1; ea.w5 = w.w5; ea.b5 = net->args.b5; ea.out = out4;
     HIPCHK(timed(ctx, "sdf_wide_final", [&] { return launch_wide_final(ea, st); }));
     return SDFNMPC_OK;
@@ -984,15 +1027,21 @@ static bool srv_enabled(sdfnmpc_ctx* ctx) {
             const double v = atof(ms);
             if (v > 0.0) ctx->srv.idle_s = v * 1e-3;
         }
+        if (const char* ms = getenv("SDFNMPC_SDF_SERVER_LIFE_MS")) {
+            const double v = atof(ms);
+            if (v > 0.0) ctx->srv.life_s = v * 1e-3;
+        }
     }
-    return ctx->srv.mode == 1;
+    return ctx->srv.mode == 1 && !ctx->srv.abandoned;
 }
 
 // One request to the resident SDF server (sdf_row.hip): the staged fp32 request (hp [rows][4], hl
 // [rows][L]) goes into the mailbox, the results come back into ho in the staged path's layout.  The
 // server is (re)launched when it is not running -- first call, a different network, or after it left on
-// its idle timeout; a server that exits while a request is posted is relaunched and serves it (it
-// serves every seq_in above the seq_out it finds).
+// its idle timeout or its life bound (1 ms and 0.8 ms by default: the longest a device-wide synchronisation
+// elsewhere in the process waits for it); a server that exits while a request is posted writes its epoch
+// to `gone`, and the caller relaunches at once (the new server serves every seq_in above the seq_out it
+// finds).
 static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const float* hp, const float* hl, bool grad,
                     float* ho) {
     using clk = std::chrono::steady_clock;
@@ -1009,11 +1058,17 @@ static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const fl
         if (khz <= 0) khz = 100000;
         S.khz = khz;
         S.idle_ticks = (long long)(S.idle_s * khz * 1e3);
-        S.life_ticks = (long long)(10.0 * khz * 1e3);  // relaunched at most every 10 s
+        S.life_ticks = (long long)(S.life_s * khz * 1e3);
         S.seq = 0;
         S.live = false;
     }
-    if (S.live && S.net != net->uid) srv_stop(ctx);
+    if (S.live && S.net != net->uid && !srv_stop(ctx)) return SDFNMPC_E_HIP;
+    if (S.live && __atomic_load_n(&S.mb->gone, __ATOMIC_ACQUIRE) == S.epoch) {
+        // it left (idle, life or stop) after publishing its last answer: nothing of it runs any more but
+        // its kernel's exit, which the stream orders before the relaunch
+        S.live = false;
+        __atomic_store_n(&S.mb->stop, 0ull, __ATOMIC_RELEASE);
+    }
     if (S.live && (S.mb->stop || std::chrono::duration<double>(clk::now() - S.last).count() > 0.5 * S.idle_s)) {
         const hipError_t q = hipStreamQuery(S.stream);
         if (q == hipSuccess) {
@@ -1032,19 +1087,29 @@ static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const fl
     const unsigned long long seq = ++S.seq;
     __atomic_store_n(&S.mb->seq_in, seq, __ATOMIC_RELEASE);
     SdfRowArgs ra = net->row;
+    auto relaunch = [&]() {
+        ++S.epoch;
+        return launch_sdf_server(ra, S.mb_dev, S.idle_ticks, S.life_ticks, S.epoch, S.stream);
+    };
     if (!S.live) {
-        HIPCHK(launch_sdf_server(ra, S.mb_dev, S.idle_ticks, S.life_ticks, S.stream));
+        HIPCHK(relaunch());
         S.live = true;
         S.net = net->uid;
     }
     const auto t0 = clk::now();
     for (unsigned long spin = 1;; ++spin) {
         if (__atomic_load_n(&S.mb->seq_out, __ATOMIC_ACQUIRE) == seq) break;
+        if (__atomic_load_n(&S.mb->gone, __ATOMIC_ACQUIRE) == S.epoch) {
+            // the server left between requests (idle / life) without seeing this one: relaunch now
+            if (__atomic_load_n(&S.mb->seq_out, __ATOMIC_ACQUIRE) == seq) break;
+            HIPCHK(relaunch());
+            continue;
+        }
         if ((spin & 1023) == 0) {
             const hipError_t q = hipStreamQuery(S.stream);
             if (q == hipSuccess) {  // the server left before it saw this request
                 if (__atomic_load_n(&S.mb->seq_out, __ATOMIC_ACQUIRE) == seq) break;
-                HIPCHK(launch_sdf_server(ra, S.mb_dev, S.idle_ticks, S.life_ticks, S.stream));
+                HIPCHK(relaunch());
             } else if (q != hipErrorNotReady) {
                 S.live = false;
                 return fail(SDFNMPC_E_HIP, std::string("sdf server: ") + hipGetErrorString(q));
@@ -1090,7 +1155,7 @@ extern "C" int sdfnmpc_ctx_set_sdf_server(sdfnmpc_ctx* ctx, int on) {
     if (!ctx || on < 0 || on > 1) return fail(SDFNMPC_E_ARG, "bad sdfnmpc_ctx_set_sdf_server arguments");
     std::lock_guard<std::mutex> lk(ctx->mu);
     ScopedDevice sd(ctx->device);
-    if (!on) srv_stop(ctx);
+    if (!on && !srv_stop(ctx)) return SDFNMPC_E_HIP;
     ctx->srv.mode = on;
     return SDFNMPC_OK;
 }
@@ -1101,7 +1166,7 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
     if (rows == 0) return SDFNMPC_OK;
     std::lock_guard<std::mutex> lk(ctx->mu);
     ScopedDevice sd(ctx->device);
-    const int D = 3 + L;
+    const int L = net->host.L, D = 3 + L;  // 131 for the deployed net (and every 128-latent one)
     // pinned staging: in [rows][4] pos | [rows][L] latent, out [rows][4] (df, d/dpos) | [rows][L] d/dlatent
     // (double -> float as L4CasADi does); one copy each way, one synchronisation
     const size_t nin = (size_t)rows * (4 + L), bytes = 2 * nin * sizeof(float);

@@ -65,6 +65,8 @@ __host__ __device__ inline size_t qp_lds_doubles(int N) {
 __host__ __device__ inline size_t qp_lds_bytes(int N) { return qp_lds_doubles(N) * sizeof(double); }
 size_t qp_seg_lds_bytes(int N);  // LDS per instance of the segmented kernel chosen for N (static; 0: unsupported)
 
+int rti_qp_blocks_per_cu(int N);      // instances per CU the serial IPM runs at once (0: does not fit)
+int rti_qp_seg_blocks_per_cu(int N);  // the same for the segmented IPM
 hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s);  // stage records into the workspace
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s);       // the IPM (after launch_rti_qp_pack)
 bool rti_qp_seg_supported(int N);                               // the segmented IPM handles this horizon

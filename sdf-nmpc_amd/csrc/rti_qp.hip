@@ -292,7 +292,10 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
 #define RSTAMP(i)
 #endif
 
-__global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
+#ifndef QP_LB_WAVES  // diagnostic: minimum waves per SIMD the register allocation must allow
+#define QP_LB_WAVES 1
+#endif
+__global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     extern __shared__ __align__(16) double lds_q[];
     STAMP_DECL
     const int b = blockIdx.x, lane = threadIdx.x;
@@ -304,9 +307,18 @@ __global__ __launch_bounds__(64) void rti_qp_kernel(QpArgs A) {
     const __amdgpu_buffer_rsrc_t rsF = __builtin_amdgcn_make_buffer_rsrc(F, (short)0, N1 * FREC * 8, 0x00020000);
 
     // ------------------------------------------------------------ per-node constants into LDS
-    for (int e = lane; e < N * NU; e += 64) {
-        s.uu[e] = A.u[(size_t)b * N * NU + e];
-        s.du[e] = A.warm_start ? A.du[(size_t)b * N * NU + e] : 0.0;  // primal warm start: the previous QP's du
+    {
+        // primal warm start: the previous QP's du -- unless it holds a non-finite entry (a failed QP's
+        // output), which gives a cold start, so a failure does not stick to the instance
+        bool fin = true;
+        for (int e = lane; e < N * NU; e += 64) {
+            s.uu[e] = A.u[(size_t)b * N * NU + e];
+            const double v = A.warm_start ? A.du[(size_t)b * N * NU + e] : 0.0;
+            fin = fin && __builtin_isfinite(v);
+            s.du[e] = v;
+        }
+        if (__builtin_amdgcn_ballot_w64(!fin) != 0)
+            for (int e = lane; e < N * NU; e += 64) s.du[e] = 0.0;
     }
     for (int e = lane; e < N1 * NS; e += 64) s.hv[e] = A.h[(size_t)b * N1 * NS + e];
     {
@@ -1119,6 +1131,17 @@ hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(rti_qp_pack_kernel, dim3((unsigned)((a.B * (a.N + 1) + PACK_NODES - 1) / PACK_NODES)),
                        dim3(64 * PACK_NODES), 0, s, a);
     return hipGetLastError();
+}
+
+int rti_qp_blocks_per_cu(int N) {
+    // every limit at once (LDS per instance, the 375-register allocation: one wave per SIMD, waves per CU),
+    // as the runtime applies them
+    const size_t lds = qp_lds_bytes(N);
+    if (hipFuncSetAttribute((const void*)rti_qp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
+        return 0;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rti_qp_kernel, 64, lds) != hipSuccess) return 0;
+    return n;
 }
 
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s) {

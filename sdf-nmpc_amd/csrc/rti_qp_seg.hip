@@ -297,7 +297,15 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     if (tid < NX) s.dxc[tid] = A.x0[(size_t)b * 10 + tid] - A.x[(size_t)b * N1 * 10 + tid];
     // du of the start iterate into dua (free until the first forward sweep): 0, or on a primal warm start
     // the previous QP's du as found in A.du (qp_solver_warm_start, ocp.py:116)
-    for (int e = tid; e < N * NU; e += 64 * NSEG) s.dua[e] = A.warm_start ? A.du[(size_t)b * N * NU + e] : 0.0;
+    // (a du with a non-finite entry, a failed QP's output, gives a cold start: the failure does not stick)
+    int nonfin = 0;
+    for (int e = tid; e < N * NU; e += 64 * NSEG) {
+        const double v = A.warm_start ? A.du[(size_t)b * N * NU + e] : 0.0;
+        nonfin |= !__builtin_isfinite(v);
+        s.dua[e] = v;
+    }
+    if (__syncthreads_or(nonfin))
+        for (int e = tid; e < N * NU; e += 64 * NSEG) s.dua[e] = 0.0;
     wg_sync();
     // row constants: box rows at du = 0 (dlo, dup), soft rows at C dx = 0 (hl0, hu0), slack weights
     auto dlo = [&]() { return ubv - s.cst[ib]; };
@@ -1071,8 +1079,9 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     wg_sync();
     for (int e = lane; e < nn * NX; e += 64) A.dx[((size_t)b * N1 + sa) * NX + e] = s.dxc[sa * NX + e];
     const int nu_ = (sb < N ? sb : N) - sa;
-    if (!A.warm_start)
-        for (int e = lane; e < nu_ * NU; e += 64) A.du[((size_t)b * N + sa) * NU + e] = 0.0;
+    // the iterate's du lives in A.du: the start point (0 cold; the entry values on a warm start, unless
+    // they held a non-finite entry)
+    for (int e = lane; e < nu_ * NU; e += 64) A.du[((size_t)b * N + sa) * NU + e] = s.dua[sa * NU + e];
     double rp = 0.0;
     {
         double rl = 0.0;
@@ -1410,6 +1419,24 @@ size_t qp_seg_lds_bytes(int N) {
     for (const SegCfg& c : SEG_CFGS)
         if (c.P == P) return seg_lds_bytes(c.P, c.NMAX);
     return 0;
+}
+
+template <int P, int NMAX>
+static int seg_blocks_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rti_qp_seg_kernel<P, NMAX>, 64 * P, 0) != hipSuccess) return 0;
+    return n;
+}
+
+// workgroups (instances) per CU at horizon N: the minimum of the LDS, register (__launch_bounds__) and wave
+// limits, as the runtime applies them
+int rti_qp_seg_blocks_per_cu(int N) {
+    switch (rti_qp_seg_count(N)) {
+        case 2: return seg_blocks_per_cu<2, 31>();
+        case 3: return seg_blocks_per_cu<3, 47>();
+        case 4: return seg_blocks_per_cu<4, 63>();
+        default: return 0;
+    }
 }
 
 template <int P, int NMAX>

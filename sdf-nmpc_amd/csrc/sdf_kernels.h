@@ -100,9 +100,10 @@ struct alignas(128) SdfMbox {
     unsigned long long seq_out;
     unsigned long long pad1[15];
     unsigned long long stop;
+    unsigned long long gone;             // the server writes its launch epoch here when it exits
     int rows, grad;
     long long t_seen, t_staged, t_done;  // server wall-clock stamps of the last request (diagnostics)
-    unsigned long long pad2[11];
+    unsigned long long pad2[10];
     long long t_phase[16];               // row_eval's phase stamps of the last request (diagnostics)
     float in[SDF_ROW_MAX * (4 + 128)];   // [rows][4] Co_p_B | [rows][L] latent
     float out[SDF_ROW_MAX * (4 + 128)];  // [rows][4] (df, d df / d pos) | [rows][L] d df / d latent
@@ -156,7 +157,8 @@ struct WideSdfArgs {
 };
 
 hipError_t launch_wide_gemm(const WideGemmArgs& a, int epi, hipStream_t s);
-hipError_t launch_wide_latent(const double* lat, long long stride, int n_inst, float* z, hipStream_t s);
+template <typename T>  // double (stage parameters) or float
+hipError_t launch_wide_latent(const T* lat, long long stride, int n_inst, int lh, int lz, float* z, hipStream_t s);
 hipError_t launch_wide_emb(const WideSdfArgs& a, hipStream_t s);
 hipError_t launch_wide_final(const WideSdfArgs& a, hipStream_t s);
 
@@ -165,7 +167,7 @@ hipError_t sdf_set_lds_limits();
 hipError_t launch_sdf_mlp(const SdfArgs& a, int M, bool latent_grad, hipStream_t s);
 hipError_t launch_sdf_row(const SdfRowArgs& a, hipStream_t s);
 hipError_t launch_sdf_server(const SdfRowArgs& a, SdfMbox* mb_dev, long long idle_ticks, long long life_ticks,
-                             hipStream_t s);
+                             unsigned long long epoch, hipStream_t s);
 template <typename T>
 hipError_t launch_hoist(const HoistArgs<T>& a, hipStream_t s);
 

@@ -330,9 +330,12 @@ __device__ __forceinline__ void mb_store(long long* p, long long v) {
 // The resident server (SdfMbox, sdf_kernels.h): thread 0 polls seq_in; the request is staged into LDS
 // with one PCIe read per word; the rows are evaluated by row_eval with the outputs written straight into
 // the mailbox; after a system-scope fence seq_out publishes them.  Every exit path (stop, idle, life) is
-// taken by the whole workgroup together (the decision goes through LDS behind a barrier).
+// taken by the whole workgroup together (the decision goes through LDS behind a barrier), between
+// requests, and ends with the launch's epoch stored to `gone`, so a caller that posted a request the
+// leaving server did not see relaunches at once instead of waiting for the stream to drain.  The life
+// bound (0.8 ms by default) is what a device-wide synchronisation elsewhere in the process can wait.
 __global__ __launch_bounds__(64 * RW) void sdf_server_kernel(SdfRowArgs A, SdfMbox* mb, long long idle,
-                                                              long long life) {
+                                                              long long life, unsigned long long epoch) {
     __shared__ __align__(16) float s_in[SDF_ROW_MAX * (4 + L)], s_out[SDF_ROW_MAX * (4 + L)];
     __shared__ unsigned long long s_seq;
     __shared__ int s_go, s_rows, s_grad;
@@ -363,7 +366,13 @@ __global__ __launch_bounds__(64 * RW) void sdf_server_kernel(SdfRowArgs A, SdfMb
             }
         }
         __syncthreads();
-        if (!s_go) break;
+        if (!s_go) {
+            if (threadIdx.x == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(&mb->gone, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+            break;
+        }
         const long long t_seen = wall_clock64();
         const int rows = s_rows;
         for (int i = threadIdx.x; i < rows * (4 + L); i += 64 * RW)
@@ -408,8 +417,8 @@ __global__ __launch_bounds__(64 * RW) void sdf_server_kernel(SdfRowArgs A, SdfMb
 }
 
 hipError_t launch_sdf_server(const SdfRowArgs& a, SdfMbox* mb_dev, long long idle_ticks, long long life_ticks,
-                             hipStream_t s) {
-    hipLaunchKernelGGL(sdf_server_kernel, dim3(1), dim3(64 * RW), 0, s, a, mb_dev, idle_ticks, life_ticks);
+                             unsigned long long epoch, hipStream_t s) {
+    hipLaunchKernelGGL(sdf_server_kernel, dim3(1), dim3(64 * RW), 0, s, a, mb_dev, idle_ticks, life_ticks, epoch);
     return hipGetLastError();
 }
 

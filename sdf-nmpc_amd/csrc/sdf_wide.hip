@@ -186,12 +186,15 @@ hipError_t launch_wide_gemm(const WideGemmArgs& a, int epi, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// latent (fp64, strided) -> fp32 [n_inst][L]
-__global__ void wide_latent_kernel(const double* lat, long long stride, int n_inst, float* z) {
+// latent (fp64 stage parameters or fp32, strided, lh entries) -> fp32 [n_inst][lz], zero past lh: a
+// size_latent below the GEMMs' 128-multiple K is zero-padded (the padded columns of Hz / rows of Bz are
+// zero too, so they add exact zeros)
+template <typename T>
+__global__ void wide_latent_kernel(const T* lat, long long stride, int n_inst, int lh, int lz, float* z) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (long long)n_inst * L) return;
-    const long long inst = i / L, k = i - inst * L;
-    z[i] = (float)lat[inst * stride + k];
+    if (i >= (long long)n_inst * lz) return;
+    const long long inst = i / lz, k = i - inst * lz;
+    z[i] = k < lh ? (float)lat[inst * stride + k] : 0.0f;
 }
 
 // positional embedding e (embeddings.py:106-111) and its derivative factors, nek features per row
@@ -274,12 +277,16 @@ __global__ __launch_bounds__(256) void wide_final_kernel(WideSdfArgs a) {
     }
 }
 
-hipError_t launch_wide_latent(const double* lat, long long stride, int n_inst, float* z, hipStream_t s) {
+template <typename T>
+hipError_t launch_wide_latent(const T* lat, long long stride, int n_inst, int lh, int lz, float* z, hipStream_t s) {
     if (n_inst <= 0) return hipSuccess;
-    const long long n = (long long)n_inst * L;
-    hipLaunchKernelGGL(wide_latent_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lat, stride, n_inst, z);
+    const long long n = (long long)n_inst * lz;
+    hipLaunchKernelGGL(wide_latent_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, lat, stride, n_inst,
+                       lh, lz, z);
     return hipGetLastError();
 }
+template hipError_t launch_wide_latent<double>(const double*, long long, int, int, int, float*, hipStream_t);
+template hipError_t launch_wide_latent<float>(const float*, long long, int, int, int, float*, hipStream_t);
 
 hipError_t launch_wide_emb(const WideSdfArgs& a, hipStream_t s) {
     if (a.rows <= 0) return hipSuccess;

@@ -122,7 +122,10 @@ __global__ __launch_bounds__(256) void vae_stem_kernel(VaeStemArgs a) {
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx) m = fmaxf(m, conv[((2 * pyl + dy) * ST_CX + 2 * pxl + dx) * ST_CS + c]);
+            for (int dx = 0; dx < 3; ++dx) {  // NaN-sticky, as torch's max_pool2d (fmaxf would drop it)
+                const float v = conv[((2 * pyl + dy) * ST_CX + 2 * pxl + dx) * ST_CS + c];
+                m = (v > m || v != v) ? v : m;
+            }
         a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c] = m;
     }
 }
@@ -327,7 +330,7 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
                     const size_t o = (size_t)m * a.Cout + n;
                     float v = acc[i][j][r] + bias;
                     if (a.resid) v += a.resid[o];
-                    if (a.relu) v = fmaxf(v, 0.f);
+                    if (a.relu) v = v < 0.f ? 0.f : v;  // torch.relu keeps a NaN (fmaxf would drop it)
                     a.out[o] = v;
                 }
             }

@@ -28,7 +28,15 @@ MAGIC = b"SDFNMPCW"
 VERSION = 1  # res='full', act='sin' networks (every deployed / C5 blob); version 2 adds the activation
 _HDR = struct.Struct("<8s10I2f")  # magic, version, nb_states, L, n1..n4, nb_freqs, n_dirs, res, w0, max_df
 _HDR2 = struct.Struct("<8s11I2f")  # version 2: ... n_dirs, res, act, w0, max_df
-RES_CODES = {"full": 0, "state": 1, "latent": 2}   # neural_df.py:76-78, 97-100
+# neural_df.py:76-78, 97-100: layer 3 sees [h2 | e | z] ('full'), [h2 | e] ('state'), [h2 | z] ('latent');
+# any other value of `res` gives a plain MLP (layer 3 sees h2 only), stored as 'none'
+RES_CODES = {"full": 0, "state": 1, "latent": 2, "none": 3}
+
+
+def norm_res(res) -> str:
+    """The reference's `res` argument as this build names it: 'full' / 'state' / 'latent', anything else
+    (None, 'none', False, ...) 'none' -- neural_df.py only tests membership in those three."""
+    return res if res in ("full", "state", "latent") else "none"
 ACT_CODES = {"sin": 0, "relu": 1, "softplus": 2}   # neural_df.py:40-47
 
 # embedding projection directions, one row per direction (embeddings.py:20-100)
@@ -84,7 +92,10 @@ class NetSpec:
     max_df: float = 1.0
     nb_states: int = 3
     act: str = "sin"    # 'sin' | 'relu' | 'softplus' (neural_df.py:40-47)
-    res: str = "full"   # 'full' | 'state' | 'latent': what layer 3 sees besides h2 (neural_df.py:76-78)
+    res: str = "full"   # 'full' | 'state' | 'latent' | 'none': what layer 3 sees besides h2 (neural_df.py:76-78)
+
+    def __post_init__(self):
+        object.__setattr__(self, "res", norm_res(self.res))
 
     @property
     def n_dirs(self) -> int:
@@ -98,7 +109,7 @@ class NetSpec:
         """Parameter names/shapes in torch ``state_dict`` order (neural_df.py:61-89)."""
         E, L = self.n_embed, self.size_latent
         n1, n2, n3, n4 = self.layer_sizes
-        c3 = n2 + {"full": E + L, "state": E, "latent": L}[self.res]
+        c3 = n2 + {"full": E + L, "state": E, "latent": L, "none": 0}[self.res]
         return [
             ("layers.main1.0.weight", (n1, E + L)), ("layers.main1.0.bias", (n1,)),
             ("layers.main1.3.weight", (n2, n1)), ("layers.main1.3.bias", (n2,)),
@@ -248,7 +259,7 @@ def from_torchscript(path: str) -> Tuple[NetSpec, Dict[str, np.ndarray]]:
     embed = EMBED_BY_DIRS[nd]
     spec = NetSpec(size_latent=L, layer_sizes=(n1, n2, n3, n4), nb_freqs=nf, embed=embed,
                    w0=float(m.w0), max_df=float(m.max_df), act=str(getattr(m, "activation", "sin")),
-                   res=str(getattr(m, "res", "full")))
+                   res=norm_res(getattr(m, "res", "full")))
     if nd and not np.array_equal(sd["embed.dirs"], embedding_dirs(embed)):
         raise ValueError("unexpected embedding directions")
     return spec, {k: sd[k] for k, _ in spec.param_shapes()}

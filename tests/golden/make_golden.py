@@ -513,9 +513,14 @@ def variants_golden(n=32):
     for name, spec in NET_VARIANTS.items():
         params = W.siren_weights(spec, seed=SEED, bias_gain=BIAS_GAIN)
         out[f"{name}/sha256"] = np.frombuffer(hashlib.sha256(W.pack(spec, params)).digest(), dtype=np.uint8)
+        vin = inp
+        if spec.size_latent != 128:  # its own inputs (3 + size_latent columns), the shared positions
+            vin = np.concatenate([inp[:, :3], np.random.default_rng(778 + spec.size_latent).normal(
+                size=(n, spec.size_latent)).astype(np.float32)], 1)
+            out[f"{name}/input"] = vin
         for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
             net = ref_net(spec, params, dt)
-            x = torch.from_numpy(inp).to(dt).requires_grad_(True)
+            x = torch.from_numpy(vin).to(dt).requires_grad_(True)
             df = net(x)
             (g,) = torch.autograd.grad(df.sum(), x)
             out[f"{name}/df_{tag}"] = df.detach().numpy()[:, 0]

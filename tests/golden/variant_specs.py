@@ -15,5 +15,15 @@ NET_VARIANTS = {
     "sin_ico_full": W.NetSpec(act="sin", embed="ico", res="full", layer_sizes=(128, 128, 128, 128)),
     "relu_none_state": W.NetSpec(act="relu", embed="none", res="state", layer_sizes=(192, 160, 100, 50), w0=1.0),
     "sin_oct6_full": W.NetSpec(act="sin", embed="oct", res="full", nb_freqs=6, w0=30.0),
+    # round 4: a plain MLP (any `res` outside full / state / latent, neural_df.py:76-78, 97-100) and latent
+    # sizes other than 128 (neural_df.py:16): 64 and 200 (zero-padded to 256 on the GEMMs)
+    "relu_pos_none": W.NetSpec(act="relu", embed="pos", res="none", layer_sizes=(256, 192, 128, 64), w0=1.0),
+    "sin_oct_full_L64": W.NetSpec(act="sin", embed="oct", res="full", size_latent=64),
+    "softplus_cube_latent_L200": W.NetSpec(act="softplus", embed="cube", res="latent", size_latent=200, w0=1.0),
 }
 SEED, BIAS_GAIN = 7, 0.5  # variants_golden.npz weights: W.siren_weights(spec, SEED, bias_gain=BIAS_GAIN)
+
+
+def variant_input(g, name):
+    """The fixture inputs of variant `name`: its own ([n, 3 + size_latent]) when its latent is not 128."""
+    return g[f"{name}/input"] if f"{name}/input" in g.files else g["input"]

@@ -136,3 +136,65 @@ def test_c5_deterministic_and_permutation_equivariant(run, gpu_ctx):
     cp = C5(gpu_ctx, perm=perm)
     np.testing.assert_array_equal(cp.step(), u0[perm])
     np.testing.assert_array_equal(cp.solver.download("iters").ravel(), c5.solver.download("iters").ravel()[perm])
+
+
+def test_c5_full_batch_through_shard_plan(tmp_path):
+    """BASELINE.json configs[4] (C5) at its real batch: 4096 instances at N = 60 with the 4x-wide SDF and the
+    in-loop VAE, through Ocp(devices=[0] * 8) -- shard.plan gives eight 512-instance parts (the N = 60
+    capacity) -- and VaeWrapper(batch=4096).encode_to, which packs each part's latents on its own device.
+    One RTI step converges on every instance inside the input boxes, and two parts solved alone (their own
+    512 images through their own VaeWrapper, the same QP kernel) agree bit for bit."""
+    from sdf_nmpc_amd import shard
+    from sdf_nmpc_amd.controller import Nmpc
+    from sdf_nmpc_amd.ocp import Ocp
+    from sdf_nmpc_amd.reference import Ref, yaw2quat
+    cfg = Config(mpc__N=N)
+    Bt, n_img = 4096, 64
+    wpath = str(tmp_path / "c5.sdfw")
+    with open(wpath, "wb") as f:
+        f.write(W.pack(W.WIDE_SPEC, W.siren_weights(W.WIDE_SPEC, 0)))
+    assert shard.plan(Bt, _lib.Context(0).qp_capacity(N), 8) == [(g, 512 * g, 512 * (g + 1)) for g in range(8)]
+    rng = np.random.default_rng(45)
+    x0 = np.zeros((Bt, 10))
+    x0[:, :3] = rng.uniform(-2, 2, (Bt, 3))
+    x0[:, 3:7] = np.stack([yaw2quat(y) for y in rng.uniform(-np.pi, np.pi, Bt)])
+    imgs = synth.depth_images(n_img, 270, 480, seed=46)
+    sel_img = rng.integers(0, n_img, Bt)
+    r = Ref(cfg)
+    r.p, r.q = np.array([1.0, 2.0, 1.5]), yaw2quat(0.3)
+    r.use_weights(r.W_on)
+    W_R = quat2rot(x0[:, 3:7]).reshape(Bt, 3, 3)
+
+    def run(lo, hi, devices, kernel=None):
+        nb = hi - lo
+        o = Ocp(Quad(cfg), batch=nb, devices=devices, weights=wpath)
+        if kernel is not None:
+            for p in o.parts:
+                p.ctx.set_qp_kernel(kernel)
+        n = Nmpc(cfg, batch=nb, ocp=o)
+        vw = V.VaeWrapper(cfg, batch=nb, ctx=o.ctx)
+        vw.set_img(imgs[sel_img[lo:hi]])
+        vw.encode_to(n, x0[lo:hi, :3], W_R[lo:hi], flag=1.0)
+        for k in range(N + 1):
+            n.set_ref(r, k)
+        n.set_x0(x0[lo:hi])
+        assert n.solve() == 0
+        out = dict(u0=n.get_u(), status=o.status.copy(), iters=o.iters.copy(), u=o.download("u"),
+                   p=o.download("p"), parts=len(o.parts), kind=o.parts[0].ctx.qp_kernel(N, nb))
+        o.close()
+        return out
+
+    full = run(0, Bt, [0] * 8)
+    assert full["parts"] == 8
+    assert (full["status"] == 0).all() and full["iters"].max() < 100
+    m = Quad(cfg)
+    assert (full["u"] >= m.lbu - 1e-9).all() and (full["u"] <= m.ubu + 1e-9).all()
+    # the latents every part packed: instances sharing an image carry the same latent at every node
+    b0 = np.flatnonzero(sel_img == sel_img[0])
+    assert len(b0) > 8 and (b0 // 512).min() != (b0 // 512).max()  # shared across parts
+    np.testing.assert_array_equal(full["p"][b0][:, :, 17:], np.broadcast_to(full["p"][b0[0], 0, 17:], (len(b0), N + 1, 128)))
+    for g in (0, 6):
+        lo, hi = 512 * g, 512 * (g + 1)
+        alone = run(lo, hi, [0], kernel=full["kind"])
+        np.testing.assert_array_equal(alone["u0"], full["u0"][lo:hi])
+        np.testing.assert_array_equal(alone["iters"], full["iters"][lo:hi])

@@ -243,6 +243,37 @@ def test_qp_sdf_cost_matches_riccati_oracle(gpu_ctx, oracle_lib, cfg):
 
 
 @pytest.mark.parametrize("kernel", ["serial", "segmented"])
+def test_qp_warm_start_recovers_after_failure(gpu_ctx, cfg, kernel):
+    """with the primal warm start (ocp.py:116) a failed QP (status 2, non-finite) leaves NaN in
+    the du buffer that the next QP starts from.  A du with a non-finite entry gives that instance a cold
+    start, so step 2 on clean data converges (status 0) and equals a cold solve bit for bit; the other
+    instances keep their warm starts."""
+    import torch
+    B, N = 6, 40
+    prob, x0, t = setup(gpu_ctx, cfg, B, N, seed=21)
+    gpu_ctx.set_qp_kernel(kernel)
+    try:
+        t["du"].zero_()
+        solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL)
+        cold = t["du"].cpu().numpy().copy()
+        good_jh = t["Jh"][2, 5, 1, 2].item()
+        t["Jh"][2, 5, 1, 2] = float("nan")  # step 1: instance 2 fails
+        t["du"].zero_()
+        solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL, warm_start=True)
+        st1 = t["status"].cpu().numpy()
+        assert st1[2] == 2 and not np.isfinite(t["du"][2].cpu().numpy()).all()
+        t["Jh"][2, 5, 1, 2] = good_jh  # step 2: clean data, du buffer as step 1 left it
+        du1 = t["du"].cpu().numpy().copy()
+        solve(gpu_ctx, cfg, t, B, N, tol=QP_TOL, warm_start=True)
+        st2, du2 = t["status"].cpu().numpy(), t["du"].cpu().numpy()
+    finally:
+        gpu_ctx.set_qp_kernel("auto")
+    assert (st2 == 0).all(), st2
+    assert np.array_equal(du2[2], cold[2]), "the failed instance restarts cold"
+    assert np.isfinite(du1[[0, 1, 3, 4, 5]]).all() and np.isfinite(du2).all()
+
+
+@pytest.mark.parametrize("kernel", ["serial", "segmented"])
 def test_qp_warm_start_matches_riccati_oracle(gpu_ctx, oracle_lib, cfg, kernel):
     """qp_solver_warm_start (ocp.py:116): the IPM starts from the du found in the du buffer.  Both kernels
     against the C restatement started from the same du (same iteration counts up to a rounding tie, the

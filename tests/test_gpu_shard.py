@@ -81,8 +81,10 @@ def test_two_rank_sharded_rti_equals_single_process():
 
 
 def test_qp_capacity_from_the_library():
-    """The occupancy gate's capacity comes from the C ABI (sdfnmpc_qp_capacity: device CUs x LDS per CU
-    // the kernel's LDS per instance) at N in {20, 40, 60, 80}; 1024 instances at N = 40 on an MI355X."""
+    """The occupancy gate's capacity comes from the C ABI (sdfnmpc_qp_capacity: device CUs x min(LDS per
+    CU // the kernel's LDS per instance, the runtime's occupancy of the kernel -- registers included)) at N
+    in {20, 40, 60, 80}.  The serial kernel holds 375 registers, one wave per SIMD: four instances per CU
+    even where the LDS would admit seven (N = 20); 1024 instances at N = 20 and 40 on an MI355X."""
     import torch
     from sdf_nmpc_amd import _lib
     ctx = _lib.Context(0)
@@ -94,8 +96,10 @@ def test_qp_capacity_from_the_library():
         per = int(_lib.load().sdfnmpc_qp_lds_bytes(N))
         assert per > 0
         caps[N] = ctx.qp_capacity(N)
-        assert caps[N] == cus * (lds // per), (N, caps[N], cus, per)
-    assert caps[40] == 1024 and caps[20] >= caps[40] >= caps[60] >= caps[80] > 0
+        assert 0 < caps[N] <= cus * min(4, lds // per), (N, caps[N], cus, per)
+        if lds // per <= 4:
+            assert caps[N] == cus * (lds // per), (N, caps[N], cus, per)
+    assert caps[20] == caps[40] == 1024 and caps[40] >= caps[60] >= caps[80] > 0
     assert ctx.qp_capacity(400) == 0  # no instance of that horizon fits one CU's LDS
     with pytest.raises(_lib.SdfnmpcError):
         ctx.qp_capacity(0)
@@ -116,6 +120,9 @@ def test_qp_kernel_auto_policy():
     ctx.set_qp_kernel("segmented")
     assert ctx.qp_kernel(40, 1024) == "segmented" and ctx.qp_kernel(20, 1) == "segmented"
     assert ctx.qp_kernel(80, 1) == "serial"  # unsupported horizon: serial whatever is asked
+    # the P = 4 segmented kernel's registers (__launch_bounds__(256, 2)) allow two workgroups per CU, fewer
+    # than its LDS would (three): the capacity follows the registers
+    assert ctx.qp_capacity(40) == 2 * 256
     ctx.set_qp_kernel("auto")
     assert ctx.qp_capacity(40) == 1024
 
@@ -155,3 +162,64 @@ def test_ocp_occupancy_gate_parts_equal_one_part():
         res.append(n.get_u())
         o.close()
     np.testing.assert_array_equal(res[0], res[1])
+
+
+def _c4_inputs(cfg, Bt, seed):
+    from sdf_nmpc_amd.reference import Ref, yaw2quat
+    rng = np.random.default_rng(seed)
+    x0 = np.zeros((Bt, 10))
+    x0[:, :3] = rng.uniform(-2, 2, (Bt, 3))
+    x0[:, 3:7] = np.stack([yaw2quat(y) for y in rng.uniform(-np.pi, np.pi, Bt)])
+    x0[:, 7:] = rng.uniform(-1, 1, (Bt, 3))
+    lat = rng.normal(size=(Bt, 128))
+    r = Ref(cfg)
+    r.p, r.q = np.array([1.0, 2.0, 1.5]), yaw2quat(0.3)
+    r.use_weights(r.W_on)
+    return x0, lat, r
+
+
+def _c4_run(cfg, x0, lat, r, devices, kernel=None, steps=2):
+    from sdf_nmpc_amd.controller import Nmpc
+    from sdf_nmpc_amd.model import Quad
+    from sdf_nmpc_amd.ocp import Ocp
+    Bt = x0.shape[0]
+    o = Ocp(Quad(cfg), batch=Bt, devices=devices)
+    if kernel is not None:
+        for p in o.parts:
+            p.ctx.set_qp_kernel(kernel)
+    n = Nmpc(cfg, batch=Bt, ocp=o)
+    n.set_sdf_flag(1.0)
+    n.set_latent(lat, x0[:, :3], np.stack([np.eye(3)] * Bt))
+    for k in range(cfg.mpc.N + 1):
+        n.set_ref(r, k)
+    n.set_x0(x0)
+    for _ in range(steps):  # the carried iterate too
+        assert n.solve() == 0
+    out = dict(u0=n.get_u(), status=o.status.copy(), iters=o.iters.copy(), u=o.download("u"), n_parts=len(o.parts))
+    o.close()
+    return out
+
+
+def test_c4_full_batch_through_the_occupancy_gate():
+    """BASELINE.json configs[3] (C4) at its real batch: 8192 instances at N = 40 through
+    Ocp(devices=[0] * 8) -- the eight device slots of an 8-GPU node, all on the one GPU here.  shard.plan
+    splits the batch into eight 1024-instance parts (the occupancy gate, sdfnmpc_qp_capacity); two RTI steps
+    converge on every instance, the iterate respects the input boxes, and each part equals the same
+    instances solved alone, bit for bit (a part never sees its neighbours)."""
+    from sdf_nmpc_amd import _lib, shard
+    from sdf_nmpc_amd.config import Config
+    from sdf_nmpc_amd.model import Quad
+    cfg = Config()
+    Bt = 8192
+    assert shard.plan(Bt, _lib.Context(0).qp_capacity(40), 8) == [(g, 1024 * g, 1024 * (g + 1)) for g in range(8)]
+    x0, lat, r = _c4_inputs(cfg, Bt, 40)
+    full = _c4_run(cfg, x0, lat, r, [0] * 8)
+    assert full["n_parts"] == 8
+    assert (full["status"] == 0).all() and full["iters"].max() < 100
+    m = Quad(cfg)
+    assert (full["u"] >= m.lbu - 1e-9).all() and (full["u"] <= m.ubu + 1e-9).all()
+    for g in (0, 5, 7):  # parts solved alone (the same QP kernel the split pinned: serial at B = 8192)
+        sl = slice(1024 * g, 1024 * (g + 1))
+        alone = _c4_run(cfg, x0[sl], lat[sl], r, [0], kernel="serial")
+        np.testing.assert_array_equal(alone["u0"], full["u0"][sl])
+        np.testing.assert_array_equal(alone["iters"], full["iters"][sl])

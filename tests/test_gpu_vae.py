@@ -68,6 +68,26 @@ def test_encoder_vs_oracle_batch(gpu_ctx, dev_vae, cfg, oracle_lib):
         assert vae_latent_err(lat[b], ref[b]) <= VAE_LATENT_RTOL, b
 
 
+def test_encoder_non_finite_pixels(gpu_ctx, dev_vae, cfg, oracle_lib):
+    """ADVICE r3 (split-bf16 exactness): the convolutions see only preprocessed pixels, and ClipDistance /
+    Depth2Range clip to [0, 1] (utils/preprocessing.py:30-31, 78-79) -- an Inf depth pixel reaches them as
+    1.0, where the split is exact, and the latent matches the fp64 oracle as for any image.  A NaN pixel
+    passes the clips as NaN (torch.clip and the kernel's compare-selects both keep it) and poisons the
+    latent, as in the reference: NaN in, NaN out, never a silently finite latent."""
+    _, vae, flat = dev_vae
+    imgs = synth.depth_images(2, 270, 480, seed=29)
+    imgs[0, 100, 200] = np.inf
+    imgs[0, 0, 0] = np.inf
+    imgs[1, 135, 240] = np.nan
+    lat, _ = _encode(gpu_ctx, vae, cfg, imgs, 5.0)
+    yz = V.depth2range_table(cfg.sensor.shape_imgs, cfg.sensor.hfov, cfg.sensor.vfov)
+    pre = oracle_lib.vae_preprocess(imgs[0], (270, 480), 5.0, yz)
+    assert pre[100, 200] == 1.0 and np.isfinite(pre).all()
+    ref = oracle_lib.vae_encode(pre[None], flat)
+    assert np.isfinite(lat[0]).all() and vae_latent_err(lat[0], ref[0]) <= VAE_LATENT_RTOL
+    assert np.isnan(lat[1]).any()
+
+
 def test_batch_invariance_and_determinism(gpu_ctx, dev_vae, cfg):
     """Each image's latent is independent of its batch neighbours (bitwise) and runs are bitwise repeatable;
     37 images leave a ragged last GEMM row tile in every layer."""

@@ -127,7 +127,7 @@ def test_oracle_batch_equals_per_node_calls(oracle_lib, cfg):
 
 
 # ---- NeuralDF variants (neural_df.py:13-103): act / embed / res / layer sizes / frequencies
-from variant_specs import BIAS_GAIN, NET_VARIANTS, SEED  # noqa: E402
+from variant_specs import BIAS_GAIN, NET_VARIANTS, SEED, variant_input  # noqa: E402
 
 
 @pytest.mark.parametrize("name", sorted(NET_VARIANTS))
@@ -143,7 +143,7 @@ def test_neural_df_np_matches_reference_variants(golden, name):
     assert spec2 == spec and all(np.array_equal(params[k], params2[k]) for k in params)
     if f"{name}/dirs" in g.files:  # weights.embedding_dirs == the buffer the reference builds
         assert np.array_equal(W.embedding_dirs(spec.embed), g[f"{name}/dirs"])
-    df, gr, gz = neural_df_np.forward_grad(spec, params, g["input"], latent_grad=True)
+    df, gr, gz = neural_df_np.forward_grad(spec, params, variant_input(g, name), latent_grad=True)
     ref_df, ref_g = g[f"{name}/df_f64"], g[f"{name}/grad_f64"]
     assert np.abs(df - ref_df).max() <= 1e-12 * max(1.0, np.abs(ref_df).max())
     assert np.abs(gr - ref_g[:, :3]).max() <= 1e-12 * max(1.0, np.abs(ref_g).max())
