@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--no-b1", action="store_true", help="skip the B=1 latency probe (profiling runs)")
     ap.add_argument("--no-c2", action="store_true", help="skip the CasADi-external (libsdf_l4c.so) call leg")
     ap.add_argument("--no-c1", action="store_true", help="skip the B=1, N=20 controller-step leg (config C1)")
+    ap.add_argument("--no-scene", action="store_true", help="skip the obstacle-scene SDF side leg")
     ap.add_argument("--config", choices=("c3", "c5"), default="c3",
                     help="c3: the headline 1024 x 40 RTI (default); c5: 4x-wide SDF MLP + in-loop VAE encode, "
                          "N = 60, 4096 instances over 8 GPUs (512 per GPU)")
@@ -283,6 +284,10 @@ def main():
     if rank == 0 and not args.no_c1:
         c1 = bench_c1(local, args.no_cpu_baseline)
 
+    # the headline workload's size on the obstacle-scene SDF net (active / releasing SDF rows)
+    scene = None
+    if rank == 0 and not args.no_scene:
+        scene = bench_scene(local, B, N)
     # traffic from the committed PMC profile of this same command (profiles/)
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -367,6 +372,7 @@ def main():
         "prep": prep_out,
         "c2": c2,
         "c1": c1,
+        "scene": scene,
     }
     if rank == 0:
         print(json.dumps(out))
@@ -434,6 +440,57 @@ def bench_c1(device, no_cpu, steps=200):
                                "sample": f"{steps} closed-loop steps of the same problem: C oracle preparation "
                                          "(oracle/oracle.c) + structured Riccati IPM (oracle/qp_ipm.c), one thread"}
     n.ocp.close()
+    return res
+
+
+def bench_scene(device, B=1024, N=40, warm_steps=6, steps=10):
+    """Side leg (not the headline): the headline's batch and horizon with the SDF network fitted to an obstacle
+    scene (tests/golden/scene.sdfw, tools/fit_scene_sdf.py; tests/scene_setup.py) instead of the SIREN
+    initialisation, whose df ~ 0 makes every SDF row of every QP active.  B instances start at x in [0, 2.5] m
+    and lateral offsets in [-1, 1.5] m and fly towards a waypoint beyond the pillar; the loop is closed with a
+    perfect-model plant (x_0 of the next step = node 1 of the updated iterate).  After `warm_steps` steps
+    (the pillar inside most horizons), `steps` further steps are timed per kernel (HIP events): the rti_qp
+    time and IPM iterations on this net, and how many instances have an active SDF soft row."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import scene_setup as S
+    from sdf_nmpc_amd.config import Config
+    from sdf_nmpc_amd.controller import Nmpc
+    from sdf_nmpc_amd.model import Quad
+    from sdf_nmpc_amd.ocp import Ocp
+    cfg = Config(mpc__N=N)
+    o = Ocp(Quad(cfg), batch=B, device=device, weights=S.SCENE)
+    n = Nmpc(cfg, batch=B, ocp=o)
+    rng = np.random.default_rng(77)
+    x = S.setup(n, y0=rng.uniform(-1.0, 1.5, B))
+    x[:, 0] = rng.uniform(0.0, 2.5, B)
+    for _ in range(warm_steps):
+        n.set_x0(x)
+        n.solve()
+        x = n.get_matrices()[0][:, 1].copy()
+    o.ctx.enable_timing(True)
+    o.ctx.reset_stats()
+    iters, active, wall = [], [], []
+    for _ in range(steps):
+        n.set_x0(x)
+        t0 = time.perf_counter()
+        n.solve()
+        wall.append(time.perf_counter() - t0)
+        iters.append(o.iters.copy())
+        sl = o.download("slack").reshape(B, N + 1, 3, 2)
+        active.append((sl[:, :, 2, 0] > 1e-6).any(axis=1))
+        x = n.get_matrices()[0][:, 1].copy()
+    kms = {k: (v[0] / v[1] if v[1] else None) for k, v in
+           ((k, o.ctx.kernel_stats(k)) for k in ("sdf_mlp", "linearize", "rti_qp", "rti_qp_pack"))}
+    o.ctx.enable_timing(False)
+    it = np.array(iters)
+    res = {"workload": f"{B} instances x N={N}, obstacle-scene SDF net (deployed architecture fitted to a pillar "
+                       "and a box), closed loop past the pillar, timed steps {warm_steps}..{warm_steps + steps - 1}",
+           "kernel_ms": kms, "qp_iters_max": int(it.max()), "qp_iters_mean": float(it.mean()),
+           "qp_iters_max_per_step": [int(v) for v in it.max(axis=1)],
+           "sdf_active_frac": float(np.mean(active)), "instances_with_active_sdf_row_per_step":
+               [int(v) for v in np.sum(active, axis=1)],
+           "solve_wall_ms_p50": float(np.median(wall) * 1e3)}
+    o.close()
     return res
 
 

@@ -7,8 +7,9 @@
 //
 // Kernels (activations NHWC fp32, resident in one workspace):
 //   vae_pre_kernel   raw depth -> range image (resize, clip, depth->range), one thread per pixel
-//   vae_stem_kernel  conv7x7/2 + ELU + maxpool3/2 fused per 7x8 pooled tile: the 15x17 conv tile lives
-//                    in LDS, the tap weights are wave-uniform (scalar loads), one conv pixel per lane
+//   vae_stem_kernel  conv7x7/2 + ELU + maxpool3/2 fused per 7x8 pooled tile: an implicit GEMM (255 conv
+//                    pixels x 64 channels x 49 taps) on the bf16 matrix pipe with fp32-exact split
+//                    products, the conv tile in LDS for the pool
 //   vae_conv_kernel  every ResBlock convolution as an implicit GEMM on f32 MFMA 32x32x2 (exact fp32
 //                    products): 128x128 output tile per workgroup, K staged 16 at a time through
 //                    double-buffered LDS, bias / residual / ReLU fused into the epilogue
@@ -69,17 +70,43 @@ hipError_t launch_vae_pre(const VaePreArgs& a, hipStream_t s) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// stem: conv7x7/2 pad 3 (1 -> 64) + bias + ELU + maxpool3/2 pad 1 (vae.py:19-21)
+// stem: conv7x7/2 pad 3 (1 -> 64) + bias + ELU + maxpool3/2 pad 1 (vae.py:19-21), as an implicit GEMM on
+// the bf16 matrix pipe with fp32-exact products (the split of the ResBlock convolutions below):
+//   out[p][n] = sum_k A[p][k] W[k][n],  p = the 255 conv pixels of a workgroup's 7 x 8 pooled tile (15 x 17,
+//   one slot of padding: 8 row blocks of 32), n = 64 channels, k = the 49 taps padded to 64 (4 K-steps of
+//   16).  Each wave owns two row blocks x two channel blocks.  The weights are split once per workgroup into
+//   hi / mid / lo bf16 planes in LDS (B operand, k-contiguous rows); each lane gathers its pixel's 8 taps
+//   of a K-step from the input patch in LDS and splits them in registers (A operand).  Six
+//   v_mfma_f32_32x32x16_bf16 per block and K-step (al.bh, ah.bl, am.bm, am.bh, ah.bm, ah.bh) accumulate in
+//   fp32; the dropped products are <= 2^-24 relative.  Bias + ELU into the conv tile in LDS (aliasing the
+//   patch and the planes once the products are done), then the maxpool.
 constexpr int ST_PY = 7, ST_PX = 8;                        // pooled tile
 constexpr int ST_CY = 2 * ST_PY + 1, ST_CX = 2 * ST_PX + 1;  // conv tile 15 x 17 = 255 pixels
 constexpr int ST_IY = 2 * ST_CY + 5, ST_IX = 2 * ST_CX + 5;  // input patch 35 x 39
 constexpr int ST_IXP = ST_IX + 1;
 constexpr int ST_CS = 65;                                  // conv tile stride (floats): odd -> no conflicts
+constexpr int ST_KL = 72;                                  // weight-plane row stride (bf16): 144 B rows
+constexpr int ST_PATCH = ST_IY * ST_IXP;                   // floats
+constexpr int ST_WPL = 64 * ST_KL;                         // bf16 per weight plane
+constexpr int ST_LDS_A = ST_PATCH * 4 + 3 * ST_WPL * 2;    // patch + planes (bytes)
+constexpr int ST_LDS_C = ST_CY * ST_CX * ST_CS * 4;        // conv tile (bytes)
+constexpr int ST_LDS = ST_LDS_A > ST_LDS_C ? ST_LDS_A : ST_LDS_C;
 
-__global__ __launch_bounds__(256) void vae_stem_kernel(VaeStemArgs a) {
-    __shared__ float patch[ST_IY * ST_IXP];
-    __shared__ float conv[ST_CY * ST_CX * ST_CS];
-    const int t = threadIdx.x, img = blockIdx.z;
+// x = hi + mid + lo exactly, each a bf16 truncation of the remainder (the split of split3_store)
+__device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
+    h = __float_as_uint(x) & 0xffff0000u;
+    const float r1 = x - __uint_as_float(h);
+    m = __float_as_uint(r1) & 0xffff0000u;
+    const float r2 = r1 - __uint_as_float(m);
+    l = __float_as_uint(r2) & 0xffff0000u;
+}
+
+__global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a) {
+    __shared__ __align__(16) unsigned char smem[ST_LDS];
+    float* patch = (float*)smem;
+    unsigned short* wpl = (unsigned short*)(smem + ST_PATCH * 4);  // [3][64 n][ST_KL]
+    float* conv = (float*)smem;                                    // after the products
+    const int t = threadIdx.x, img = blockIdx.z, lane = t & 63, wave = t >> 6, lr = lane & 31, lh = lane >> 5;
     const int py0 = blockIdx.y * ST_PY, px0 = blockIdx.x * ST_PX;
     const int gy0 = 4 * py0 - 5, gx0 = 4 * px0 - 5;
     const float* in = a.in + (size_t)img * a.H * a.W;
@@ -88,29 +115,98 @@ __global__ __launch_bounds__(256) void vae_stem_kernel(VaeStemArgs a) {
         const int gy = gy0 + r, gx = gx0 + c;
         patch[r * ST_IXP + c] = ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W) ? in[(size_t)gy * a.W + gx] : 0.f;
     }
+    for (int e = t; e < 64 * 64; e += 256) {  // W[k][n] (tap-major) -> planes[n][k], taps 49..63 zero
+        const int n = e & 63, k = e >> 6;
+        unsigned h = 0, m = 0, l = 0;
+        if (k < 49) split3(a.w[k * 64 + n], h, m, l);
+        wpl[0 * ST_WPL + n * ST_KL + k] = (unsigned short)(h >> 16);
+        wpl[1 * ST_WPL + n * ST_KL + k] = (unsigned short)(m >> 16);
+        wpl[2 * ST_WPL + n * ST_KL + k] = (unsigned short)(l >> 16);
+    }
     __syncthreads();
-    if (t < ST_CY * ST_CX) {
-        const int cyl = t / ST_CX, cxl = t - cyl * ST_CX;
-        float acc[64];
+    // this lane's two pixels (row blocks i = 0, 1 of the wave): conv pixel q = 64 wave + 32 i + lr
+    int pbase[2];
 #pragma unroll
-        for (int c = 0; c < 64; ++c) acc[c] = a.b[c];
-        const float* pp = patch + (2 * cyl) * ST_IXP + 2 * cxl;
-        for (int ky = 0; ky < 7; ++ky) {
+    for (int i = 0; i < 2; ++i) {
+        const int q = wave * 64 + 32 * i + lr, qq = q < ST_CY * ST_CX ? q : 0;
+        const int cyl = qq / ST_CX, cxl = qq - cyl * ST_CX;
+        pbase[i] = (2 * cyl) * ST_IXP + 2 * cxl;
+    }
+    floatx16 acc[2][2];
 #pragma unroll
-            for (int kx = 0; kx < 7; ++kx) {
-                const float v = pp[ky * ST_IXP + kx];
-                const float* wr = a.w + (ky * 7 + kx) * 64;  // wave-uniform: scalar loads
+    for (int i = 0; i < 2; ++i)
 #pragma unroll
-                for (int c = 0; c < 64; ++c) acc[c] = fmaf(wr[c], v, acc[c]);
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        // A: taps k = 16 s + 8 lh + jj of the lane's pixels, split in registers (padded taps read 0)
+        bf16x8 ah[2], am[2], al[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            unsigned hp[4], mp[4], lp[4];
+#pragma unroll
+            for (int jj = 0; jj < 8; jj += 2) {
+                float v2[2];
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const int k = 16 * s + 8 * lh + jj + u;     // lh is per lane: k < 49 is a lane predicate
+                    const int kc = k < 49 ? k : 48, ky = kc / 7, kx = kc - 7 * ky;
+                    const float v = patch[pbase[i] + ky * ST_IXP + kx];
+                    v2[u] = k < 49 ? v : 0.f;
+                }
+                unsigned h0, m0, l0, h1, m1, l1;
+                split3(v2[0], h0, m0, l0);
+                split3(v2[1], h1, m1, l1);
+                hp[jj / 2] = (h0 >> 16) | h1;
+                mp[jj / 2] = (m0 >> 16) | m1;
+                lp[jj / 2] = (l0 >> 16) | l1;
             }
+            ah[i] = __builtin_bit_cast(bf16x8, make_uint4(hp[0], hp[1], hp[2], hp[3]));
+            am[i] = __builtin_bit_cast(bf16x8, make_uint4(mp[0], mp[1], mp[2], mp[3]));
+            al[i] = __builtin_bit_cast(bf16x8, make_uint4(lp[0], lp[1], lp[2], lp[3]));
         }
-        const int cy = 2 * py0 - 1 + cyl, cx = 2 * px0 - 1 + cxl;
-        const bool ok = (unsigned)cy < (unsigned)a.Hc && (unsigned)cx < (unsigned)a.Wc;
+        // B: channel n = 32 j + lr, taps 16 s + 8 lh .. + 7 of each plane (16-byte reads)
+        bf16x8 bh[2], bm[2], bl[2];
 #pragma unroll
-        for (int c = 0; c < 64; ++c) {
-            const float v = acc[c] > 0.f ? acc[c] : expm1f(acc[c]);  // ELU(alpha = 1)
-            conv[t * ST_CS + c] = ok ? v : -INFINITY;                // outside the map: never the max
+        for (int j = 0; j < 2; ++j) {
+            const int o = (32 * j + lr) * ST_KL + 16 * s + 8 * lh;
+            bh[j] = *(const bf16x8*)&wpl[0 * ST_WPL + o];
+            bm[j] = *(const bf16x8*)&wpl[1 * ST_WPL + o];
+            bl[j] = *(const bf16x8*)&wpl[2 * ST_WPL + o];
         }
+#define ST_MM(X, Y)                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)         \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[i], Y[j], acc[i][j], 0, 0, 0);
+        ST_MM(al, bh)
+        ST_MM(ah, bl)
+        ST_MM(am, bm)
+        ST_MM(am, bh)
+        ST_MM(ah, bm)
+        ST_MM(ah, bh)
+#undef ST_MM
+    }
+    __syncthreads();  // every wave is done with the patch and the planes: the conv tile takes their place
+    // epilogue: lane (lr, lh), register r holds row 8 (r / 4) + 4 lh + r % 4 (pixel), column lr (channel)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const int c = 32 * j + lr;
+        const float bias = a.b[c];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+                const int q = wave * 64 + 32 * i + 8 * (r >> 2) + 4 * lh + (r & 3);
+                if (q < ST_CY * ST_CX) {
+                    const int cyl = q / ST_CX, cxl = q - cyl * ST_CX;
+                    const int cy = 2 * py0 - 1 + cyl, cx = 2 * px0 - 1 + cxl;
+                    const bool ok = (unsigned)cy < (unsigned)a.Hc && (unsigned)cx < (unsigned)a.Wc;
+                    const float x = acc[i][j][r] + bias;
+                    const float v = x > 0.f ? x : expm1f(x);  // ELU(alpha = 1); a NaN stays a NaN
+                    conv[q * ST_CS + c] = ok ? v : -INFINITY;  // outside the map: never the max
+                }
+            }
     }
     __syncthreads();
     const int c = t & 63;
@@ -146,7 +242,8 @@ hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s) {
 // LDS rows are 16 k-values padded to 20 floats: the ds_read_b128 lane groups then hit 16 distinct
 // 16-byte slots (conflict-free).  Within a K-tile, MFMA step s feeds lane half h with k = 8h + s
 // (the same permutation for A and B), so each lane reads its 8 k-values with two ds_read_b128.
-constexpr int CV_BM = 128, CV_BN = 128, CV_BK = 16, CV_LD = 20;
+constexpr int CV_BM = 128, CV_BN = 128, CV_BK = 16;
+[[maybe_unused]] constexpr int CV_LD = 20;  // the VAE_F32_MFMA diagnostic build's fp32 row stride
 constexpr int CV_SLD = 24;  // bf16 plane row stride (48 bytes)
 
 // fp32 -> three bf16 by truncation: x = hi + mid + lo EXACTLY (each takes the next 8 significant bits of
@@ -204,7 +301,9 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
     const float* pa1 = a.in + (size_t)im1 * a.Hi * a.Wi * Cin + 4 * kq;
     const float* pb0 = a.w + (size_t)(nt * CV_BN + (tid >> 2)) * K + 4 * kq;
     const float* pb1 = pb0 + (size_t)64 * K;
+#ifdef VAE_F32_MFMA
     const int srow0 = (tid >> 2) * CV_LD + 4 * kq, srow1 = srow0 + 64 * CV_LD;
+#endif
 
     float4 ra0, ra1, rb0, rb1;
     int ky = 0, kx = 0, c0 = 0;  // K-tile position (tap, channel block) being loaded

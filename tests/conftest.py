@@ -31,7 +31,7 @@ def golden():
     import numpy as np
     d = os.path.join(ROOT, "tests", "golden")
     return {k: np.load(os.path.join(d, f"{k}_golden.npz")) for k in ("sdf", "lin", "grid", "params", "sdfc3",
-                                                                                  "variants")}
+                                                                                  "variants", "scene")}
 
 
 @pytest.fixture(scope="session")

@@ -620,10 +620,37 @@ def vae_golden():
     print("vae_golden.npz", len(out))
 
 
+def scene_golden(n=256):
+    """The reference's own NeuralDF on the scene-fitted weights (tests/golden/scene.sdfw, written by
+    tools/fit_scene_sdf.py) and the scene latent, in fp32 and fp64: df and the full 1 x 131 Jacobian on
+    points along the corridor the closed-loop test flies (camera-origin frame), plus the analytic scene
+    distance the weights were fitted to (what the fit is, not a parity bar)."""
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import fit_scene_sdf as FS
+    with open(os.path.join(HERE, "scene.sdfw"), "rb") as f:
+        blob = f.read()
+    spec, params = W.unpack(blob)
+    rng = np.random.default_rng(4242)
+    pos = np.stack([rng.uniform(-0.5, 7.0, n), rng.uniform(-2.5, 2.5, n), rng.uniform(-1.0, 1.0, n)], 1)
+    z = FS.scene_latent()
+    inp = np.concatenate([pos.astype(np.float32), np.broadcast_to(z, (n, len(z)))], 1).astype(np.float32)
+    out = {"input": inp, "latent": z, "sha256": np.frombuffer(hashlib.sha256(blob).digest(), dtype=np.uint8),
+           "scene_df": FS.scene_sdf(pos)[0]}
+    for dt, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        net = ref_net(spec, params, dt)
+        x = torch.from_numpy(inp).to(dt).requires_grad_(True)
+        df = net(x)
+        (g,) = torch.autograd.grad(df.sum(), x)
+        out[f"df_{tag}"] = df.detach().numpy()[:, 0]
+        out[f"grad_{tag}"] = g.numpy()
+    np.savez_compressed(os.path.join(HERE, "scene_golden.npz"), **out)
+    print("scene_golden.npz", {k: v.shape for k, v in out.items()})
+
+
 if __name__ == "__main__":
     only = sys.argv[1:]
     for name, fn in (("sdf", sdf_golden), ("lin", lin_golden), ("grid", grid_golden), ("params", params_golden),
                      ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden), ("wide", wide_golden), ("sdfc3", sdfc3_golden),
-                     ("variants", variants_golden)):
+                     ("variants", variants_golden), ("scene", scene_golden)):
         if not only or name in only:
             fn()

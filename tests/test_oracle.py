@@ -148,3 +148,22 @@ def test_neural_df_np_matches_reference_variants(golden, name):
     assert np.abs(df - ref_df).max() <= 1e-12 * max(1.0, np.abs(ref_df).max())
     assert np.abs(gr - ref_g[:, :3]).max() <= 1e-12 * max(1.0, np.abs(ref_g).max())
     assert np.abs(gz - ref_g[:, 3:]).max() <= 1e-12 * max(1.0, np.abs(ref_g).max())
+
+
+def test_oracle_pinned_on_the_scene_net(golden, oracle_lib):
+    """The scene-fitted weights (tests/golden/scene.sdfw, tools/fit_scene_sdf.py): the fp64 C restatement
+    reproduces the reference NeuralDF's fp64 outputs (df and the full 1 x 131 Jacobian), and the fit is the
+    analytic scene to a few centimetres (tests/scene_setup.py)."""
+    import os
+    g = golden["scene"]
+    with open(os.path.join(os.path.dirname(__file__), "golden", "scene.sdfw"), "rb") as f:
+        blob = f.read()
+    assert hashlib.sha256(blob).digest() == g["sha256"].tobytes()
+    spec, params = W.unpack(blob)
+    assert spec == W.DEFAULT_SPEC  # the deployed architecture: the fused kernels serve it
+    net = oracle_lib.Net(spec, params)
+    df, gp, gf = net.f64(g["input"].astype(np.float64))
+    scale = max(1.0, np.abs(g["grad_f64"]).max())
+    assert np.abs(df - g["df_f64"]).max() < 1e-12 * max(1.0, np.abs(g["df_f64"]).max())
+    assert np.abs(gf - g["grad_f64"]).max() < 1e-12 * scale
+    assert np.quantile(np.abs(g["df_f64"] - g["scene_df"]), 0.95) < 0.1

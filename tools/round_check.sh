@@ -19,13 +19,13 @@ cat $O/bench.json
 timeout -k 10 400 python $R/bench.py --config c5 > $O/bench_c5.json 2> $O/bench_c5.err
 cat $O/bench_c5.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o bench -- \
-    python3 $R/bench.py --no-cpu-baseline --no-b1 --no-c2 --no-c1 > $O/bench_traced.json 2> $O/trace.err
+    python3 $R/bench.py --no-cpu-baseline --no-b1 --no-c2 --no-c1 --no-scene > $O/bench_traced.json 2> $O/trace.err
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace_c5 -o bench -- \
     python3 $R/bench.py --config c5 --no-cpu-baseline > $O/bench_c5_traced.json 2> $O/trace_c5.err
 timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/fetch -o p -- \
-    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 --prep-steps 2 --no-b1 --no-c2 --no-c1 > /dev/null 2> $O/fetch.err
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 --prep-steps 2 --no-b1 --no-c2 --no-c1 --no-scene > /dev/null 2> $O/fetch.err
 timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/write -o p -- \
-    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 --prep-steps 2 --no-b1 --no-c2 --no-c1 > /dev/null 2> $O/write.err
+    python3 $R/bench.py --no-cpu-baseline --steps 5 --warmup 2 --prep-steps 2 --no-b1 --no-c2 --no-c1 --no-scene > /dev/null 2> $O/write.err
 # the stamps driver is rebuilt from the current rti_qp.hip, so the stamps always describe this tree's kernel
 (cd $R && timeout -k 10 300 hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -DQP_STAMPS -I sdf-nmpc_amd/csrc \
     tools/qp_stamps_drv.hip sdf-nmpc_amd/csrc/rti_qp.hip -o tools/_qp_stamps_drv)
