@@ -1542,6 +1542,7 @@ struct sdfnmpc_vae {
     int bh[4] = {0}, bw[4] = {0};  // block output maps
     void* dmem = nullptr;
     VaeLayer stem, conv[11], head;  // conv: b0a b0s b0b b1a b1s b1b b2a b2s b2b b3a b3b
+    const unsigned short* stem_wpl = nullptr;  // the stem weights split into bf16 planes (VaeStemArgs::wpl)
     DevBuf ws;
     int ws_B = 0;
 };
@@ -1589,14 +1590,37 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
         delete v;
         return fail(SDFNMPC_E_FORMAT, "vaew: parameter count does not match the reference encoder");
     }
-    std::vector<float> dev(need);
+    // + the stem weights split exactly into three bf16 planes [3][64 n][64 k] (vae_enc.hip's split3), in
+    // the kernel's K order (vae_stem_slot_tap), appended after the layers (16-byte aligned)
+    const size_t wpl_off = (need + 3) & ~(size_t)3;
+    std::vector<float> dev(wpl_off + 3 * VAE_STEM_PLANE / 2, 0.0f);
     size_t off = 0;
     for (size_t li = 0; li < specs.size(); ++li) {
         const Spec& s = specs[li];
         const size_t nw = (size_t)s.cout * s.ks * s.ks * s.cin;
-        if (li == 0) {  // stem [64][7][7][1] -> tap-major [49][64]
+        if (li == 0) {  // stem [64][7][7][1] -> tap-major [49][64], and the split planes
+            unsigned short* wpl = (unsigned short*)&dev[wpl_off];
             for (int c = 0; c < 64; ++c)
                 for (int t = 0; t < 49; ++t) dev[off + t * 64 + c] = src[off + c * 49 + t];
+            for (int c = 0; c < 64; ++c)
+                for (int k = 0; k < 49; ++k) {
+                    const float x = src[off + c * 49 + vae_stem_slot_tap(k)];
+                    uint32_t u, hb, mb, lb;
+                    memcpy(&u, &x, 4);
+                    hb = u & 0xffff0000u;
+                    float hf, r1, mf, r2;
+                    memcpy(&hf, &hb, 4);
+                    r1 = x - hf;  // exact (the leading 8 significant bits removed)
+                    memcpy(&u, &r1, 4);
+                    mb = u & 0xffff0000u;
+                    memcpy(&mf, &mb, 4);
+                    r2 = r1 - mf;
+                    memcpy(&u, &r2, 4);
+                    lb = u & 0xffff0000u;
+                    wpl[0 * VAE_STEM_PLANE + c * 64 + k] = (unsigned short)(hb >> 16);
+                    wpl[1 * VAE_STEM_PLANE + c * 64 + k] = (unsigned short)(mb >> 16);
+                    wpl[2 * VAE_STEM_PLANE + c * 64 + k] = (unsigned short)(lb >> 16);
+                }
         } else if (li + 1 == specs.size()) {  // head [L][2048] -> [2048][L]
             for (int o = 0; o < s.cout; ++o)
                 for (int f = 0; f < 2048; ++f) dev[off + (size_t)f * s.cout + o] = src[off + (size_t)o * 2048 + f];
@@ -1607,13 +1631,14 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
         off += nw + s.cout;
     }
     ScopedDevice sd(ctx->device);
-    if (hipMalloc(&v->dmem, need * 4) != hipSuccess ||
-        hipMemcpy(v->dmem, dev.data(), need * 4, hipMemcpyHostToDevice) != hipSuccess) {
+    if (hipMalloc(&v->dmem, dev.size() * 4) != hipSuccess ||
+        hipMemcpy(v->dmem, dev.data(), dev.size() * 4, hipMemcpyHostToDevice) != hipSuccess) {
         if (v->dmem) (void)hipFree(v->dmem);
         delete v;
         return fail(SDFNMPC_E_HIP, "vaew: device upload failed");
     }
     const float* d = (const float*)v->dmem;
+    v->stem_wpl = (const unsigned short*)(d + wpl_off);
     off = 0;
     for (size_t li = 0; li < specs.size(); ++li) {
         const Spec& s = specs[li];
@@ -1664,7 +1689,7 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
     hipStream_t st = ctx->stream;
     VaePreArgs pa{img, o->dtype, B, o->in_h, o->in_w, v->H, v->W, o->clip, o->yz, P};
     HIPCHK(timed(ctx, "vae_pre", [&] { return launch_vae_pre(pa, st); }));
-    VaeStemArgs sa{P, v->stem.w, v->stem.b, X, B, v->H, v->W, v->Hc, v->Wc, v->Hp, v->Wp};
+    VaeStemArgs sa{P, v->stem_wpl, v->stem.b, X, B, v->H, v->W, v->Hc, v->Wc, v->Hp, v->Wp};
     HIPCHK(timed(ctx, "vae_stem", [&] { return launch_vae_stem(sa, st); }));
     int h = v->Hp, w = v->Wp, li = 0;
     for (int k = 0; k < 4; ++k) {

@@ -72,25 +72,26 @@ hipError_t launch_vae_pre(const VaePreArgs& a, hipStream_t s) {
 // ------------------------------------------------------------------------------------------------
 // stem: conv7x7/2 pad 3 (1 -> 64) + bias + ELU + maxpool3/2 pad 1 (vae.py:19-21), as an implicit GEMM on
 // the bf16 matrix pipe with fp32-exact products (the split of the ResBlock convolutions below):
-//   out[p][n] = sum_k A[p][k] W[k][n],  p = the 255 conv pixels of a workgroup's 7 x 8 pooled tile (15 x 17,
-//   one slot of padding: 8 row blocks of 32), n = 64 channels, k = the 49 taps padded to 64 (4 K-steps of
-//   16).  Each wave owns two row blocks x two channel blocks.  The weights are split once per workgroup into
-//   hi / mid / lo bf16 planes in LDS (B operand, k-contiguous rows); each lane gathers its pixel's 8 taps
-//   of a K-step from the input patch in LDS and splits them in registers (A operand).  Six
-//   v_mfma_f32_32x32x16_bf16 per block and K-step (al.bh, ah.bl, am.bm, am.bh, ah.bm, ah.bh) accumulate in
-//   fp32; the dropped products are <= 2^-24 relative.  Bias + ELU into the conv tile in LDS (aliasing the
-//   patch and the planes once the products are done), then the maxpool.
+//   out[p][n] = sum_k A[p][k] W[k][n],  p = the 255 conv pixels of a 7 x 8 pooled tile (15 x 17, one slot of
+//   padding: 8 pixel blocks of 32), n = 64 channels, k = 48 of the 49 taps (3 K-steps of 16, in the order
+//   of vae_stem_slot_tap) + tap 48 as one fp32 fma per output on the vector ALU.  Each wave owns two pixel
+//   blocks x two channel blocks.  The weights come split into hi / mid / lo bf16 planes (once at load,
+//   sdfnmpc_vae_load) and sit in registers for the workgroup's life; the input patch is split likewise, once
+//   per tile, into three bf16 planes in LDS, from which each lane gathers its pixel's taps (a horizontal tap
+//   pair = one 32-bit read).  Six v_mfma_f32_32x32x16_bf16 per block and K-step (al.bh, ah.bl, am.bm, am.bh,
+//   ah.bm, ah.bh) accumulate in fp32; the dropped products are <= 2^-24 relative.  conv + bias into the conv
+//   tile in LDS (over the patch), then the maxpool and the ELU of the pooled values, four channels per
+//   thread (16-byte LDS reads and global stores).  Persistent: two workgroups per CU walk the tiles, the next
+//   tile's patch loads in flight in registers under the current tile's products.
 constexpr int ST_PY = 7, ST_PX = 8;                        // pooled tile
 constexpr int ST_CY = 2 * ST_PY + 1, ST_CX = 2 * ST_PX + 1;  // conv tile 15 x 17 = 255 pixels
 constexpr int ST_IY = 2 * ST_CY + 5, ST_IX = 2 * ST_CX + 5;  // input patch 35 x 39
-constexpr int ST_IXP = ST_IX + 1;
-constexpr int ST_CS = 65;                                  // conv tile stride (floats): odd -> no conflicts
-constexpr int ST_KL = 72;                                  // weight-plane row stride (bf16): 144 B rows
-constexpr int ST_PATCH = ST_IY * ST_IXP;                   // floats
-constexpr int ST_WPL = 64 * ST_KL;                         // bf16 per weight plane
-constexpr int ST_LDS_A = ST_PATCH * 4 + 3 * ST_WPL * 2;    // patch + planes (bytes)
-constexpr int ST_LDS_C = ST_CY * ST_CX * ST_CS * 4;        // conv tile (bytes)
-constexpr int ST_LDS = ST_LDS_A > ST_LDS_C ? ST_LDS_A : ST_LDS_C;
+constexpr int ST_IXP = 2 * ((ST_IX + 1) / 2);               // patch row (bf16, even: 32-bit aligned pairs)
+constexpr int ST_CS = 68;                                  // conv tile row (floats): 16-byte rows for the pool
+constexpr int ST_PATCH = ST_IY * ST_IXP;                   // values per patch plane (bf16)
+constexpr int ST_CONV = ST_CY * ST_CX * ST_CS;             // floats
+constexpr int ST_LDS = (3 * ST_PATCH * 2 > ST_CONV * 4 ? 3 * ST_PATCH * 2 : ST_CONV * 4);
+static_assert(ST_IXP % 2 == 0 && ST_PATCH % 2 == 0, "32-bit tap-pair reads need even rows and planes");
 
 // x = hi + mid + lo exactly, each a bf16 truncation of the remainder (the split of split3_store)
 __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
@@ -101,128 +102,229 @@ __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsign
     l = __float_as_uint(r2) & 0xffff0000u;
 }
 
-__global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a) {
-    __shared__ __align__(16) unsigned char smem[ST_LDS];
-    float* patch = (float*)smem;
-    unsigned short* wpl = (unsigned short*)(smem + ST_PATCH * 4);  // [3][64 n][ST_KL]
-    float* conv = (float*)smem;                                    // after the products
-    const int t = threadIdx.x, img = blockIdx.z, lane = t & 63, wave = t >> 6, lr = lane & 31, lh = lane >> 5;
-    const int py0 = blockIdx.y * ST_PY, px0 = blockIdx.x * ST_PX;
-    const int gy0 = 4 * py0 - 5, gx0 = 4 * px0 - 5;
-    const float* in = a.in + (size_t)img * a.H * a.W;
-    for (int e = t; e < ST_IY * ST_IX; e += 256) {
-        const int r = e / ST_IX, c = e - r * ST_IX;
-        const int gy = gy0 + r, gx = gx0 + c;
-        patch[r * ST_IXP + c] = ((unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W) ? in[(size_t)gy * a.W + gx] : 0.f;
+// ELU(alpha = 1) = x for x > 0, expm1(x) otherwise (torch elu).  expm1 on x <= 0: the Taylor series to
+// x^8 / 8! on (-0.35, 0] (truncation <= 2.3e-10 relative, Horner in fp32), exp(x) - 1 below, where exp(x)
+// <= 0.71 leaves no cancellation; exp(x) as v_exp_f32(x log2 e): the rounding of the product costs at most
+// |x| exp(x) log2(e) 2^-24 <= 3.2e-8 absolute, under the fp32 rounding of the result.  A NaN stays a NaN.
+// ELU is increasing, so the kernel pools first and activates the pooled values only (4.6x fewer).  Two
+// values at a time: the series on the packed fp32 pipe (v_pk_fma_f32).
+typedef float float2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float2v elu2(float2v x) {
+    float2v p = (float2v)(1.0f / 40320.0f);
+    p = __builtin_elementwise_fma(p, x, (float2v)(1.0f / 5040.0f));
+    p = __builtin_elementwise_fma(p, x, (float2v)(1.0f / 720.0f));
+    p = __builtin_elementwise_fma(p, x, (float2v)(1.0f / 120.0f));
+    p = __builtin_elementwise_fma(p, x, (float2v)(1.0f / 24.0f));
+    p = __builtin_elementwise_fma(p, x, (float2v)(1.0f / 6.0f));
+    p = __builtin_elementwise_fma(p, x, (float2v)(0.5f));
+    const float2v taylor = __builtin_elementwise_fma(p * x, x, x);
+    const float2v y = x * 1.44269504088896341f;
+    const float2v viaexp = float2v{__builtin_amdgcn_exp2f(y.x), __builtin_amdgcn_exp2f(y.y)} - 1.0f;
+    return float2v{!(x.x <= 0.f) ? x.x : (x.x > -0.35f ? taylor.x : viaexp.x),
+                   !(x.y <= 0.f) ? x.y : (x.y > -0.35f ? taylor.y : viaexp.y)};
+}
+
+__device__ __forceinline__ float max9(const float4 (&v)[9], int f) {
+    float m[3];
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const float a = (&v[3 * r].x)[f], b = (&v[3 * r + 1].x)[f], c = (&v[3 * r + 2].x)[f];
+        m[r] = __builtin_elementwise_maximum(__builtin_elementwise_maximum(a, b), c);
     }
-    for (int e = t; e < 64 * 64; e += 256) {  // W[k][n] (tap-major) -> planes[n][k], taps 49..63 zero
-        const int n = e & 63, k = e >> 6;
-        unsigned h = 0, m = 0, l = 0;
-        if (k < 49) split3(a.w[k * 64 + n], h, m, l);
-        wpl[0 * ST_WPL + n * ST_KL + k] = (unsigned short)(h >> 16);
-        wpl[1 * ST_WPL + n * ST_KL + k] = (unsigned short)(m >> 16);
-        wpl[2 * ST_WPL + n * ST_KL + k] = (unsigned short)(l >> 16);
+    return __builtin_elementwise_maximum(__builtin_elementwise_maximum(m[0], m[1]), m[2]);
+}
+
+constexpr int ST_PRE = (ST_IY * ST_IX + 255) / 256;  // patch values per thread
+
+__global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a, int tiles_x, int tiles_img, int n_tiles) {
+    __shared__ __align__(16) float smem[ST_LDS / 4];  // the split patch, then the conv tile
+    __shared__ __align__(16) int poff[24];  // slot pair -> patch offset ky * ST_IXP + kx of its first tap from the
+                                            // pixel's tap 0; general pairs: both offsets, the second << 16
+    __shared__ __align__(16) float bias[64];
+    __shared__ __align__(16) float w48[64];           // tap 48 = (6, 6) of each channel, fp32
+    // [hi | mid | lo][row][column] bf16: a horizontal tap pair of a pixel is one aligned 32-bit word, and
+    // the stride-2 pixels of a lane group read consecutive words (conflict-free)
+    unsigned short* patch = (unsigned short*)smem;
+    float* conv = smem;  // after the products
+    const int t = threadIdx.x, lane = t & 63, wave = t >> 6, lr = lane & 31, lh = lane >> 5;
+    // the weight fragments of the three K-steps, once per workgroup: channel n = 32 j + lr, taps
+    // 16 s + 8 lh .. + 7 of each plane
+    bf16x8 bw[3][3][2];
+#pragma unroll
+    for (int s = 0; s < 3; ++s)
+#pragma unroll
+        for (int pl = 0; pl < 3; ++pl)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+                bw[s][pl][j] = *(const bf16x8*)&a.wpl[pl * VAE_STEM_PLANE + (32 * j + lr) * 64 + 16 * s + 8 * lh];
+    if (t < 24) {
+        const int k0 = vae_stem_slot_tap(2 * t), k1 = vae_stem_slot_tap(2 * t + 1);
+        const int o0 = (k0 / 7) * ST_IXP + k0 % 7, o1 = (k1 / 7) * ST_IXP + k1 % 7;
+        poff[t] = vae_stem_general_pair(t) ? o0 | (o1 << 16) : o0;
     }
-    __syncthreads();
-    // this lane's two pixels (row blocks i = 0, 1 of the wave): conv pixel q = 64 wave + 32 i + lr
-    int pbase[2];
+    if (t < 64) {
+        bias[t] = a.b[t];
+        // hi + mid + lo = the fp32 weight exactly
+        w48[t] = (__uint_as_float((unsigned)a.wpl[t * 64 + 48] << 16) +
+                  __uint_as_float((unsigned)a.wpl[VAE_STEM_PLANE + t * 64 + 48] << 16)) +
+                 __uint_as_float((unsigned)a.wpl[2 * VAE_STEM_PLANE + t * 64 + 48] << 16);
+    }
+    // this lane's two pixels (pixel blocks i = 0, 1 of the wave): conv pixel q = 64 wave + 32 i + lr
+    int pbase[2], pcy[2], pcx[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int q = wave * 64 + 32 * i + lr, qq = q < ST_CY * ST_CX ? q : 0;
-        const int cyl = qq / ST_CX, cxl = qq - cyl * ST_CX;
-        pbase[i] = (2 * cyl) * ST_IXP + 2 * cxl;
+        pcy[i] = qq / ST_CX;
+        pcx[i] = qq - pcy[i] * ST_CX;
+        pbase[i] = (2 * pcy[i]) * ST_IXP + 2 * pcx[i];
     }
-    floatx16 acc[2][2];
+    // the next tile's input patch, in flight in registers while this tile computes
+    float pre[ST_PRE];
+    auto fetch = [&](int tile) {
+        const int img = tile / tiles_img, tt = tile - img * tiles_img, ty = tt / tiles_x;
+        const int gy0 = 4 * ty * ST_PY - 5, gx0 = 4 * (tt - ty * tiles_x) * ST_PX - 5;
+        const float* in = a.in + (size_t)img * a.H * a.W;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+        for (int u = 0; u < ST_PRE; ++u) {
+            const int e = t + 256 * u, r = e / ST_IX, c = e - r * ST_IX, gy = gy0 + r, gx = gx0 + c;
+            pre[u] = e < ST_IY * ST_IX && (unsigned)gy < (unsigned)a.H && (unsigned)gx < (unsigned)a.W
+                         ? in[(size_t)gy * a.W + gx] : 0.f;
+        }
+    };
+    fetch(blockIdx.x);  // the grid is at most n_tiles workgroups
+    for (int tile = blockIdx.x; tile < n_tiles; tile += gridDim.x) {
+        const int img = tile / tiles_img, tt = tile - img * tiles_img, ty = tt / tiles_x;
+        const int py0 = ty * ST_PY, px0 = (tt - ty * tiles_x) * ST_PX;
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        // A: taps k = 16 s + 8 lh + jj of the lane's pixels, split in registers (padded taps read 0)
-        bf16x8 ah[2], am[2], al[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            unsigned hp[4], mp[4], lp[4];
-#pragma unroll
-            for (int jj = 0; jj < 8; jj += 2) {
-                float v2[2];
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const int k = 16 * s + 8 * lh + jj + u;     // lh is per lane: k < 49 is a lane predicate
-                    const int kc = k < 49 ? k : 48, ky = kc / 7, kx = kc - 7 * ky;
-                    const float v = patch[pbase[i] + ky * ST_IXP + kx];
-                    v2[u] = k < 49 ? v : 0.f;
-                }
-                unsigned h0, m0, l0, h1, m1, l1;
-                split3(v2[0], h0, m0, l0);
-                split3(v2[1], h1, m1, l1);
-                hp[jj / 2] = (h0 >> 16) | h1;
-                mp[jj / 2] = (m0 >> 16) | m1;
-                lp[jj / 2] = (l0 >> 16) | l1;
+        for (int u = 0; u < ST_PRE; ++u) {
+            const int e = t + 256 * u, r = e / ST_IX, c = e - r * ST_IX;
+            if (e < ST_IY * ST_IX) {
+                unsigned h, m, l;
+                split3(pre[u], h, m, l);
+                const int o = r * ST_IXP + c;
+                patch[o] = (unsigned short)(h >> 16);
+                patch[ST_PATCH + o] = (unsigned short)(m >> 16);
+                patch[2 * ST_PATCH + o] = (unsigned short)(l >> 16);
             }
-            ah[i] = __builtin_bit_cast(bf16x8, make_uint4(hp[0], hp[1], hp[2], hp[3]));
-            am[i] = __builtin_bit_cast(bf16x8, make_uint4(mp[0], mp[1], mp[2], mp[3]));
-            al[i] = __builtin_bit_cast(bf16x8, make_uint4(lp[0], lp[1], lp[2], lp[3]));
         }
-        // B: channel n = 32 j + lr, taps 16 s + 8 lh .. + 7 of each plane (16-byte reads)
-        bf16x8 bh[2], bm[2], bl[2];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            const int o = (32 * j + lr) * ST_KL + 16 * s + 8 * lh;
-            bh[j] = *(const bf16x8*)&wpl[0 * ST_WPL + o];
-            bm[j] = *(const bf16x8*)&wpl[1 * ST_WPL + o];
-            bl[j] = *(const bf16x8*)&wpl[2 * ST_WPL + o];
-        }
-#define ST_MM(X, Y)                                                                                   \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)         \
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[i], Y[j], acc[i][j], 0, 0, 0);
-        ST_MM(al, bh)
-        ST_MM(ah, bl)
-        ST_MM(am, bm)
-        ST_MM(am, bh)
-        ST_MM(ah, bm)
-        ST_MM(ah, bh)
-#undef ST_MM
-    }
-    __syncthreads();  // every wave is done with the patch and the planes: the conv tile takes their place
-    // epilogue: lane (lr, lh), register r holds row 8 (r / 4) + 4 lh + r % 4 (pixel), column lr (channel)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int c = 32 * j + lr;
-        const float bias = a.b[c];
+        __syncthreads();
+        if (tile + (int)gridDim.x < n_tiles) fetch(tile + gridDim.x);
+        // C^T = W^T A^T: rows = channels (the weight fragment is the first operand), columns = pixels, so
+        // each lane ends with four consecutive channels of one pixel per register quad (16-byte LDS writes)
+        floatx16 acc[2][2];
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int q = wave * 64 + 32 * i + 8 * (r >> 2) + 4 * lh + (r & 3);
-                if (q < ST_CY * ST_CX) {
-                    const int cyl = q / ST_CX, cxl = q - cyl * ST_CX;
-                    const int cy = 2 * py0 - 1 + cyl, cx = 2 * px0 - 1 + cxl;
-                    const bool ok = (unsigned)cy < (unsigned)a.Hc && (unsigned)cx < (unsigned)a.Wc;
-                    const float x = acc[i][j][r] + bias;
-                    const float v = x > 0.f ? x : expm1f(x);  // ELU(alpha = 1); a NaN stays a NaN
-                    conv[q * ST_CS + c] = ok ? v : -INFINITY;  // outside the map: never the max
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+                for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            // A: slots k = 16 s + 8 lh + 2 jj (+1) of the lane's pixels, slot pair 8 s + 4 lh + jj (offsets
+            // from the pair table: one 16-byte read), from the split planes: a horizontal pair is one 32-bit
+            // read per plane, a general pair (K-step 2, jj >= 2, for both lane halves) two 16-bit reads
+            const int4 of = *(const int4*)&poff[8 * s + 4 * lh];
+            const int pof[4] = {of.x, of.y, of.z, of.w};
+            bf16x8 ah[2], am[2], al[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                unsigned hp[4], mp[4], lp[4];
+#pragma unroll
+                for (int jj = 0; jj < 4; ++jj) {
+                    if (s == 2 && jj >= 2) {
+                        const unsigned short* p0 = patch + pbase[i] + (pof[jj] & 0xffff);
+                        const unsigned short* p1 = patch + pbase[i] + (pof[jj] >> 16);
+                        hp[jj] = p0[0] | ((unsigned)p1[0] << 16);
+                        mp[jj] = p0[ST_PATCH] | ((unsigned)p1[ST_PATCH] << 16);
+                        lp[jj] = p0[2 * ST_PATCH] | ((unsigned)p1[2 * ST_PATCH] << 16);
+                    } else {
+                        const unsigned* p0 = (const unsigned*)(patch + pbase[i] + pof[jj]);
+                        hp[jj] = p0[0];
+                        mp[jj] = p0[ST_PATCH / 2];
+                        lp[jj] = p0[ST_PATCH];
+                    }
                 }
+                ah[i] = __builtin_bit_cast(bf16x8, make_uint4(hp[0], hp[1], hp[2], hp[3]));
+                am[i] = __builtin_bit_cast(bf16x8, make_uint4(mp[0], mp[1], mp[2], mp[3]));
+                al[i] = __builtin_bit_cast(bf16x8, make_uint4(lp[0], lp[1], lp[2], lp[3]));
             }
-    }
-    __syncthreads();
-    const int c = t & 63;
-    for (int q = t >> 6; q < ST_PY * ST_PX; q += 4) {
-        const int pyl = q / ST_PX, pxl = q - pyl * ST_PX;
-        const int py = py0 + pyl, px = px0 + pxl;
-        if (py >= a.Hp || px >= a.Wp) continue;
-        float m = -INFINITY;
+#define ST_MM(X, PL)                                                                                    \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)           \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bw[s][PL][j], X[i], acc[i][j], 0, 0, 0);
+            ST_MM(al, 0)
+            ST_MM(ah, 2)
+            ST_MM(am, 1)
+            ST_MM(am, 0)
+            ST_MM(ah, 1)
+            ST_MM(ah, 0)
+#undef ST_MM
+        }
+        // tap 48, the 49th, on the vector ALU (one fp32 fma per output) rather than a fourth K-step that
+        // would be 15/16 padding: the lane's pixel value, hi + mid + lo = the fp32 input exactly
+        float x48[2];
 #pragma unroll
-        for (int dy = 0; dy < 3; ++dy)
+        for (int i = 0; i < 2; ++i) {
+            const unsigned short* p = patch + pbase[i] + 6 * ST_IXP + 6;  // (ky, kx) = (6, 6)
+            x48[i] = (__uint_as_float((unsigned)p[0] << 16) + __uint_as_float((unsigned)p[ST_PATCH] << 16)) +
+                     __uint_as_float((unsigned)p[2 * ST_PATCH] << 16);
+        }
+        __syncthreads();  // every wave is done with the patch: the conv tile takes its place
+        // epilogue: conv + bias (pre-activation) into the tile; lane (lr, lh), register r holds channel
+        // 32 j + 8 (r / 4) + 4 lh + r % 4 of pixel 64 wave + 32 i + lr.  Conv pixels outside the map (the
+        // pool's padding, the map's far edge) get -inf: they never win the pool.
+        const int cy0 = 2 * py0 - 1, cx0 = 2 * px0 - 1;
 #pragma unroll
-            for (int dx = 0; dx < 3; ++dx) {  // NaN-sticky, as torch's max_pool2d (fmaxf would drop it)
-                const float v = conv[((2 * pyl + dy) * ST_CX + 2 * pxl + dx) * ST_CS + c];
-                m = (v > m || v != v) ? v : m;
+        for (int i = 0; i < 2; ++i) {
+            const int q = wave * 64 + 32 * i + lr;
+            if (q >= ST_CY * ST_CX) continue;
+            if ((unsigned)(cy0 + pcy[i]) < (unsigned)a.Hc && (unsigned)(cx0 + pcx[i]) < (unsigned)a.Wc) {
+                const float2v x2 = (float2v)(x48[i]);
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g) {
+                        const int c = 32 * j + 8 * g + 4 * lh;
+                        const float4 b4 = *(const float4*)&bias[c], w4 = *(const float4*)&w48[c];
+                        const float2v lo = __builtin_elementwise_fma(x2, float2v{w4.x, w4.y}, float2v{acc[i][j][4 * g], acc[i][j][4 * g + 1]}) + float2v{b4.x, b4.y};
+                        const float2v hi = __builtin_elementwise_fma(x2, float2v{w4.z, w4.w}, float2v{acc[i][j][4 * g + 2], acc[i][j][4 * g + 3]}) + float2v{b4.z, b4.w};
+                        *(float4*)&conv[q * ST_CS + c] = make_float4(lo.x, lo.y, hi.x, hi.y);
+                    }
+            } else {
+#pragma unroll
+                for (int j = 0; j < 2; ++j)
+#pragma unroll
+                    for (int g = 0; g < 4; ++g)
+                        *(float4*)&conv[q * ST_CS + 32 * j + 8 * g + 4 * lh] = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
             }
-        a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c] = m;
+        }
+        __syncthreads();
+        // maxpool 3/2 of the pre-activations, then the ELU of the pooled value (ELU is increasing: the same
+        // result as pooling the activations, vae.py:19-21); thread -> (pooled pixel, four channels).
+        // NaN-sticky as torch's max_pool2d: IEEE 754-2019 maximum (v_maximum3_f32), which propagates a NaN
+        for (int e = t; e < ST_PY * ST_PX * 16; e += 256) {
+            const int q = e >> 4, c4 = 4 * (e & 15);
+            const int pyl = q >> 3, pxl = q & 7;
+            const int py = py0 + pyl, px = px0 + pxl;
+            if (py >= a.Hp || px >= a.Wp) continue;
+#ifdef STEM_DIAG_NOPOOL  // diagnostic builds only (tools/build_variant.sh)
+            *(float4*)&a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c4] = *(const float4*)&conv[((2 * pyl + 1) * ST_CX + 2 * pxl + 1) * ST_CS + c4];
+#else
+            float4 v[9];
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx)
+                    v[3 * dy + dx] = *(const float4*)&conv[((2 * pyl + dy) * ST_CX + 2 * pxl + dx) * ST_CS + c4];
+#ifdef STEM_DIAG_NOELU
+            *(float4*)&a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c4] =
+                make_float4(max9(v, 0), max9(v, 1), max9(v, 2), max9(v, 3));
+#else
+            const float2v e0 = elu2(float2v{max9(v, 0), max9(v, 1)}), e1 = elu2(float2v{max9(v, 2), max9(v, 3)});
+            *(float4*)&a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c4] = make_float4(e0.x, e0.y, e1.x, e1.y);
+#endif
+#endif
+        }
+        __syncthreads();  // the pool is done with the conv tile: the next patch takes its place
     }
 }
 
@@ -231,8 +333,19 @@ hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s) {
     if (a.Hc != (a.H - 1) / 2 + 1 || a.Wc != (a.W - 1) / 2 + 1 || a.Hp != (a.Hc - 1) / 2 + 1 ||
         a.Wp != (a.Wc - 1) / 2 + 1)
         return hipErrorInvalidValue;
-    dim3 grid((a.Wp + ST_PX - 1) / ST_PX, (a.Hp + ST_PY - 1) / ST_PY, a.B);
-    hipLaunchKernelGGL(vae_stem_kernel, grid, dim3(256), 0, s, a);
+    const int tiles_x = (a.Wp + ST_PX - 1) / ST_PX, tiles_img = tiles_x * ((a.Hp + ST_PY - 1) / ST_PY);
+    if ((long long)tiles_img * a.B > 0x7fffffff) return hipErrorInvalidValue;
+    const int n_tiles = tiles_img * a.B;
+    // persistent: two workgroups per CU (the 69 KB conv tile), each walking the tiles with a stride of
+    // the grid, the next tile's patch loads in flight under the current tile's products
+    static int n_cu = 0;
+    if (n_cu == 0) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
+            return hipErrorInvalidDevice;
+    }
+    const int grid = n_tiles < 2 * n_cu ? n_tiles : 2 * n_cu;
+    hipLaunchKernelGGL(vae_stem_kernel, dim3(grid), dim3(256), 0, s, a, tiles_x, tiles_img, n_tiles);
     return hipGetLastError();
 }
 

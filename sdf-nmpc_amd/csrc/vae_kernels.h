@@ -16,11 +16,47 @@ struct VaePreArgs {
 // conv7x7/2 (+bias) + ELU + maxpool3/2 (vae.py:19-21), NHWC output [B][Hp][Wp][64]
 struct VaeStemArgs {
     const float* in;   // [B][H][W]
-    const float* w;    // [7][7][64]   (tap-major: one uniform 64-channel row per tap)
+    const unsigned short* wpl;  // [3][64 n][64 k] bf16 bits: the weights split hi / mid / lo, slot k holding
+                                // tap vae_stem_slot_tap(k)
     const float* b;    // [64]
     float* out;        // [B][Hp][Wp][64]
     int B, H, W, Hc, Wc, Hp, Wp;
 };
+constexpr int VAE_STEM_PLANE = 64 * 64;  // bf16 per plane of VaeStemArgs::wpl
+
+// The stem's K order: slot k of a plane row holds tap vae_stem_slot_tap(k) = ky * 7 + kx (-1: zero).
+// Slots pair up (2p, 2p + 1).  Pairs 0..17, 20, 21 are horizontal neighbours (ky, kx), (ky, kx + 1) with kx
+// even, read from the patch as one 32-bit word; pairs 18, 19, 22 join two rows' kx = 6 taps and pair 23 is
+// (6, 4), (6, 5), read as two 16-bit values (the "general" pairs: K-step 2, slots 2 and 3 of both lane
+// halves).  Slot 48 is tap (6, 6), applied on the vector ALU; 49..63 are zero.
+constexpr bool vae_stem_general_pair(int p) { return p == 18 || p == 19 || p == 22 || p == 23; }
+constexpr int vae_stem_slot_tap(int k) {
+    if (k == 48) return 48;
+    if (k > 48 || k < 0) return -1;
+    const int p = k / 2, h = k % 2;
+    if (p == 18 || p == 19 || p == 22) {
+        const int r = 2 * (p == 18 ? 0 : p == 19 ? 1 : 2) + h;  // rows 0..5, column 6
+        return r * 7 + 6;
+    }
+    if (p == 23) return 6 * 7 + 4 + h;
+    const int m = p < 18 ? p : p - 2;  // adjacent pairs 0..19
+    return (m / 3) * 7 + 2 * (m % 3) + h;
+}
+constexpr bool vae_stem_order_ok() {  // every tap exactly once; horizontal pairs start at an even column
+    int seen[49] = {};
+    for (int k = 0; k < 64; ++k) {
+        const int t = vae_stem_slot_tap(k);
+        if (t < 0) continue;
+        if (t > 48 || seen[t]++) return false;
+        if (k < 48 && k % 2 == 0 && !vae_stem_general_pair(k / 2) &&
+            (t % 7 % 2 != 0 || vae_stem_slot_tap(k + 1) != t + 1))
+            return false;
+    }
+    for (int t = 0; t < 49; ++t)
+        if (!seen[t]) return false;
+    return true;
+}
+static_assert(vae_stem_order_ok(), "stem K order");
 
 // implicit-GEMM convolution (BatchNorm folded) + bias (+ residual) (+ ReLU), NHWC
 struct VaeConvArgs {
