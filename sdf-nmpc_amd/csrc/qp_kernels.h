@@ -32,7 +32,10 @@ struct QpArgs {
 
 constexpr int QP_REC = 304;   // stage record: [A B | c | g | C^T | H upper | 0 ..] (128-B rows) (rti_qp.hip)
 constexpr int QP_FREC = 192;  // factor record: [A~|b~ | K|k_ff (rows of 12) | chol(R^) (1/diag) | P_{k+1} c_k | 4 junk]
-constexpr int QP_RING = 3;    // stream positions in flight per wavefront
+#ifndef QP_RING_DEPTH
+#define QP_RING_DEPTH 3
+#endif
+constexpr int QP_RING = QP_RING_DEPTH;  // stream positions in flight per wavefront
 constexpr int QP_SLOT = 5;    // 64-double loads per stream position (committed LDS window = 320 doubles)
 // segmented kernel (rti_qp_seg.hip): four wavefronts per instance, each a segment of the horizon
 constexpr int QP_NSEG = 4;  // at most

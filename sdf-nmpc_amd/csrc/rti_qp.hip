@@ -37,6 +37,7 @@
 #include <hip/hip_runtime.h>
 
 #include <type_traits>
+#include <utility>
 
 #include "qp_kernels.h"
 #include "qp_dev.h"
@@ -70,9 +71,14 @@ __host__ __device__ constexpr int load_at(int K, int j) {
 // 64-lane load touches only the cache lines the stage uses)
 __host__ __device__ constexpr int f_end(int K) { return (K == 2 || K == 4) ? F_FW : F_J; }
 __host__ __device__ constexpr int r_end(int K) { return K == 1 ? REC : R_CT + 30; }
-static_assert(FREC == F_J + 4 && (REC * 8) % 128 == 0 && (FREC * 8) % 128 == 0 && F_FW <= WF_CT && FREC <= 192 && PD == 3 && SLOT == 5, "record layout");
+static_assert(FREC == F_J + 4 && (REC * 8) % 128 == 0 && (FREC * 8) % 128 == 0 && F_FW <= WF_CT && FREC <= 192 && PD >= 2 && SLOT == 5, "record layout");
 static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT && WB_R + 96 + 128 <= 64 * SLOT && (96 * 8) % 128 == 0 && R_Z < 64 * SLOT,
               "window layout");
+
+template <typename Fn, int... S>
+__device__ __forceinline__ void for_each_ic(Fn& fn, std::integer_sequence<int, S...>) {
+    (fn(IC<S>{}), ...);
+}
 
 struct Smem {
     ldsd *t, *lam;                 // [m] inequality slacks / duals
@@ -359,6 +365,8 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     // commits; the window loads of every kind are unpredicated (clamped addresses).
     const int NP = (N1 + PD - 1) / PD * PD;
     double ring[PD][SLOT];
+    // fn(IC<S>) for the ring slots S = 0 .. PD - 1 in order (static slots: the loops are unrolled by PD)
+    auto each_slot = [](auto&& fn) { for_each_ic(fn, std::make_integer_sequence<int, PD>{}); };
     auto issue = [&](auto KIc, double* rs, int q) {
         constexpr int KI = decltype(KIc)::value;
         const int qq = q < N ? q : N;
@@ -1015,31 +1023,34 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         }();
         using T_ = IC<1>;
         using F_ = IC<0>;
+        // slot S of a trip: position q0 + S (the first position of the sweep is its first node: the
+        // terminal node of a backward sweep)
         if (NP > PD) {
-            // first trip: position 0 is the sweep's first node (terminal node of a backward sweep)
-            position(Kc, Kc, IC<0>{}, T_{}, 0, PD, true, ln);
-            position(Kc, Kc, IC<1>{}, F_{}, 1, 1 + PD, true, ln);
-            position(Kc, Kc, IC<2>{}, F_{}, 2, 2 + PD, true, ln);
+            // first trip
+            each_slot([&](auto Sc) {
+                constexpr int S = decltype(Sc)::value;
+                position(Kc, Kc, Sc, std::conditional_t<S == 0, T_, F_>{}, S, S + PD, true, ln);
+            });
             int q0 = PD;
-            for (; q0 < NP - PD; q0 += PD) {  // every position of these trips is a node
-                position(Kc, Kc, IC<0>{}, F_{}, q0, q0 + PD, true, ln);
-                position(Kc, Kc, IC<1>{}, F_{}, q0 + 1, q0 + 1 + PD, true, ln);
-                position(Kc, Kc, IC<2>{}, F_{}, q0 + 2, q0 + 2 + PD, true, ln);
-            }
+            for (; q0 < NP - PD; q0 += PD)  // every position of these trips is a node
+                each_slot([&](auto Sc) {
+                    constexpr int S = decltype(Sc)::value;
+                    position(Kc, Kc, Sc, F_{}, q0 + S, q0 + S + PD, true, ln);
+                });
             // last trip: refill with the next sweep's first positions; tail positions compute nothing
-            position(Kc, IC<KN>{}, IC<0>{}, F_{}, q0, 0, q0 < N1, ln);
-            position(Kc, IC<KN>{}, IC<1>{}, F_{}, q0 + 1, 1, q0 + 1 < N1, ln);
-            position(Kc, IC<KN>{}, IC<2>{}, F_{}, q0 + 2, 2, q0 + 2 < N1, ln);
+            each_slot([&](auto Sc) {
+                constexpr int S = decltype(Sc)::value;
+                position(Kc, IC<KN>{}, Sc, F_{}, q0 + S, S, q0 + S < N1, ln);
+            });
         } else {  // N + 1 <= PD: a single trip
-            position(Kc, IC<KN>{}, IC<0>{}, T_{}, 0, 0, true, ln);
-            position(Kc, IC<KN>{}, IC<1>{}, F_{}, 1, 1, 1 < N1, ln);
-            position(Kc, IC<KN>{}, IC<2>{}, F_{}, 2, 2, 2 < N1, ln);
+            each_slot([&](auto Sc) {
+                constexpr int S = decltype(Sc)::value;
+                position(Kc, IC<KN>{}, Sc, std::conditional_t<S == 0, T_, F_>{}, S, S, S == 0 || S < N1, ln);
+            });
         }
     };
 
-    issue(IC<0>{}, ring[0], 0);
-    issue(IC<0>{}, ring[1], 1);
-    issue(IC<0>{}, ring[2], 2);
+    each_slot([&](auto Sc) { issue(IC<0>{}, ring[decltype(Sc)::value], decltype(Sc)::value); });
     sweep(IC<0>{});
     STAMP(1);
     rp = rows_init();
