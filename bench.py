@@ -484,7 +484,7 @@ def bench_scene(device, B=1024, N=40, warm_steps=6, steps=10):
     o.ctx.enable_timing(False)
     it = np.array(iters)
     res = {"workload": f"{B} instances x N={N}, obstacle-scene SDF net (deployed architecture fitted to a pillar "
-                       "and a box), closed loop past the pillar, timed steps {warm_steps}..{warm_steps + steps - 1}",
+                       f"and a box), closed loop past the pillar, timed steps {warm_steps}..{warm_steps + steps - 1}",
            "kernel_ms": kms, "qp_iters_max": int(it.max()), "qp_iters_mean": float(it.mean()),
            "qp_iters_max_per_step": [int(v) for v in it.max(axis=1)],
            "sdf_active_frac": float(np.mean(active)), "instances_with_active_sdf_row_per_step":
