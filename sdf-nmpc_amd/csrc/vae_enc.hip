@@ -356,13 +356,20 @@ hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s) {
 // 16-byte slots (conflict-free).  Within a K-tile, MFMA step s feeds lane half h with k = 8h + s
 // (the same permutation for A and B), so each lane reads its 8 k-values with two ds_read_b128.
 constexpr int CV_BM = 128, CV_BN = 128, CV_BK = 16;
-[[maybe_unused]] constexpr int CV_LD = 20;  // the VAE_F32_MFMA diagnostic build's fp32 row stride
 constexpr int CV_SLD = 24;  // bf16 plane row stride (48 bytes)
 
 // fp32 -> three bf16 by truncation: x = hi + mid + lo EXACTLY (each takes the next 8 significant bits of
 // the 24; the remainders are exact fp32 differences).  A float4 of one row -> its 4-bf16 pieces of the
 // hi / mid / lo planes (8-byte stores).
 __device__ __forceinline__ void split3_store(float4 v, unsigned short (*planes)[CV_BM * CV_SLD], int off) {
+#ifdef VAE_DIAG_NOSPLIT  // diagnostic build (tools/build_variant.sh): the time without the split's VALU work
+    const uint2 q = make_uint2((__float_as_uint(v.x) >> 16) | (__float_as_uint(v.y) & 0xffff0000u),
+                               (__float_as_uint(v.z) >> 16) | (__float_as_uint(v.w) & 0xffff0000u));
+    *(uint2*)&planes[0][off] = q;
+    *(uint2*)&planes[1][off] = q;
+    *(uint2*)&planes[2][off] = q;
+    return;
+#endif
     const float x[4] = {v.x, v.y, v.z, v.w};
     unsigned hb[4], mb[4], lb[4];
 #pragma unroll
@@ -383,18 +390,18 @@ __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
     return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
 }
 
+#ifndef VAE_LOAD_DEPTH
+#define VAE_LOAD_DEPTH 2
+#endif
+constexpr int CV_D = VAE_LOAD_DEPTH;  // K-tiles whose global loads are in flight in registers
+
 template <int KS, int S>
 __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
     constexpr int P = KS / 2;
-#ifdef VAE_F32_MFMA
-    __shared__ float As[2][CV_BM * CV_LD];
-    __shared__ float Bs[2][CV_BN * CV_LD];
-#else
     // the K-tile split ONCE, by the thread that loads it, into bf16 hi / mid / lo planes: rows of 16 bf16
     // at a 24-bf16 (48-byte) stride, so the lane groups of a ds_read_b128 hit distinct 16-byte slots
     __shared__ __align__(16) unsigned short As3[2][3][CV_BM * CV_SLD];
     __shared__ __align__(16) unsigned short Bs3[2][3][CV_BN * CV_SLD];
-#endif
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
     const int M = a.B * a.Ho * a.Wo, MT = (M + CV_BM - 1) / CV_BM;
@@ -414,51 +421,42 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
     const float* pa1 = a.in + (size_t)im1 * a.Hi * a.Wi * Cin + 4 * kq;
     const float* pb0 = a.w + (size_t)(nt * CV_BN + (tid >> 2)) * K + 4 * kq;
     const float* pb1 = pb0 + (size_t)64 * K;
-#ifdef VAE_F32_MFMA
-    const int srow0 = (tid >> 2) * CV_LD + 4 * kq, srow1 = srow0 + 64 * CV_LD;
-#endif
-
-    float4 ra0, ra1, rb0, rb1;
-    int ky = 0, kx = 0, c0 = 0;  // K-tile position (tap, channel block) being loaded
-#define VAE_LOAD(kt)                                                                                          \
-    do {                                                                                                      \
-        const int iy0_ = iyA + ky, ix0_ = ixA + kx, iy1_ = iyB + ky, ix1_ = ixB + kx;                          \
-        const bool ok0_ = v0 && (unsigned)iy0_ < (unsigned)a.Hi && (unsigned)ix0_ < (unsigned)a.Wi;           \
-        const bool ok1_ = v1 && (unsigned)iy1_ < (unsigned)a.Hi && (unsigned)ix1_ < (unsigned)a.Wi;           \
-        /* always load from a valid address (the image origin when outside), then select */                  \
-        const float4 t0_ = *(const float4*)(pa0 + (ok0_ ? ((size_t)iy0_ * a.Wi + ix0_) * Cin + c0 : 0));         \
-        const float4 t1_ = *(const float4*)(pa1 + (ok1_ ? ((size_t)iy1_ * a.Wi + ix1_) * Cin + c0 : 0));         \
-        ra0 = sel4(ok0_, t0_);                                                                                \
-        ra1 = sel4(ok1_, t1_);                                                                                \
-        rb0 = *(const float4*)(pb0 + (size_t)(kt) * CV_BK);                                                   \
-        rb1 = *(const float4*)(pb1 + (size_t)(kt) * CV_BK);                                                   \
-        c0 += CV_BK;                                                                                          \
-        if (c0 == Cin) {                                                                                      \
-            c0 = 0;                                                                                           \
-            if (++kx == KS) {                                                                                 \
-                kx = 0;                                                                                       \
-                ++ky;                                                                                         \
-            }                                                                                                 \
-        }                                                                                                     \
-    } while (0)
-#ifdef VAE_F32_MFMA
-#define VAE_STASH(buf)                                        \
-    do {                                                      \
-        *(float4*)(&As[buf][srow0]) = ra0;                    \
-        *(float4*)(&As[buf][srow1]) = ra1;                    \
-        *(float4*)(&Bs[buf][srow0]) = rb0;                    \
-        *(float4*)(&Bs[buf][srow1]) = rb1;                    \
-    } while (0)
-#else
     const int hrow0 = (tid >> 2) * CV_SLD + 4 * kq, hrow1 = hrow0 + 64 * CV_SLD;
-#define VAE_STASH(buf)                                        \
-    do {                                                      \
-        split3_store(ra0, As3[buf], hrow0);                   \
-        split3_store(ra1, As3[buf], hrow1);                   \
-        split3_store(rb0, Bs3[buf], hrow0);                   \
-        split3_store(rb1, Bs3[buf], hrow1);                   \
-    } while (0)
-#endif
+
+    // a ring of CV_D register sets (A rows m0, m1; B columns n0, n1 of one K-tile): the loads of K-tile
+    // kt + 1 + CV_D are issued when tile kt + 1 has been stashed.  Depth 2, 3 and 4 measure the same
+    // (15.5 / 15.6 / 15.6 ms of convolutions per 512 images): the loop is not load-latency bound.
+    float4 ring[CV_D][4];
+    int ky = 0, kx = 0, c0 = 0, kl = 0;  // the next K-tile to load: tap (ky, kx), channel block c0, index kl
+    auto load = [&](float4(&r)[4]) {
+        if (kl < KT) {
+            const int iy0 = iyA + ky, ix0 = ixA + kx, iy1 = iyB + ky, ix1 = ixB + kx;
+            const bool ok0 = v0 && (unsigned)iy0 < (unsigned)a.Hi && (unsigned)ix0 < (unsigned)a.Wi;
+            const bool ok1 = v1 && (unsigned)iy1 < (unsigned)a.Hi && (unsigned)ix1 < (unsigned)a.Wi;
+            // always load from a valid address (the image origin when outside), then select
+            const float4 t0 = *(const float4*)(pa0 + (ok0 ? ((size_t)iy0 * a.Wi + ix0) * Cin + c0 : 0));
+            const float4 t1 = *(const float4*)(pa1 + (ok1 ? ((size_t)iy1 * a.Wi + ix1) * Cin + c0 : 0));
+            r[0] = sel4(ok0, t0);
+            r[1] = sel4(ok1, t1);
+            r[2] = *(const float4*)(pb0 + (size_t)kl * CV_BK);
+            r[3] = *(const float4*)(pb1 + (size_t)kl * CV_BK);
+            c0 += CV_BK;
+            if (c0 == Cin) {
+                c0 = 0;
+                if (++kx == KS) {
+                    kx = 0;
+                    ++ky;
+                }
+            }
+        }
+        ++kl;
+    };
+    auto stash = [&](int buf, const float4(&r)[4]) {
+        split3_store(r[0], As3[buf], hrow0);
+        split3_store(r[1], As3[buf], hrow1);
+        split3_store(r[2], Bs3[buf], hrow0);
+        split3_store(r[3], Bs3[buf], hrow1);
+    };
 
     floatx16 acc[2][2];
 #pragma unroll
@@ -468,40 +466,12 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    VAE_LOAD(0);
-    VAE_STASH(0);
-    __syncthreads();
-    for (int kt = 0; kt < KT; ++kt) {
-        const int buf = kt & 1;
-        if (kt + 1 < KT) VAE_LOAD(kt + 1);
-#ifdef VAE_F32_MFMA
-        float av[2][8], bv[2][8];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const float* ap = &As[buf][(wm * 64 + 32 * i + lr) * CV_LD + 8 * lh];
-            const float* bp = &Bs[buf][(wn * 64 + 32 * i + lr) * CV_LD + 8 * lh];
-            const float4 a0 = *(const float4*)ap, a1 = *(const float4*)(ap + 4);
-            const float4 b0 = *(const float4*)bp, b1 = *(const float4*)(bp + 4);
-            av[i][0] = a0.x; av[i][1] = a0.y; av[i][2] = a0.z; av[i][3] = a0.w;
-            av[i][4] = a1.x; av[i][5] = a1.y; av[i][6] = a1.z; av[i][7] = a1.w;
-            bv[i][0] = b0.x; bv[i][1] = b0.y; bv[i][2] = b0.z; bv[i][3] = b0.w;
-            bv[i][4] = b1.x; bv[i][5] = b1.y; bv[i][6] = b1.z; bv[i][7] = b1.w;
-        }
-        // diagnostic: the exact-fp32 MFMA (eight 32x32x2 steps per K-tile)
-#pragma unroll
-        for (int s = 0; s < 8; ++s)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j)
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[i][s], bv[j][s], acc[i][j], 0, 0, 0);
-#else
+    auto products = [&](int buf) {
         // fp32 products on the bf16 matrix pipe: a = ah + am + al, b = bh + bm + bl exactly, and the six
         // products down to 2^-16 relative (al.bh, ah.bl, am.bm, am.bh, ah.bm, ah.bh; smallest first)
         // are accumulated in fp32 -- the dropped ones (am.bl, al.bm, al.bl) are <= 2^-24 relative, the
         // fp32 rounding level.  One 32x32x16 K-step covers the K-tile (lane half h: k = 8h .. 8h + 7,
-        // the same permutation for A and B).  6 x 32 cycles of the matrix pipe per block and K-tile
-        // against 8 x 64 for the fp32 MFMA.
+        // the same permutation for A and B).  6 x 32 cycles of the matrix pipe per block and K-tile.
         bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -516,16 +486,41 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
 #define VAE_MM(X, Y)                                                                                   \
     _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)         \
         acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[i], Y[j], acc[i][j], 0, 0, 0);
+#ifndef VAE_DIAG_ONEMM  // diagnostic build: one product per block and K-tile instead of six (results invalid)
         VAE_MM(al, bh)
         VAE_MM(ah, bl)
         VAE_MM(am, bm)
         VAE_MM(am, bh)
         VAE_MM(ah, bm)
+#else
+        (void)al; (void)bl; (void)am; (void)bm;
+#endif
         VAE_MM(ah, bh)
 #undef VAE_MM
-#endif
-        if (kt + 1 < KT) VAE_STASH(buf ^ 1);
-        __syncthreads();
+    };
+
+    // prologue: K-tiles 0 .. CV_D - 1 in flight, tile 0 stashed, slot 0 refilled with tile CV_D
+#pragma unroll
+    for (int d = 0; d < CV_D; ++d) load(ring[d]);
+    stash(0, ring[0]);
+    load(ring[0]);
+    __syncthreads();
+    // K-tile kt: products from LDS buffer kt & 1; then tile kt + 1 (ring slot (kt + 1) % CV_D) is split
+    // into the other buffer and its slot refilled with tile kt + 1 + CV_D.  Unrolled by CV_D so that the
+    // ring slots are static registers.
+    for (int kt0 = 0; kt0 < KT; kt0 += CV_D) {
+#pragma unroll
+        for (int d = 0; d < CV_D; ++d) {
+            const int kt = kt0 + d;
+            if (kt < KT) {
+                products(kt & 1);
+                if (kt + 1 < KT) {
+                    stash((kt + 1) & 1, ring[(d + 1) % CV_D]);
+                    load(ring[(d + 1) % CV_D]);
+                }
+                __syncthreads();
+            }
+        }
     }
 
     // epilogue: lane (lr, lh), register r holds row 8(r/4) + 4 lh + r%4, column lr of each block
@@ -547,8 +542,6 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
                 }
             }
     }
-#undef VAE_LOAD
-#undef VAE_STASH
 }
 
 hipError_t launch_vae_conv(const VaeConvArgs& a, int ks, int stride, hipStream_t s) {
