@@ -1532,6 +1532,7 @@ extern "C" int sdfnmpc_shooting_grid(int N, double T, int uniform, int n_short, 
 struct VaeLayer {
     const float* w = nullptr;
     const float* b = nullptr;
+    const unsigned short* wpl = nullptr;  // convolutions: w split into bf16 planes (VaeConvArgs::wpl)
     int cin = 0, cout = 0, ks = 0, stride = 0;
 };
 
@@ -1591,9 +1592,34 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
         return fail(SDFNMPC_E_FORMAT, "vaew: parameter count does not match the reference encoder");
     }
     // + the stem weights split exactly into three bf16 planes [3][64 n][64 k] (vae_enc.hip's split3), in
-    // the kernel's K order (vae_stem_slot_tap), appended after the layers (16-byte aligned)
+    // the kernel's K order (vae_stem_slot_tap), appended after the layers (16-byte aligned), then every
+    // ResBlock convolution's weights split the same way into planes [3][Cout][K] (16-byte aligned each)
+    auto split3 = [](float x, unsigned short* hi, unsigned short* mid, unsigned short* lo) {
+        uint32_t u, hb, mb, lb;
+        memcpy(&u, &x, 4);
+        hb = u & 0xffff0000u;
+        float hf, r1, mf, r2;
+        memcpy(&hf, &hb, 4);
+        r1 = x - hf;  // exact (the leading 8 significant bits removed)
+        memcpy(&u, &r1, 4);
+        mb = u & 0xffff0000u;
+        memcpy(&mf, &mb, 4);
+        r2 = r1 - mf;
+        memcpy(&u, &r2, 4);
+        lb = u & 0xffff0000u;
+        *hi = (unsigned short)(hb >> 16);
+        *mid = (unsigned short)(mb >> 16);
+        *lo = (unsigned short)(lb >> 16);
+    };
     const size_t wpl_off = (need + 3) & ~(size_t)3;
-    std::vector<float> dev(wpl_off + 3 * VAE_STEM_PLANE / 2, 0.0f);
+    size_t cpl_end = wpl_off + 3 * VAE_STEM_PLANE / 2;  // in floats
+    std::vector<size_t> cpl_off(specs.size(), 0);
+    for (size_t li = 1; li + 1 < specs.size(); ++li) {
+        cpl_off[li] = cpl_end;
+        const size_t nw = (size_t)specs[li].cout * specs[li].ks * specs[li].ks * specs[li].cin;
+        cpl_end += ((3 * nw + 1) / 2 + 3) & ~(size_t)3;
+    }
+    std::vector<float> dev(cpl_end, 0.0f);
     size_t off = 0;
     for (size_t li = 0; li < specs.size(); ++li) {
         const Spec& s = specs[li];
@@ -1603,29 +1629,16 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
             for (int c = 0; c < 64; ++c)
                 for (int t = 0; t < 49; ++t) dev[off + t * 64 + c] = src[off + c * 49 + t];
             for (int c = 0; c < 64; ++c)
-                for (int k = 0; k < 49; ++k) {
-                    const float x = src[off + c * 49 + vae_stem_slot_tap(k)];
-                    uint32_t u, hb, mb, lb;
-                    memcpy(&u, &x, 4);
-                    hb = u & 0xffff0000u;
-                    float hf, r1, mf, r2;
-                    memcpy(&hf, &hb, 4);
-                    r1 = x - hf;  // exact (the leading 8 significant bits removed)
-                    memcpy(&u, &r1, 4);
-                    mb = u & 0xffff0000u;
-                    memcpy(&mf, &mb, 4);
-                    r2 = r1 - mf;
-                    memcpy(&u, &r2, 4);
-                    lb = u & 0xffff0000u;
-                    wpl[0 * VAE_STEM_PLANE + c * 64 + k] = (unsigned short)(hb >> 16);
-                    wpl[1 * VAE_STEM_PLANE + c * 64 + k] = (unsigned short)(mb >> 16);
-                    wpl[2 * VAE_STEM_PLANE + c * 64 + k] = (unsigned short)(lb >> 16);
-                }
+                for (int k = 0; k < 49; ++k)
+                    split3(src[off + c * 49 + vae_stem_slot_tap(k)], &wpl[0 * VAE_STEM_PLANE + c * 64 + k],
+                           &wpl[1 * VAE_STEM_PLANE + c * 64 + k], &wpl[2 * VAE_STEM_PLANE + c * 64 + k]);
         } else if (li + 1 == specs.size()) {  // head [L][2048] -> [2048][L]
             for (int o = 0; o < s.cout; ++o)
                 for (int f = 0; f < 2048; ++f) dev[off + (size_t)f * s.cout + o] = src[off + (size_t)o * 2048 + f];
         } else {
             memcpy(&dev[off], src + off, nw * 4);
+            unsigned short* pl = (unsigned short*)&dev[cpl_off[li]];
+            for (size_t e = 0; e < nw; ++e) split3(src[off + e], &pl[e], &pl[nw + e], &pl[2 * nw + e]);
         }
         memcpy(&dev[off + nw], src + off + nw, (size_t)s.cout * 4);
         off += nw + s.cout;
@@ -1642,7 +1655,8 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
     off = 0;
     for (size_t li = 0; li < specs.size(); ++li) {
         const Spec& s = specs[li];
-        VaeLayer L{d + off, d + off + (size_t)s.cout * s.ks * s.ks * s.cin, s.cin, s.cout, s.ks, s.stride};
+        VaeLayer L{d + off, d + off + (size_t)s.cout * s.ks * s.ks * s.cin,
+                   cpl_off[li] ? (const unsigned short*)(d + cpl_off[li]) : nullptr, s.cin, s.cout, s.ks, s.stride};
         if (li == 0) v->stem = L;
         else if (li + 1 == specs.size()) v->head = L;
         else v->conv[li - 1] = L;
@@ -1695,17 +1709,17 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
     for (int k = 0; k < 4; ++k) {
         const int s = kVaeBlockStride[k], ho = v->bh[k], wo = v->bw[k];
         const VaeLayer& ca = v->conv[li++];
-        VaeConvArgs a1{X, ca.w, ca.b, nullptr, T, B, h, w, ca.cin, ho, wo, ca.cout, 1};
+        VaeConvArgs a1{X, ca.w, ca.wpl, ca.b, nullptr, T, B, h, w, ca.cin, ho, wo, ca.cout, 1};
         HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a1, 3, s, st); }));
         const float* resid = X;
         if (s != 1) {
             const VaeLayer& cs = v->conv[li++];
-            VaeConvArgs a2{X, cs.w, cs.b, nullptr, S, B, h, w, cs.cin, ho, wo, cs.cout, 0};
+            VaeConvArgs a2{X, cs.w, cs.wpl, cs.b, nullptr, S, B, h, w, cs.cin, ho, wo, cs.cout, 0};
             HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a2, 1, s, st); }));
             resid = S;
         }
         const VaeLayer& cb = v->conv[li++];
-        VaeConvArgs a3{T, cb.w, cb.b, resid, Y, B, ho, wo, cb.cin, ho, wo, cb.cout, 1};
+        VaeConvArgs a3{T, cb.w, cb.wpl, cb.b, resid, Y, B, ho, wo, cb.cin, ho, wo, cb.cout, 1};
         HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a3, 3, 1, st); }));
         std::swap(X, Y);
         h = ho;

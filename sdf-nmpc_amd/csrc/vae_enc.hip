@@ -361,13 +361,13 @@ constexpr int CV_SLD = 24;  // bf16 plane row stride (48 bytes)
 // fp32 -> three bf16 by truncation: x = hi + mid + lo EXACTLY (each takes the next 8 significant bits of
 // the 24; the remainders are exact fp32 differences).  A float4 of one row -> its 4-bf16 pieces of the
 // hi / mid / lo planes (8-byte stores).
-__device__ __forceinline__ void split3_store(float4 v, unsigned short (*planes)[CV_BM * CV_SLD], int off) {
+__device__ __forceinline__ void split3_store(float4 v, unsigned short* planes, int pstride, int off) {
 #ifdef VAE_DIAG_NOSPLIT  // diagnostic build (tools/build_variant.sh): the time without the split's VALU work
     const uint2 q = make_uint2((__float_as_uint(v.x) >> 16) | (__float_as_uint(v.y) & 0xffff0000u),
                                (__float_as_uint(v.z) >> 16) | (__float_as_uint(v.w) & 0xffff0000u));
-    *(uint2*)&planes[0][off] = q;
-    *(uint2*)&planes[1][off] = q;
-    *(uint2*)&planes[2][off] = q;
+    *(uint2*)&planes[off] = q;
+    *(uint2*)&planes[pstride + off] = q;
+    *(uint2*)&planes[2 * pstride + off] = q;
     return;
 #endif
     const float x[4] = {v.x, v.y, v.z, v.w};
@@ -380,9 +380,9 @@ __device__ __forceinline__ void split3_store(float4 v, unsigned short (*planes)[
         const float r2 = r1 - __uint_as_float(mb[q]);
         lb[q] = __float_as_uint(r2) & 0xffff0000u;
     }
-    *(uint2*)&planes[0][off] = make_uint2((hb[0] >> 16) | hb[1], (hb[2] >> 16) | hb[3]);
-    *(uint2*)&planes[1][off] = make_uint2((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3]);
-    *(uint2*)&planes[2][off] = make_uint2((lb[0] >> 16) | lb[1], (lb[2] >> 16) | lb[3]);
+    *(uint2*)&planes[off] = make_uint2((hb[0] >> 16) | hb[1], (hb[2] >> 16) | hb[3]);
+    *(uint2*)&planes[pstride + off] = make_uint2((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3]);
+    *(uint2*)&planes[2 * pstride + off] = make_uint2((lb[0] >> 16) | lb[1], (lb[2] >> 16) | lb[3]);
 }
 
 // component-wise select (a ?: on the float4 struct goes through a stack slot)
@@ -419,16 +419,23 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
     const int iyA = oy0 * S - P, ixA = ox0 * S - P, iyB = oy1 * S - P, ixB = ox1 * S - P;
     const float* pa0 = a.in + (size_t)im0 * a.Hi * a.Wi * Cin + 4 * kq;
     const float* pa1 = a.in + (size_t)im1 * a.Hi * a.Wi * Cin + 4 * kq;
-    const float* pb0 = a.w + (size_t)(nt * CV_BN + (tid >> 2)) * K + 4 * kq;
-    const float* pb1 = pb0 + (size_t)64 * K;
+    // B from the weight planes split at load: column tid / 2, k-values 8 (tid % 2) .. + 7 (16 bytes) of
+    // each plane
+    const size_t wps = (size_t)a.Cout * K;
+    const unsigned short* pb = a.wpl + (size_t)(nt * CV_BN + (tid >> 1)) * K + 8 * (tid & 1);
+    const int brow = (tid >> 1) * CV_SLD + 8 * (tid & 1);
     const int hrow0 = (tid >> 2) * CV_SLD + 4 * kq, hrow1 = hrow0 + 64 * CV_SLD;
 
     // a ring of CV_D register sets (A rows m0, m1; B columns n0, n1 of one K-tile): the loads of K-tile
     // kt + 1 + CV_D are issued when tile kt + 1 has been stashed.  Depth 2, 3 and 4 measure the same
     // (15.5 / 15.6 / 15.6 ms of convolutions per 512 images): the loop is not load-latency bound.
-    float4 ring[CV_D][4];
+    struct Stage {
+        float4 a0, a1;  // A rows m0, m1 (fp32, split at the stash)
+        uint4 b[3];     // B: hi / mid / lo (split at load)
+    };
+    Stage ring[CV_D];
     int ky = 0, kx = 0, c0 = 0, kl = 0;  // the next K-tile to load: tap (ky, kx), channel block c0, index kl
-    auto load = [&](float4(&r)[4]) {
+    auto load = [&](Stage& r) {
         if (kl < KT) {
             const int iy0 = iyA + ky, ix0 = ixA + kx, iy1 = iyB + ky, ix1 = ixB + kx;
             const bool ok0 = v0 && (unsigned)iy0 < (unsigned)a.Hi && (unsigned)ix0 < (unsigned)a.Wi;
@@ -436,10 +443,10 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
             // always load from a valid address (the image origin when outside), then select
             const float4 t0 = *(const float4*)(pa0 + (ok0 ? ((size_t)iy0 * a.Wi + ix0) * Cin + c0 : 0));
             const float4 t1 = *(const float4*)(pa1 + (ok1 ? ((size_t)iy1 * a.Wi + ix1) * Cin + c0 : 0));
-            r[0] = sel4(ok0, t0);
-            r[1] = sel4(ok1, t1);
-            r[2] = *(const float4*)(pb0 + (size_t)kl * CV_BK);
-            r[3] = *(const float4*)(pb1 + (size_t)kl * CV_BK);
+            r.a0 = sel4(ok0, t0);
+            r.a1 = sel4(ok1, t1);
+#pragma unroll
+            for (int p = 0; p < 3; ++p) r.b[p] = *(const uint4*)(pb + p * wps + (size_t)kl * CV_BK);
             c0 += CV_BK;
             if (c0 == Cin) {
                 c0 = 0;
@@ -451,11 +458,11 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
         }
         ++kl;
     };
-    auto stash = [&](int buf, const float4(&r)[4]) {
-        split3_store(r[0], As3[buf], hrow0);
-        split3_store(r[1], As3[buf], hrow1);
-        split3_store(r[2], Bs3[buf], hrow0);
-        split3_store(r[3], Bs3[buf], hrow1);
+    auto stash = [&](int buf, const Stage& r) {
+        split3_store(r.a0, As3[buf][0], CV_BM * CV_SLD, hrow0);
+        split3_store(r.a1, As3[buf][0], CV_BM * CV_SLD, hrow1);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) *(uint4*)&Bs3[buf][p][brow] = r.b[p];
     };
 
     floatx16 acc[2][2];

@@ -62,6 +62,7 @@ static_assert(vae_stem_order_ok(), "stem K order");
 struct VaeConvArgs {
     const float* in;     // [B][Hi][Wi][Cin]
     const float* w;      // [Cout][KS][KS][Cin]
+    const unsigned short* wpl;  // the same weights split into bf16 planes [3 hi/mid/lo][Cout][KS KS Cin] (at load)
     const float* b;      // [Cout]
     const float* resid;  // [B][Ho][Wo][Cout] or nullptr
     float* out;          // [B][Ho][Wo][Cout]
