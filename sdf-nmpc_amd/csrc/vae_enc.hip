@@ -356,7 +356,20 @@ hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s) {
 // 16-byte slots (conflict-free).  Within a K-tile, MFMA step s feeds lane half h with k = 8h + s
 // (the same permutation for A and B), so each lane reads its 8 k-values with two ds_read_b128.
 constexpr int CV_BM = 128, CV_BN = 128, CV_BK = 16;
-constexpr int CV_SLD = 24;  // bf16 plane row stride (48 bytes)
+#ifndef VAE_CONV_WGS
+#define VAE_CONV_WGS 3
+#endif
+// bf16 plane rows of 16 k-values, 32 bytes, unpadded; the two 16-byte halves of rows 8..15 of every 16
+// swapped (row bit 3), so the lane groups of the fragments' ds_read_b128 hit 16 distinct 16-byte slots
+// and the staging stores stay contiguous.  Two stages x 3 planes x 256 rows = 48 KB: three workgroups
+// per CU (the 48-byte padded rows took 72 KB, two per CU).
+#if VAE_CONV_WGS == 3
+constexpr int CV_SLD = 16;
+__device__ __forceinline__ int cv_off(int row, int half) { return row * 16 + 8 * (half ^ ((row >> 3) & 1)); }
+#else  // diagnostic build: the round-3 layout (48-byte rows, two workgroups per CU)
+constexpr int CV_SLD = 24;
+__device__ __forceinline__ int cv_off(int row, int half) { return row * 24 + 8 * half; }
+#endif
 
 // fp32 -> three bf16 by truncation: x = hi + mid + lo EXACTLY (each takes the next 8 significant bits of
 // the 24; the remainders are exact fp32 differences).  A float4 of one row -> its 4-bf16 pieces of the
@@ -396,7 +409,7 @@ __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
 constexpr int CV_D = VAE_LOAD_DEPTH;  // K-tiles whose global loads are in flight in registers
 
 template <int KS, int S>
-__global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
+__global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs a) {
     constexpr int P = KS / 2;
     // the K-tile split ONCE, by the thread that loads it, into bf16 hi / mid / lo planes: rows of 16 bf16
     // at a 24-bf16 (48-byte) stride, so the lane groups of a ds_read_b128 hit distinct 16-byte slots
@@ -423,8 +436,8 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
     // each plane
     const size_t wps = (size_t)a.Cout * K;
     const unsigned short* pb = a.wpl + (size_t)(nt * CV_BN + (tid >> 1)) * K + 8 * (tid & 1);
-    const int brow = (tid >> 1) * CV_SLD + 8 * (tid & 1);
-    const int hrow0 = (tid >> 2) * CV_SLD + 4 * kq, hrow1 = hrow0 + 64 * CV_SLD;
+    const int brow = cv_off(tid >> 1, tid & 1);
+    const int hrow0 = cv_off(tid >> 2, kq >> 1) + 4 * (kq & 1), hrow1 = cv_off((tid >> 2) + 64, kq >> 1) + 4 * (kq & 1);
 
     // a ring of CV_D register sets (A rows m0, m1; B columns n0, n1 of one K-tile): the loads of K-tile
     // kt + 1 + CV_D are issued when tile kt + 1 has been stashed.  Depth 2, 3 and 4 measure the same
@@ -482,7 +495,7 @@ __global__ __launch_bounds__(256) void vae_conv_kernel(VaeConvArgs a) {
         bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-            const int ao = (wm * 64 + 32 * i + lr) * CV_SLD + 8 * lh, bo = (wn * 64 + 32 * i + lr) * CV_SLD + 8 * lh;
+            const int ao = cv_off(wm * 64 + 32 * i + lr, lh), bo = cv_off(wn * 64 + 32 * i + lr, lh);
             ah[i] = *(const bf16x8*)&As3[buf][0][ao];
             am[i] = *(const bf16x8*)&As3[buf][1][ao];
             al[i] = *(const bf16x8*)&As3[buf][2][ao];
