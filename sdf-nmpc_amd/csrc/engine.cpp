@@ -1685,7 +1685,7 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
     const int B = o->B;
     if (B == 0) return SDFNMPC_OK;
     ScopedDevice sd(ctx->device);
-    // workspace: pre [B][H][W] | X | Y (block in/out ping-pong) | T (conv_a) | S (shortcut)
+    // workspace: pre [B][H][W] | X | Y (block in/out ping-pong) | T (conv_a) | S (shortcut) | F (head features)
     const size_t n_pre = (size_t)v->H * v->W;
     size_t n_x = (size_t)v->Hp * v->Wp * 64, n_t = 0;
     for (int k = 0; k < 4; ++k) {
@@ -1693,13 +1693,14 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
         n_x = std::max(n_x, nb);
         n_t = std::max(n_t, nb);
     }
-    const size_t per = n_pre + 2 * n_x + 2 * n_t;
+    const size_t per = n_pre + 2 * n_x + 2 * n_t + 2048;
     HIPCHK(v->ws.ensure(per * B * sizeof(float)));
     float* P = (float*)v->ws.p;
     float* X = P + n_pre * B;
     float* Y = X + n_x * B;
     float* T = Y + n_x * B;
     float* S = T + n_t * B;
+    float* F = S + n_t * B;  // [B][2048] pooled head features
     hipStream_t st = ctx->stream;
     VaePreArgs pa{img, o->dtype, B, o->in_h, o->in_w, v->H, v->W, o->clip, o->yz, P};
     HIPCHK(timed(ctx, "vae_pre", [&] { return launch_vae_pre(pa, st); }));
@@ -1725,7 +1726,7 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
         h = ho;
         w = wo;
     }
-    VaeHeadArgs ha{X, v->head.w, v->head.b, latent, latent64, B, h, w, v->L};
+    VaeHeadArgs ha{X, F, v->head.w, v->head.b, latent, latent64, B, h, w, v->L};
     HIPCHK(timed(ctx, "vae_head", [&] { return launch_vae_head(ha, st); }));
     return SDFNMPC_OK;
 }

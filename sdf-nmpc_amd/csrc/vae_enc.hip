@@ -586,54 +586,71 @@ hipError_t launch_vae_conv(const VaeConvArgs& a, int ks, int stride, hipStream_t
 
 // ------------------------------------------------------------------------------------------------
 // head: AdaptiveAvgPool2d((2,2)) (bin i spans [floor(i h/2), ceil((i+1) h/2))), Flatten (c*4 + i*2 + j),
-// mean Linear.  4 images per workgroup; features in LDS, the [2048][L] weight read once per workgroup.
-constexpr int HD_IMG = 4;
+// mean Linear, as two launches spread over the chip:
+//   vae_pool_kernel    one workgroup per (image, 256 channels), a thread per channel and its four bins
+//                      (coalesced across channels) -> feat [B][2048]
+//   vae_linear_kernel  one workgroup per (4 images, 32 outputs): eight K-slices of 256 features per output,
+//                      summed in a fixed order (bias, then slices 0..7), so a latent does not depend on its
+//                      batch neighbours.
+// (Round 3 ran both in one workgroup per 4 images, 128 workgroups with a 2048-long serial loop: 0.59 ms
+// per 512 images.)
+__global__ __launch_bounds__(256) void vae_pool_kernel(VaeHeadArgs a) {
+    const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
+    const float* in = a.in + (size_t)b * a.h * a.w * 512 + c;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+            const int y0 = (i * a.h) / 2, y1 = ((i + 1) * a.h + 1) / 2;
+            const int x0 = (j * a.w) / 2, x1 = ((j + 1) * a.w + 1) / 2;
+            float s = 0.f;
+            for (int y = y0; y < y1; ++y)
+                for (int x = x0; x < x1; ++x) s += in[((size_t)y * a.w + x) * 512];
+            a.feat[(size_t)b * 2048 + c * 4 + i * 2 + j] = s / (float)((y1 - y0) * (x1 - x0));
+        }
+}
 
-__global__ __launch_bounds__(256) void vae_head_kernel(VaeHeadArgs a) {
-    __shared__ float feat[HD_IMG][2048];
+constexpr int HD_IMG = 4, HD_OUT = 32, HD_KS = 8;
+
+__global__ __launch_bounds__(256) void vae_linear_kernel(VaeHeadArgs a) {
+    __shared__ float fs[HD_IMG][2048];
+    __shared__ float red[HD_KS][HD_IMG][HD_OUT];
     const int t = threadIdx.x, b0 = blockIdx.x * HD_IMG;
-    for (int q = 0; q < HD_IMG; ++q) {
-        const int b = b0 + q;
-        for (int c = t; c < 512; c += 256)
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    float s = 0.f;
-                    const int y0 = (i * a.h) / 2, y1 = ((i + 1) * a.h + 1) / 2;
-                    const int x0 = (j * a.w) / 2, x1 = ((j + 1) * a.w + 1) / 2;
-                    if (b < a.B)
-                        for (int y = y0; y < y1; ++y)
-                            for (int x = x0; x < x1; ++x) s += a.in[(((size_t)b * a.h + y) * a.w + x) * 512 + c];
-                    feat[q][c * 4 + i * 2 + j] = s / (float)((y1 - y0) * (x1 - x0));
-                }
+    for (int e = t; e < HD_IMG * 2048; e += 256) {
+        const int q = e >> 11, f = e & 2047;
+        fs[q][f] = b0 + q < a.B ? a.feat[(size_t)(b0 + q) * 2048 + f] : 0.f;
     }
     __syncthreads();
-    const int pair = t >> 7;  // images 2 pair, 2 pair + 1 (wave-uniform)
-    for (int o = t & 127; o < a.L; o += 128) {
-        float s0 = a.b[o], s1 = s0;
-        const float* f0 = feat[2 * pair];
-        const float* f1 = feat[2 * pair + 1];
-        for (int f = 0; f < 2048; ++f) {
-            const float w = a.wt[(size_t)f * a.L + o];
-            s0 = fmaf(w, f0[f], s0);
-            s1 = fmaf(w, f1[f], s1);
+    const int ks = t / HD_OUT, ol = t % HD_OUT, o = blockIdx.y * HD_OUT + ol;
+    float p[HD_IMG] = {0.f, 0.f, 0.f, 0.f};
+    if (o < a.L) {
+        const float* w = a.wt + o;
+#pragma unroll 8
+        for (int f = ks * 256; f < ks * 256 + 256; ++f) {
+            const float wv = w[(size_t)f * a.L];
+#pragma unroll
+            for (int q = 0; q < HD_IMG; ++q) p[q] = fmaf(wv, fs[q][f], p[q]);
         }
-        const int bA = b0 + 2 * pair, bB = bA + 1;
-        if (bA < a.B) {
-            a.latent[(size_t)bA * a.L + o] = s0;
-            if (a.latent64) a.latent64[(size_t)bA * a.L + o] = (double)s0;
-        }
-        if (bB < a.B) {
-            a.latent[(size_t)bB * a.L + o] = s1;
-            if (a.latent64) a.latent64[(size_t)bB * a.L + o] = (double)s1;
+    }
+#pragma unroll
+    for (int q = 0; q < HD_IMG; ++q) red[ks][q][ol] = p[q];
+    __syncthreads();
+    if (t < HD_IMG * HD_OUT) {
+        const int q = t / HD_OUT, b = b0 + q, oo = blockIdx.y * HD_OUT + (t % HD_OUT);
+        if (b < a.B && oo < a.L) {
+            float s = a.b[oo];
+#pragma unroll
+            for (int k = 0; k < HD_KS; ++k) s += red[k][q][t % HD_OUT];
+            a.latent[(size_t)b * a.L + oo] = s;
+            if (a.latent64) a.latent64[(size_t)b * a.L + oo] = (double)s;
         }
     }
 }
 
 hipError_t launch_vae_head(const VaeHeadArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    hipLaunchKernelGGL(vae_head_kernel, dim3((a.B + HD_IMG - 1) / HD_IMG), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(vae_pool_kernel, dim3(a.B, 2), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(vae_linear_kernel, dim3((a.B + HD_IMG - 1) / HD_IMG, (a.L + HD_OUT - 1) / HD_OUT), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

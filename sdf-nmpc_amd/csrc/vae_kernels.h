@@ -72,6 +72,7 @@ struct VaeConvArgs {
 // AdaptiveAvgPool2d((2,2)) + Flatten + mean Linear (vae.py:26-30, 42-43)
 struct VaeHeadArgs {
     const float* in;     // [B][h][w][512]
+    float* feat;         // [B][2048] workspace: the pooled, flattened features
     const float* wt;     // [2048][L]  (transposed mean.weight)
     const float* b;      // [L]
     float* latent;       // [B][L]
