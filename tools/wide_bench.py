@@ -12,6 +12,8 @@ from sdf_nmpc_amd.config import Config  # noqa: E402
 
 
 def main(B=512, N=60, steps=10):
+    if os.environ.get("SDFNMPC_LIB"):  # a diagnostic build (tools/build_variant.sh)
+        _lib.LIB_PATH = os.environ["SDFNMPC_LIB"]
     cfg = Config(mpc__N=N)
     ctx = _lib.Context(0, stream=torch.cuda.current_stream().cuda_stream)
     net = _lib.Net.from_blob(ctx, W.pack(W.WIDE_SPEC, W.siren_weights(W.WIDE_SPEC, 0)))
