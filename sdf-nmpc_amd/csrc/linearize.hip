@@ -87,7 +87,10 @@ __device__ __forceinline__ dd qerr3(const dd* x, const double* qd) {
     return (((x[3] * qd[3] + x[4] * qd[2]) - x[5] * qd[1]) - x[6] * qd[0]) * inv;
 }
 
-__global__ __launch_bounds__(256) void linearize_kernel(LinArgs A) {
+#ifndef LIN_WAVES
+#define LIN_WAVES 1
+#endif
+__global__ __launch_bounds__(256, LIN_WAVES) void linearize_kernel(LinArgs A) {
     const int tid = threadIdx.x;
     const int t = tid & 15;                           // tangent direction of this lane
     const long long r = (long long)blockIdx.x * 16 + (tid >> 4);  // node row = b * (N+1) + k
