@@ -86,7 +86,11 @@ hipError_t launch_vae_pre(const VaePreArgs& a, hipStream_t s) {
 constexpr int ST_PY = 7, ST_PX = 8;                        // pooled tile
 constexpr int ST_CY = 2 * ST_PY + 1, ST_CX = 2 * ST_PX + 1;  // conv tile 15 x 17 = 255 pixels
 constexpr int ST_IY = 2 * ST_CY + 5, ST_IX = 2 * ST_CX + 5;  // input patch 35 x 39
-constexpr int ST_IXP = 2 * ((ST_IX + 1) / 2);               // patch row (bf16, even: 32-bit aligned pairs)
+// patch row stride (bf16): even (32-bit aligned tap pairs) and 24 words, so one conv row further (two patch
+// rows, 48 words = 16 banks) puts a lane group's second conv row on the other half of the banks: the 32
+// lanes of a gather (17 + 15 pixels of two conv rows) hit distinct banks but one (40 bf16 rows: 2-way)
+constexpr int ST_IXP = 48;
+static_assert(ST_IXP >= ST_IX + 1 && ST_IXP % 2 == 0, "patch row");
 constexpr int ST_CS = 68;                                  // conv tile row (floats): 16-byte rows for the pool
 constexpr int ST_PATCH = ST_IY * ST_IXP;                   // values per patch plane (bf16)
 constexpr int ST_CONV = ST_CY * ST_CX * ST_CS;             // floats
@@ -301,8 +305,14 @@ __global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a, int til
         // maxpool 3/2 of the pre-activations, then the ELU of the pooled value (ELU is increasing: the same
         // result as pooling the activations, vae.py:19-21); thread -> (pooled pixel, four channels).
         // NaN-sticky as torch's max_pool2d: IEEE 754-2019 maximum (v_maximum3_f32), which propagates a NaN
+        // lane -> (pooled pixel, four channels) so that each 16-lane group of a ds_read_b128
+        // ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31} and the same + 32) reads one pixel's 256 contiguous
+        // bytes (conflict-free); with 16 consecutive lanes per pixel, the groups straddled two pixels
+        // two conv columns (544 B) apart
         for (int e = t; e < ST_PY * ST_PX * 16; e += 256) {
-            const int q = e >> 4, c4 = 4 * (e & 15);
+            const int L = e & 31, g1 = L < 4 || (L >= 12 && L < 16) || (L >= 20 && L < 28);
+            const int rk = g1 ? (L < 4 ? L : L < 16 ? L - 8 : L - 12) : (L < 12 ? L - 4 : L < 20 ? L - 8 : L - 16);
+            const int q = 2 * (e >> 5) + (g1 ? 0 : 1), c4 = 4 * rk;
             const int pyl = q >> 3, pxl = q & 7;
             const int py = py0 + pyl, px = px0 + pxl;
             if (py >= a.Hp || px >= a.Wp) continue;
