@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a, int til
             const int py = py0 + pyl, px = px0 + pxl;
             if (py >= a.Hp || px >= a.Wp) continue;
 #ifdef STEM_DIAG_NOPOOL  // diagnostic builds only (tools/build_variant.sh)
-            *(float4*)&a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c4] = *(const float4*)&conv[((2 * pyl + 1) * ST_CX + 2 * pxl + 1) * ST_CS + c4];
+            *(float4*)&a.out[((size_t)img * 64 + (c4 & ~15)) * a.Hp * a.Wp + (py * a.Wp + px) * 16 + (c4 & 15)] = *(const float4*)&conv[((2 * pyl + 1) * ST_CX + 2 * pxl + 1) * ST_CS + c4];
 #else
             float4 v[9];
 #pragma unroll
@@ -326,11 +326,13 @@ __global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a, int til
                 for (int dx = 0; dx < 3; ++dx)
                     v[3 * dy + dx] = *(const float4*)&conv[((2 * pyl + dy) * ST_CX + 2 * pxl + dx) * ST_CS + c4];
 #ifdef STEM_DIAG_NOELU
-            *(float4*)&a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c4] =
+            *(float4*)&a.out[((size_t)img * 64 + (c4 & ~15)) * a.Hp * a.Wp + (py * a.Wp + px) * 16 + (c4 & 15)] =
                 make_float4(max9(v, 0), max9(v, 1), max9(v, 2), max9(v, 3));
 #else
             const float2v e0 = elu2(float2v{max9(v, 0), max9(v, 1)}), e1 = elu2(float2v{max9(v, 2), max9(v, 3)});
-            *(float4*)&a.out[(((size_t)img * a.Hp + py) * a.Wp + px) * 64 + c4] = make_float4(e0.x, e0.y, e1.x, e1.y);
+            // channel-blocked output [B][4][Hp][Wp][16] (the convolutions' layout)
+            *(float4*)&a.out[((size_t)img * 64 + (c4 & ~15)) * a.Hp * a.Wp + (py * a.Wp + px) * 16 + (c4 & 15)] =
+                make_float4(e0.x, e0.y, e1.x, e1.y);
 #endif
 #endif
         }
@@ -440,8 +442,12 @@ __global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs
     const int im0 = q0 / HW, r0 = q0 - im0 * HW, oy0 = r0 / a.Wo, ox0 = r0 - oy0 * a.Wo;
     const int im1 = q1 / HW, r1 = q1 - im1 * HW, oy1 = r1 / a.Wo, ox1 = r1 - oy1 * a.Wo;
     const int iyA = oy0 * S - P, ixA = ox0 * S - P, iyB = oy1 * S - P, ixB = ox1 * S - P;
-    const float* pa0 = a.in + (size_t)im0 * a.Hi * a.Wi * Cin + 4 * kq;
-    const float* pa1 = a.in + (size_t)im1 * a.Hi * a.Wi * Cin + 4 * kq;
+    // activations channel-blocked, [B][C / 16][H][W][16] (VaeConvArgs): a K-tile's 16 channels of
+    // consecutive pixels are consecutive 64-byte pieces, so a load instruction's 16 rows x 4 quarters
+    // read 1 KB of whole cache lines (NHWC spread them over 16 lines, half of each used)
+    const size_t HWi = (size_t)a.Hi * a.Wi;
+    const float* pa0 = a.in + (size_t)im0 * HWi * Cin + 4 * kq;
+    const float* pa1 = a.in + (size_t)im1 * HWi * Cin + 4 * kq;
     // B from the weight planes split at load: column tid / 2, k-values 8 (tid % 2) .. + 7 (16 bytes) of
     // each plane
     const size_t wps = (size_t)a.Cout * K;
@@ -458,16 +464,31 @@ __global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs
     };
     Stage ring[CV_D];
     int ky = 0, kx = 0, c0 = 0, kl = 0;  // the next K-tile to load: tap (ky, kx), channel block c0, index kl
+    // the rows' pixel pointers and validity for the current tap, recomputed only when the tap changes
+    // (every Cin / 16 K-tiles); a K-tile then adds the uniform channel-block offset c0 (H W)
+    const float *ap0 = pa0, *ap1 = pa1;
+    bool ok0 = false, ok1 = false;
+    auto tap = [&]() {
+        const int iy0 = iyA + ky, ix0 = ixA + kx, iy1 = iyB + ky, ix1 = ixB + kx;
+        ok0 = v0 && (unsigned)iy0 < (unsigned)a.Hi && (unsigned)ix0 < (unsigned)a.Wi;
+        ok1 = v1 && (unsigned)iy1 < (unsigned)a.Hi && (unsigned)ix1 < (unsigned)a.Wi;
+        // outside the map: the image origin (a valid address), the value selected away
+        ap0 = pa0 + (ok0 ? ((size_t)iy0 * a.Wi + ix0) * 16 : 0);
+        ap1 = pa1 + (ok1 ? ((size_t)iy1 * a.Wi + ix1) * 16 : 0);
+    };
+    tap();
     auto load = [&](Stage& r) {
         if (kl < KT) {
-            const int iy0 = iyA + ky, ix0 = ixA + kx, iy1 = iyB + ky, ix1 = ixB + kx;
-            const bool ok0 = v0 && (unsigned)iy0 < (unsigned)a.Hi && (unsigned)ix0 < (unsigned)a.Wi;
-            const bool ok1 = v1 && (unsigned)iy1 < (unsigned)a.Hi && (unsigned)ix1 < (unsigned)a.Wi;
-            // always load from a valid address (the image origin when outside), then select
-            const float4 t0 = *(const float4*)(pa0 + (ok0 ? ((size_t)iy0 * a.Wi + ix0) * Cin + c0 : 0));
-            const float4 t1 = *(const float4*)(pa1 + (ok1 ? ((size_t)iy1 * a.Wi + ix1) * Cin + c0 : 0));
+            const float4 t0 = *(const float4*)(ap0 + (size_t)c0 * HWi);
+            const float4 t1 = *(const float4*)(ap1 + (size_t)c0 * HWi);
+#ifdef VAE_DIAG_NOALOAD  // diagnostic build: A from registers, not memory (results invalid)
+            (void)t0; (void)t1;
+            r.a0 = make_float4(1.f + c0, 2.f, 3.f, 4.f);
+            r.a1 = make_float4(5.f, 6.f + kx, 7.f, 8.f);
+#else
             r.a0 = sel4(ok0, t0);
             r.a1 = sel4(ok1, t1);
+#endif
 #pragma unroll
             for (int p = 0; p < 3; ++p) r.b[p] = *(const uint4*)(pb + p * wps + (size_t)kl * CV_BK);
             c0 += CV_BK;
@@ -477,6 +498,7 @@ __global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs
                     kx = 0;
                     ++ky;
                 }
+                tap();
             }
         }
         ++kl;
@@ -548,7 +570,11 @@ __global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs
                     stash((kt + 1) & 1, ring[(d + 1) % CV_D]);
                     load(ring[(d + 1) % CV_D]);
                 }
+#ifdef VAE_DIAG_NOSYNC  // diagnostic build: no barrier per K-tile (results invalid)
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+#else
                 __syncthreads();
+#endif
             }
         }
     }
@@ -564,7 +590,8 @@ __global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs
             for (int r = 0; r < 16; ++r) {
                 const int m = mt * CV_BM + wm * 64 + 32 * i + 8 * (r >> 2) + 4 * lh + (r & 3);
                 if (m < M) {
-                    const size_t o = (size_t)m * a.Cout + n;
+                    const int img = m / HW, pix = m - img * HW;  // channel-blocked output
+                    const size_t o = ((size_t)img * a.Cout + (n & ~15)) * HW + pix * 16 + (n & 15);
                     float v = acc[i][j][r] + bias;
                     if (a.resid) v += a.resid[o];
                     if (a.relu) v = v < 0.f ? 0.f : v;  // torch.relu keeps a NaN (fmaxf would drop it)
@@ -606,7 +633,7 @@ hipError_t launch_vae_conv(const VaeConvArgs& a, int ks, int stride, hipStream_t
 // per 512 images.)
 __global__ __launch_bounds__(256) void vae_pool_kernel(VaeHeadArgs a) {
     const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
-    const float* in = a.in + (size_t)b * a.h * a.w * 512 + c;
+    const float* in = a.in + ((size_t)b * 512 + (c & ~15)) * a.h * a.w + (c & 15);  // channel-blocked
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -615,7 +642,7 @@ __global__ __launch_bounds__(256) void vae_pool_kernel(VaeHeadArgs a) {
             const int x0 = (j * a.w) / 2, x1 = ((j + 1) * a.w + 1) / 2;
             float s = 0.f;
             for (int y = y0; y < y1; ++y)
-                for (int x = x0; x < x1; ++x) s += in[((size_t)y * a.w + x) * 512];
+                for (int x = x0; x < x1; ++x) s += in[((size_t)y * a.w + x) * 16];
             a.feat[(size_t)b * 2048 + c * 4 + i * 2 + j] = s / (float)((y1 - y0) * (x1 - x0));
         }
 }

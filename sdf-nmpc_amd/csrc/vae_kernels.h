@@ -13,13 +13,13 @@ struct VaePreArgs {
     float* out;        // [B][H][W]
 };
 
-// conv7x7/2 (+bias) + ELU + maxpool3/2 (vae.py:19-21), NHWC output [B][Hp][Wp][64]
+// conv7x7/2 (+bias) + ELU + maxpool3/2 (vae.py:19-21), channel-blocked output [B][64/16][Hp][Wp][16]
 struct VaeStemArgs {
     const float* in;   // [B][H][W]
     const unsigned short* wpl;  // [3][64 n][64 k] bf16 bits: the weights split hi / mid / lo, slot k holding
                                 // tap vae_stem_slot_tap(k)
     const float* b;    // [64]
-    float* out;        // [B][Hp][Wp][64]
+    float* out;        // [B][4][Hp][Wp][16]
     int B, H, W, Hc, Wc, Hp, Wp;
 };
 constexpr int VAE_STEM_PLANE = 64 * 64;  // bf16 per plane of VaeStemArgs::wpl
@@ -58,20 +58,21 @@ constexpr bool vae_stem_order_ok() {  // every tap exactly once; horizontal pair
 }
 static_assert(vae_stem_order_ok(), "stem K order");
 
-// implicit-GEMM convolution (BatchNorm folded) + bias (+ residual) (+ ReLU), NHWC
+// implicit-GEMM convolution (BatchNorm folded) + bias (+ residual) (+ ReLU); activations channel-blocked,
+// [B][C/16][H][W][16]
 struct VaeConvArgs {
-    const float* in;     // [B][Hi][Wi][Cin]
+    const float* in;     // [B][Cin/16][Hi][Wi][16]
     const float* w;      // [Cout][KS][KS][Cin]
     const unsigned short* wpl;  // the same weights split into bf16 planes [3 hi/mid/lo][Cout][KS KS Cin] (at load)
     const float* b;      // [Cout]
-    const float* resid;  // [B][Ho][Wo][Cout] or nullptr
-    float* out;          // [B][Ho][Wo][Cout]
+    const float* resid;  // [B][Cout/16][Ho][Wo][16] or nullptr
+    float* out;          // [B][Cout/16][Ho][Wo][16]
     int B, Hi, Wi, Cin, Ho, Wo, Cout, relu;
 };
 
 // AdaptiveAvgPool2d((2,2)) + Flatten + mean Linear (vae.py:26-30, 42-43)
 struct VaeHeadArgs {
-    const float* in;     // [B][h][w][512]
+    const float* in;     // [B][512/16][h][w][16]
     float* feat;         // [B][2048] workspace: the pooled, flattened features
     const float* wt;     // [2048][L]  (transposed mean.weight)
     const float* b;      // [L]
