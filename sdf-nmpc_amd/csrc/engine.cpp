@@ -1544,6 +1544,7 @@ struct sdfnmpc_vae {
     void* dmem = nullptr;
     VaeLayer stem, conv[11], head;  // conv: b0a b0s b0b b1a b1s b1b b2a b2s b2b b3a b3b
     const unsigned short* stem_wpl = nullptr;  // the stem weights split into bf16 planes (VaeStemArgs::wpl)
+    const float* zero16 = nullptr;              // 16 zero floats (VaeConvArgs::zero16)
     DevBuf ws;
     int ws_B = 0;
 };
@@ -1619,7 +1620,8 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
         const size_t nw = (size_t)specs[li].cout * specs[li].ks * specs[li].ks * specs[li].cin;
         cpl_end += ((3 * nw + 1) / 2 + 3) & ~(size_t)3;
     }
-    std::vector<float> dev(cpl_end, 0.0f);
+    const size_t zero_off = cpl_end;  // + 16 zero floats: what a convolution tap outside the map reads
+    std::vector<float> dev(cpl_end + 16, 0.0f);
     size_t off = 0;
     for (size_t li = 0; li < specs.size(); ++li) {
         const Spec& s = specs[li];
@@ -1652,6 +1654,7 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
     }
     const float* d = (const float*)v->dmem;
     v->stem_wpl = (const unsigned short*)(d + wpl_off);
+    v->zero16 = d + zero_off;
     off = 0;
     for (size_t li = 0; li < specs.size(); ++li) {
         const Spec& s = specs[li];
@@ -1710,17 +1713,17 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
     for (int k = 0; k < 4; ++k) {
         const int s = kVaeBlockStride[k], ho = v->bh[k], wo = v->bw[k];
         const VaeLayer& ca = v->conv[li++];
-        VaeConvArgs a1{X, ca.w, ca.wpl, ca.b, nullptr, T, B, h, w, ca.cin, ho, wo, ca.cout, 1};
+        VaeConvArgs a1{X, ca.w, ca.wpl, ca.b, v->zero16, nullptr, T, B, h, w, ca.cin, ho, wo, ca.cout, 1};
         HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a1, 3, s, st); }));
         const float* resid = X;
         if (s != 1) {
             const VaeLayer& cs = v->conv[li++];
-            VaeConvArgs a2{X, cs.w, cs.wpl, cs.b, nullptr, S, B, h, w, cs.cin, ho, wo, cs.cout, 0};
+            VaeConvArgs a2{X, cs.w, cs.wpl, cs.b, v->zero16, nullptr, S, B, h, w, cs.cin, ho, wo, cs.cout, 0};
             HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a2, 1, s, st); }));
             resid = S;
         }
         const VaeLayer& cb = v->conv[li++];
-        VaeConvArgs a3{T, cb.w, cb.wpl, cb.b, resid, Y, B, ho, wo, cb.cin, ho, wo, cb.cout, 1};
+        VaeConvArgs a3{T, cb.w, cb.wpl, cb.b, v->zero16, resid, Y, B, ho, wo, cb.cin, ho, wo, cb.cout, 1};
         HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a3, 3, 1, st); }));
         std::swap(X, Y);
         h = ho;

@@ -416,7 +416,7 @@ __device__ __forceinline__ float4 sel4(bool ok, float4 v) {
 }
 
 #ifndef VAE_LOAD_DEPTH
-#define VAE_LOAD_DEPTH 2
+#define VAE_LOAD_DEPTH 1
 #endif
 constexpr int CV_D = VAE_LOAD_DEPTH;  // K-tiles whose global loads are in flight in registers
 
@@ -464,42 +464,44 @@ __global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs
     };
     Stage ring[CV_D];
     int ky = 0, kx = 0, c0 = 0, kl = 0;  // the next K-tile to load: tap (ky, kx), channel block c0, index kl
-    // the rows' pixel pointers and validity for the current tap, recomputed only when the tap changes
-    // (every Cin / 16 K-tiles); a K-tile then adds the uniform channel-block offset c0 (H W)
+    // the rows' pixel pointers for the current tap, recomputed only when the tap changes (every Cin / 16
+    // K-tiles); a K-tile then adds c0 (H W) of the row's channel stride.  A pixel outside the map reads a
+    // zeroed 64-byte block with stride 0 (a.zero16): the loaded value is the operand, no select.
     const float *ap0 = pa0, *ap1 = pa1;
-    bool ok0 = false, ok1 = false;
+    unsigned st0 = 0, st1 = 0;
     auto tap = [&]() {
         const int iy0 = iyA + ky, ix0 = ixA + kx, iy1 = iyB + ky, ix1 = ixB + kx;
-        ok0 = v0 && (unsigned)iy0 < (unsigned)a.Hi && (unsigned)ix0 < (unsigned)a.Wi;
-        ok1 = v1 && (unsigned)iy1 < (unsigned)a.Hi && (unsigned)ix1 < (unsigned)a.Wi;
-        // outside the map: the image origin (a valid address), the value selected away
-        ap0 = pa0 + (ok0 ? ((size_t)iy0 * a.Wi + ix0) * 16 : 0);
-        ap1 = pa1 + (ok1 ? ((size_t)iy1 * a.Wi + ix1) * 16 : 0);
+        const bool ok0 = v0 && (unsigned)iy0 < (unsigned)a.Hi && (unsigned)ix0 < (unsigned)a.Wi;
+        const bool ok1 = v1 && (unsigned)iy1 < (unsigned)a.Hi && (unsigned)ix1 < (unsigned)a.Wi;
+        ap0 = ok0 ? pa0 + ((size_t)iy0 * a.Wi + ix0) * 16 : a.zero16 + 4 * kq;
+        ap1 = ok1 ? pa1 + ((size_t)iy1 * a.Wi + ix1) * 16 : a.zero16 + 4 * kq;
+        st0 = ok0 ? (unsigned)HWi : 0u;
+        st1 = ok1 ? (unsigned)HWi : 0u;
     };
     tap();
+    // Loads are unconditional and their values untouched until the stash (past the last K-tile they
+    // re-read valid addresses: the last weight tile; A's channel offset stays inside the map, Cin (H W)
+    // at most): a select or a branch next to a load makes the compiler wait for it at once (vmcnt),
+    // which serialised every K-tile on its A loads.
     auto load = [&](Stage& r) {
-        if (kl < KT) {
-            const float4 t0 = *(const float4*)(ap0 + (size_t)c0 * HWi);
-            const float4 t1 = *(const float4*)(ap1 + (size_t)c0 * HWi);
 #ifdef VAE_DIAG_NOALOAD  // diagnostic build: A from registers, not memory (results invalid)
-            (void)t0; (void)t1;
-            r.a0 = make_float4(1.f + c0, 2.f, 3.f, 4.f);
-            r.a1 = make_float4(5.f, 6.f + kx, 7.f, 8.f);
+        r.a0 = make_float4(1.f + c0, 2.f, 3.f, 4.f);
+        r.a1 = make_float4(5.f, 6.f + kx, 7.f, 8.f);
 #else
-            r.a0 = sel4(ok0, t0);
-            r.a1 = sel4(ok1, t1);
+        r.a0 = *(const float4*)(ap0 + (size_t)c0 * st0);
+        r.a1 = *(const float4*)(ap1 + (size_t)c0 * st1);
 #endif
+        const int klc = kl < KT ? kl : KT - 1;
 #pragma unroll
-            for (int p = 0; p < 3; ++p) r.b[p] = *(const uint4*)(pb + p * wps + (size_t)kl * CV_BK);
-            c0 += CV_BK;
-            if (c0 == Cin) {
-                c0 = 0;
-                if (++kx == KS) {
-                    kx = 0;
-                    ++ky;
-                }
-                tap();
+        for (int p = 0; p < 3; ++p) r.b[p] = *(const uint4*)(pb + p * wps + (size_t)klc * CV_BK);
+        c0 += CV_BK;
+        if (c0 == Cin) {
+            c0 = 0;
+            if (++kx == KS) {
+                kx = 0;
+                ++ky;
             }
+            tap();
         }
         ++kl;
     };
@@ -560,24 +562,33 @@ __global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs
     // K-tile kt: products from LDS buffer kt & 1; then tile kt + 1 (ring slot (kt + 1) % CV_D) is split
     // into the other buffer and its slot refilled with tile kt + 1 + CV_D.  Unrolled by CV_D so that the
     // ring slots are static registers.
-    for (int kt0 = 0; kt0 < KT; kt0 += CV_D) {
+#ifdef VAE_DIAG_NOSYNC  // diagnostic build: no barrier per K-tile (results invalid)
+#define CV_SYNC() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup")
+#else
+#define CV_SYNC() __syncthreads()
+#endif
+    // main trips: CV_D K-tiles each, every one followed by a stash and a load (no conditions)
+    int kt0 = 0;
+    for (; kt0 + CV_D < KT; kt0 += CV_D) {
 #pragma unroll
         for (int d = 0; d < CV_D; ++d) {
-            const int kt = kt0 + d;
-            if (kt < KT) {
-                products(kt & 1);
-                if (kt + 1 < KT) {
-                    stash((kt + 1) & 1, ring[(d + 1) % CV_D]);
-                    load(ring[(d + 1) % CV_D]);
-                }
-#ifdef VAE_DIAG_NOSYNC  // diagnostic build: no barrier per K-tile (results invalid)
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-#else
-                __syncthreads();
-#endif
-            }
+            products((kt0 + d) & 1);
+            stash((kt0 + d + 1) & 1, ring[(d + 1) % CV_D]);
+            load(ring[(d + 1) % CV_D]);
+            CV_SYNC();
         }
     }
+    // the last 1 .. CV_D K-tiles
+#pragma unroll
+    for (int d = 0; d < CV_D; ++d) {
+        const int kt = kt0 + d;
+        if (kt < KT) {
+            products(kt & 1);
+            if (kt + 1 < KT) stash((kt + 1) & 1, ring[(d + 1) % CV_D]);
+            CV_SYNC();
+        }
+    }
+#undef CV_SYNC
 
     // epilogue: lane (lr, lh), register r holds row 8(r/4) + 4 lh + r%4, column lr of each block
 #pragma unroll

@@ -65,6 +65,7 @@ struct VaeConvArgs {
     const float* w;      // [Cout][KS][KS][Cin]
     const unsigned short* wpl;  // the same weights split into bf16 planes [3 hi/mid/lo][Cout][KS KS Cin] (at load)
     const float* b;      // [Cout]
+    const float* zero16; // 16 zero floats (64 B, 16-byte aligned): what a tap outside the map reads
     const float* resid;  // [B][Cout/16][Ho][Wo][16] or nullptr
     float* out;          // [B][Cout/16][Ho][Wo][16]
     int B, Hi, Wi, Cin, Ho, Wo, Cout, relu;
