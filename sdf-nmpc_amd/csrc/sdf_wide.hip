@@ -30,10 +30,6 @@ typedef float wf32x16 __attribute__((ext_vector_type(16)));
 
 constexpr int WG_BM = 128, WG_BN = 128, WG_BK = 16, WG_LD = 20, WG_GROUP = 8;
 
-__device__ __forceinline__ float4 wsel4(bool ok, float4 v) {
-    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
-}
-
 #ifndef WIDE_WGS
 #define WIDE_WGS 4  // 119 VGPRs, 40 KB LDS: four 256-thread workgroups per CU (three: 2.88 vs 2.59 ms at C5)
 #endif
@@ -66,10 +62,10 @@ __global__ __launch_bounds__(256, WIDE_WGS) void wide_gemm_kernel(WideGemmArgs a
     do {                                                                                                \
         const bool seg2_ = (kt) >= KT1;                                                                 \
         const int ko_ = seg2_ ? ((kt) - KT1) * WG_BK : (kt) * WG_BK;                                    \
-        const float4 t0_ = *(const float4*)((seg2_ ? pc0 : pa0) + ko_);                                 \
-        const float4 t1_ = *(const float4*)((seg2_ ? pc1 : pa1) + ko_);                                 \
-        ra0 = wsel4(v0, t0_);                                                                           \
-        ra1 = wsel4(v1, t1_);                                                                           \
+        /* rows past M read row 0 (q0, q1) unselected: they only feed accumulator rows that are never   \
+           stored, and a select next to the load made the compiler wait for it at once */               \
+        ra0 = *(const float4*)((seg2_ ? pc0 : pa0) + ko_);                                              \
+        ra1 = *(const float4*)((seg2_ ? pc1 : pa1) + ko_);                                              \
         rb0 = *(const float4*)(pb0 + (size_t)(kt) * WG_BK);                                             \
         rb1 = *(const float4*)(pb1 + (size_t)(kt) * WG_BK);                                             \
     } while (0)
