@@ -791,9 +791,6 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     // gap = prod (1 - alpha): the stationarity residual of the starting point decays by exactly this
     // factor (every Newton system is solved for the new iterate), the stand-in for HPIPM's res_g test
     double mu = 0.0, cm = 0.0, rp = 0.0, gap = 1.0;
-    // the soft rows' affine dt (rows_pred, GPL > 0), kept in registers for the corrector's update: t and
-    // lambda do not change in between, so rows_update would recompute the same values
-    double aff_dt[3][4];
     // (GPL > 0: the soft rows' affine directions are computed once and kept in registers for both passes)
     auto rows_pred_t = [&](auto GPLc) -> double {
         constexpr int GPL = decltype(GPLc)::value;
@@ -830,10 +827,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
                 if (e < N1 * NS) {
                     soft_dir(e, sdt[gi], sdl[gi]);
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        bound(s.t[8 * N + 4 * e + q], s.lam[8 * N + 4 * e + q], sdt[gi][q], sdl[gi][q]);
-                        aff_dt[gi][q] = sdt[gi][q];
-                    }
+                    for (int q = 0; q < 4; ++q) bound(s.t[8 * N + 4 * e + q], s.lam[8 * N + 4 * e + q], sdt[gi][q], sdl[gi][q]);
                 }
             }
         } else {
@@ -920,27 +914,13 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
                 dl[q] = -sg * dt[q] - l - (dta * (-sg * dta - l) - sigmu) * it;
             }
         };
-        // the same with the affine dt of rows_pred (GPL > 0): one group evaluation instead of two
-        auto soft_dir_c = [&](int e, const double* dta, double* dt, double* dl) {
-            const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
-            const Grp gc = group(k, j, 1, sigmu);
-            double vc[4];
-            soft_vals(gc, k, j, s.cxc[e], vc);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const double t = s.t[r0 + q], l = s.lam[r0 + q];
-                dt[q] = vc[q] - t;
-                const double it = rcp_nr(t), sg = l * it;
-                dl[q] = -sg * dt[q] - l - (dta[q] * (-sg * dta[q] - l) - sigmu) * it;
-            }
-        };
         double sdt[GA][4], sdl[GA][4];
         if constexpr (GPL > 0) {
 #pragma unroll
             for (int gi = 0; gi < GPL; ++gi) {
                 const int e = lane + 64 * gi;
                 if (e < N1 * NS) {
-                    soft_dir_c(e, aff_dt[gi], sdt[gi], sdl[gi]);
+                    soft_dir(e, sdt[gi], sdl[gi]);
                     const int r0 = 8 * N + 4 * e;
 #pragma unroll
                     for (int q = 0; q < 4; ++q) bound(s.t[r0 + q], s.lam[r0 + q], sdt[gi][q], sdl[gi][q]);
