@@ -35,7 +35,7 @@ timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format cs
 fi
 if [ "$PART" = all ] || [ "$PART" = 3 ]; then
 # the stamps driver is rebuilt from the current rti_qp.hip, so the stamps always describe this tree's kernel
-(cd $R && timeout -k 10 300 hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -mllvm -amdgpu-mfma-vgpr-form -DQP_STAMPS -I sdf-nmpc_amd/csrc \
+(cd $R && timeout -k 10 300 hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -mllvm -amdgpu-mfma-vgpr-form -mllvm -amdgpu-sched-strategy=max-ilp -DQP_STAMPS -I sdf-nmpc_amd/csrc \
     tools/qp_stamps_drv.hip sdf-nmpc_amd/csrc/rti_qp.hip -o tools/_qp_stamps_drv)
 timeout -k 10 200 python3 $R/tools/qp_stamps.py > $O/qp_stamps.txt 2>&1
 # the segmented kernel: per-phase stamps (P = 4, B = 64 and 1024) and the serial / segmented sweep over B and N
