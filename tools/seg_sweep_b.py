@@ -5,6 +5,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT]
 from sdf_nmpc_amd import _lib, synth
 from sdf_nmpc_amd.config import Config
+if os.environ.get("SDFNMPC_LIB"):  # a diagnostic build (tools/build_variant.sh)
+    _lib.LIB_PATH = os.environ["SDFNMPC_LIB"]
 from sdf_nmpc_amd.model import Quad
 cfg = Config(); model = Quad(cfg)
 dev = torch.device("cuda:0")
