@@ -10,6 +10,8 @@ sys.path.insert(0, ROOT)
 import sdf_nmpc_amd  # noqa: E402,F401
 from sdf_nmpc_amd import _lib  # noqa: E402
 
+if os.environ.get("SDFNMPC_LIB"):  # a diagnostic build (tools/build_variant.sh)
+    _lib.LIB_PATH = os.environ["SDFNMPC_LIB"]
 ctx = _lib.Context(0)
 net = _lib.Net.siren(ctx, 0)
 rng = np.random.default_rng(0)
