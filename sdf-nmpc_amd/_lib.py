@@ -533,11 +533,25 @@ class FieldView:
     """A solver field's device memory (borrowed: owned by the Solver) -- data_ptr() / shape for the
     lower-level entry points that write it in place (sdfnmpc_pack_refs, sdfnmpc_vae_encode)."""
 
-    def __init__(self, ptr: int, shape, dtype):
-        self.ptr, self.shape, self.dtype = ptr, tuple(shape), np.dtype(dtype)
+    def __init__(self, ptr: int, shape, dtype, ctx: "Context" = None):
+        self.ptr, self.shape, self.dtype, self.ctx = ptr, tuple(shape), np.dtype(dtype), ctx
 
     def data_ptr(self) -> int:
         return self.ptr
+
+    @property
+    def device(self) -> int:
+        if self.ctx is None:
+            raise SdfnmpcError("FieldView without a context: its device is unknown")
+        return int(self.ctx.device)
+
+    def numpy(self) -> np.ndarray:
+        """Host copy (synchronous, ordered on the owning context's stream)."""
+        if self.ctx is None:
+            raise SdfnmpcError("FieldView without a context cannot be downloaded")
+        out = np.empty(self.shape, self.dtype)
+        _check(load().sdfnmpc_memcpy(self.ctx.h, out.ctypes.data, self.ptr, out.nbytes, 2))
+        return out
 
 
 class Solver:
@@ -570,7 +584,8 @@ class Solver:
     def field(self, name: str) -> FieldView:
         p, nodes, width = C.c_void_p(), C.c_int(), C.c_int()
         _check(load().sdfnmpc_solver_field(self.h, name.encode(), C.byref(p), C.byref(nodes), C.byref(width)))
-        return FieldView(p.value, (self.B, nodes.value, width.value), np.int32 if name in self.INT_FIELDS else np.float64)
+        return FieldView(p.value, (self.B, nodes.value, width.value), np.int32 if name in self.INT_FIELDS else np.float64,
+                         self.ctx)
 
     def upload(self, name: str, host, col0: int = 0, ncol=None, mask=None):
         """host: the full [B][nodes][width] mirror (or anything broadcastable to it); mask [B][nodes] of rows."""

@@ -268,6 +268,7 @@ class Nmpc:
             elif np.dtype(str(v.dtype).replace("torch.", "")) != np.float64:
                 raise TypeError(f"device input must be float64, got {v.dtype}")
         parts = self.ocp.parts
+        synced = set()
         for part in parts:
             lo, nb = part.lo, part.hi - part.lo
             args = {"p": part.solver.field("p")}
@@ -275,10 +276,10 @@ class Nmpc:
                 if k in host:
                     args[k] = _lib.DeviceArray.from_numpy(part.ctx, np.ascontiguousarray(host[k][lo:part.hi]))
                 elif len(parts) == 1:
-                    args[k] = _lib.sync_producer(v)
+                    args[k] = _producer_done(v, part.ctx, synced)
                 elif _device_of(v) == part.ctx.device:  # a view of the part's rows, in place
-                    args[k] = _lib.FieldView(_lib.sync_producer(v).data_ptr() + lo * cols[k] * 8, (nb, cols[k]),
-                                             np.float64)
+                    v = given[k] = _producer_done(v, part.ctx, synced)
+                    args[k] = _lib.FieldView(v.data_ptr() + lo * cols[k] * 8, (nb, cols[k]), np.float64, part.ctx)
                 else:  # another device: through the host, once per array
                     host[k] = _download(v, Bn, cols[k])
                     args[k] = _lib.DeviceArray.from_numpy(part.ctx, np.ascontiguousarray(host[k][lo:part.hi]))
@@ -306,13 +307,32 @@ class Nmpc:
             self._mark("WN", b)
 
 
+def _producer_done(a, ctx, synced: set):
+    """A device array about to be read in place by a kernel on ``ctx``'s stream, once everything that
+    produces it has finished: a torch tensor waits for torch's current stream (made contiguous first: the
+    in-place views assume row-major [B][cols]); an array owned by another context (a DeviceArray or solver
+    FieldView, e.g. VaeWrapper.latent64 written by the encoder's stream) waits for that context's stream.
+    Each array is synchronised once per call (``synced``)."""
+    from . import _lib
+    if type(a).__module__.split(".")[0] == "torch":
+        if not a.is_contiguous():
+            a = a.contiguous()
+        return _lib.sync_producer(a)
+    owner = getattr(a, "ctx", None)
+    if owner is not None and owner is not ctx and id(a) not in synced:
+        owner.synchronize()
+        synced.add(id(a))
+    return a
+
+
 def _device_of(a) -> int:
-    """HIP device of a device array: DeviceArray (its context's), torch tensor (its own), else 0."""
+    """HIP device of a device array: DeviceArray / FieldView (its context's), torch tensor (its own)."""
     ctx = getattr(a, "ctx", None)
     if ctx is not None:
         return int(ctx.device)
-    dev = getattr(a, "device", None)
-    return int(getattr(dev, "index", 0) or 0)
+    if type(a).__module__.split(".")[0] == "torch":
+        return int(a.device.index or 0)
+    raise TypeError(f"device of {type(a).__name__} unknown (expected a DeviceArray, FieldView or torch tensor)")
 
 
 def _download(a, rows, cols):

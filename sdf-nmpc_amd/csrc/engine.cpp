@@ -206,6 +206,7 @@ extern "C" int sdfnmpc_ctx_create(int device, void* stream, sdfnmpc_ctx** out) {
 // answering must not hang destroy / reconfigure while the shim's lock is held): on timeout the mailbox
 // and stream are abandoned -- never freed or reused, since the server may still write to them -- and
 // the host path falls back to one launch per call.  Returns false on timeout.
+static void mark_abandoned(uint64_t uid);
 static bool srv_stop(sdfnmpc_ctx* ctx) {
     auto& S = ctx->srv;
     if (!S.mb || S.abandoned) return !S.abandoned;
@@ -218,6 +219,7 @@ static bool srv_stop(sdfnmpc_ctx* ctx) {
             S.abandoned = true;
             S.live = false;
             S.mode = 0;
+            mark_abandoned(S.net);  // its network is leaked, not freed under a running reader
             fail(SDFNMPC_E_HIP, "sdf server: did not stop within 2 s; abandoned (one launch per call from now on)");
             return false;
         }
@@ -872,8 +874,21 @@ extern "C" int sdfnmpc_net_siren(sdfnmpc_ctx* ctx, uint64_t seed, float wg, floa
     return upload_net(ctx, std::move(h), out);
 }
 
+// networks an abandoned SDF server (srv_stop timeout) may still be reading: never freed
+static std::mutex g_abandoned_mu;
+static std::vector<uint64_t> g_abandoned_nets;
+static void mark_abandoned(uint64_t uid) {
+    std::lock_guard<std::mutex> lk(g_abandoned_mu);
+    g_abandoned_nets.push_back(uid);
+}
+
 extern "C" void sdfnmpc_net_free(sdfnmpc_net* net) {
     if (!net) return;
+    {
+        std::lock_guard<std::mutex> lk(g_abandoned_mu);
+        // hipFree would also synchronise the device, i.e. wait for the very server that refused to stop
+        if (std::find(g_abandoned_nets.begin(), g_abandoned_nets.end(), net->uid) != g_abandoned_nets.end()) return;
+    }
     ScopedDevice sd(net->device);
     if (net->dmem) (void)hipFree(net->dmem);
     delete net;
@@ -1042,6 +1057,7 @@ static bool srv_enabled(sdfnmpc_ctx* ctx) {
 // elsewhere in the process waits for it); a server that exits while a request is posted writes its epoch
 // to `gone`, and the caller relaunches at once (the new server serves every seq_in above the seq_out it
 // finds).
+constexpr int SRV_FALLBACK = 1;  // srv_call: the server was abandoned; the caller takes the per-call launch path
 static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const float* hp, const float* hl, bool grad,
                     float* ho) {
     using clk = std::chrono::steady_clock;
@@ -1062,7 +1078,7 @@ static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const fl
         S.seq = 0;
         S.live = false;
     }
-    if (S.live && S.net != net->uid && !srv_stop(ctx)) return SDFNMPC_E_HIP;
+    if (S.live && S.net != net->uid && !srv_stop(ctx)) return SRV_FALLBACK;  // abandoned: serve this call per launch
     if (S.live && __atomic_load_n(&S.mb->gone, __ATOMIC_ACQUIRE) == S.epoch) {
         // it left (idle, life or stop) after publishing its last answer: nothing of it runs any more but
         // its kernel's exit, which the stream orders before the relaunch
@@ -1186,10 +1202,13 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         for (int k = 0; k < L; ++k) hl[(size_t)r * L + k] = (float)in[(size_t)r * D + 3 + k];
     }
     const bool use_row = !net->wide && rows <= SDF_ROW_MAX;
+    bool served = false;
     if (use_row && srv_enabled(ctx)) {  // the resident server: no launch, no copies, no synchronisation
         const int rc = srv_call(ctx, net, rows, hp, hl, grad != nullptr, ho);
-        if (rc) return rc;
-    } else if (use_row) {  // the latency path: one launch, no hoist (sdf_row.hip).  Zero-copy (the kernel reading
+        if (rc != SDFNMPC_OK && rc != SRV_FALLBACK) return rc;
+        served = rc == SDFNMPC_OK;
+    }
+    if (!served && use_row) {  // the latency path: one launch, no hoist (sdf_row.hip).  Zero-copy (the kernel reading
         // and writing the pinned block over PCIe) was measured equal in wall time: the PCIe reads add
         // ~2 us to the kernel, as much as the two staging copies cost.
         HIPCHK(ctx->hin.ensure(nin * sizeof(float)));
@@ -1207,7 +1226,7 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         HIPCHK(hipMemcpyAsync(ho, dout, (grad ? nin : (size_t)rows * 4) * sizeof(float), hipMemcpyDeviceToHost,
                               ctx->stream));
         HIPCHK(host_wait(ctx));
-    } else {
+    } else if (!served) {
         HIPCHK(ctx->hin.ensure(nin * sizeof(float)));
         HIPCHK(ctx->hout.ensure(nin * sizeof(float)));
         float* dpos = (float*)ctx->hin.p;
@@ -1708,7 +1727,7 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
     VaePreArgs pa{img, o->dtype, B, o->in_h, o->in_w, v->H, v->W, o->clip, o->yz, P};
     HIPCHK(timed(ctx, "vae_pre", [&] { return launch_vae_pre(pa, st); }));
     VaeStemArgs sa{P, v->stem_wpl, v->stem.b, X, B, v->H, v->W, v->Hc, v->Wc, v->Hp, v->Wp};
-    HIPCHK(timed(ctx, "vae_stem", [&] { return launch_vae_stem(sa, st); }));
+    HIPCHK(timed(ctx, "vae_stem", [&] { return launch_vae_stem(sa, ctx->n_cu, st); }));
     int h = v->Hp, w = v->Wp, li = 0;
     for (int k = 0; k < 4; ++k) {
         const int s = kVaeBlockStride[k], ho = v->bh[k], wo = v->bw[k];

@@ -340,7 +340,7 @@ __global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a, int til
     }
 }
 
-hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s) {
+hipError_t launch_vae_stem(const VaeStemArgs& a, int n_cu, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     if (a.Hc != (a.H - 1) / 2 + 1 || a.Wc != (a.W - 1) / 2 + 1 || a.Hp != (a.Hc - 1) / 2 + 1 ||
         a.Wp != (a.Wc - 1) / 2 + 1)
@@ -350,15 +350,7 @@ hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s) {
     const int n_tiles = tiles_img * a.B;
     // persistent: two workgroups per CU (the 69 KB conv tile), each walking the tiles with a stride of
     // the grid, the next tile's patch loads in flight under the current tile's products
-    static int cu_of_dev[64];  // per device, read once (a racing first call writes the same value)
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return hipErrorInvalidDevice;
-    int n_cu = cu_of_dev[dev];
-    if (n_cu <= 0) {
-        if (hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n_cu <= 0)
-            return hipErrorInvalidDevice;
-        cu_of_dev[dev] = n_cu;
-    }
+    if (n_cu <= 0) return hipErrorInvalidDevice;
     const int grid = n_tiles < 2 * n_cu ? n_tiles : 2 * n_cu;
     hipLaunchKernelGGL(vae_stem_kernel, dim3(grid), dim3(256), 0, s, a, tiles_x, tiles_img, n_tiles);
     return hipGetLastError();

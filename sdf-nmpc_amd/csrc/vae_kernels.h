@@ -83,7 +83,7 @@ struct VaeHeadArgs {
 };
 
 hipError_t launch_vae_pre(const VaePreArgs& a, hipStream_t s);
-hipError_t launch_vae_stem(const VaeStemArgs& a, hipStream_t s);
+hipError_t launch_vae_stem(const VaeStemArgs& a, int n_cu, hipStream_t s);  // n_cu: the device's CUs (sdfnmpc_ctx::n_cu)
 hipError_t launch_vae_conv(const VaeConvArgs& a, int ks, int stride, hipStream_t s);
 hipError_t launch_vae_head(const VaeHeadArgs& a, hipStream_t s);
 

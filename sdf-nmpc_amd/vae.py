@@ -324,8 +324,7 @@ class VaeWrapper:
 
     def encode_to(self, nmpc, W_p_Bo, W_R_Bo, flag=None):
         """encode + ``nmpc.set_latent_device`` with the fp64 latents (no host round trip).  The encoder and
-        the controller may use different streams: the encoder's is drained first."""
+        the controller's parts may use other streams: set_latent_device drains the encoder's stream before
+        any part on another context reads latent64 in place (controller._producer_done)."""
         self._run()
-        if nmpc.ocp.ctx is not self.ctx:
-            self.ctx.synchronize()
         nmpc.set_latent_device(self.latent64, W_p_Bo, W_R_Bo, flag)

@@ -223,3 +223,61 @@ def test_c4_full_batch_through_the_occupancy_gate():
         alone = _c4_run(cfg, x0[sl], lat[sl], r, [0], kernel="serial")
         np.testing.assert_array_equal(alone["u0"], full["u0"][sl])
         np.testing.assert_array_equal(alone["iters"], full["iters"][sl])
+
+
+def test_set_latent_device_multi_part_inputs_from_another_stream():
+    """with the batch split into parts, every part after the first reads a device latent in place
+    (a view at its first row).  Here latent, W_p_Bo and W_R_Bo are all device arrays of a third context whose
+    values are still being written by a kernel on that context's stream (rti_apply: x += dx) when
+    set_latent_device is called, and no flag is passed (no host temporary whose free would drain the device).
+    The packed parameters and the RTI step must equal those of the host-array path bit for bit."""
+    from sdf_nmpc_amd import _lib
+    from sdf_nmpc_amd.config import Config
+    from sdf_nmpc_amd.controller import Nmpc
+    from sdf_nmpc_amd.model import Quad
+    from sdf_nmpc_amd.ocp import Ocp
+    from sdf_nmpc_amd.reference import Ref, yaw2quat
+    Bt, cfg = 600, Config(mpc__N=60)
+    rng = np.random.default_rng(9)
+    x0 = np.zeros((Bt, 10))
+    x0[:, :3] = rng.uniform(-1, 1, (Bt, 3))
+    x0[:, 3:7] = np.stack([yaw2quat(y) for y in rng.uniform(-np.pi, np.pi, Bt)])
+    lat = rng.normal(size=(Bt, 128))
+    R = np.stack([np.eye(3)] * Bt)
+    r = Ref(cfg)
+    r.p, r.q = np.array([1.0, 2.0, 1.5]), yaw2quat(0.3)
+    r.use_weights(r.W_on)
+    prod = _lib.Context(0)  # the producer: its own stream
+
+    def produced(a, nb, n1):  # device array whose final values an async kernel on prod's stream writes
+        a = np.ascontiguousarray(a, dtype=np.float64).reshape(nb, n1, 10)
+        out = _lib.DeviceArray.from_numpy(prod, np.zeros_like(a))
+        d = _lib.DeviceArray.from_numpy(prod, a)
+        uu = _lib.DeviceArray.from_numpy(prod, np.zeros((nb, n1 - 1, 4)))
+        du = _lib.DeviceArray.from_numpy(prod, np.zeros((nb, n1 - 1, 4)))
+        _lib.rti_apply(prod, nb, n1 - 1, out, uu, d, du)  # asynchronous: out = 0 + a
+        out.keep = (d, uu, du)
+        out.shape = (Bt, a.size // Bt)
+        return out
+
+    res = []
+    for dev_inputs in (False, True):
+        o = Ocp(Quad(cfg), batch=Bt, devices=[0, 0])
+        assert len(o.parts) == 2
+        n = Nmpc(cfg, batch=Bt, ocp=o)
+        n.set_sdf_flag(1.0)
+        for k in range(61):
+            n.set_ref(r, k)
+        n.set_x0(x0)
+        n._flush()
+        if dev_inputs:
+            n.set_latent_device(produced(lat, 120, 64), produced(x0[:, :3], 1, 180), produced(R.reshape(Bt, 9), 1, 540))
+        else:
+            n.set_latent_device(lat, x0[:, :3], R)
+        p = o.download("p")
+        assert n.solve() == 0
+        res.append((p, n.get_u()))
+        o.close()
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    prod.close()
