@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SDFNMPC_ABI_VERSION 4
+#define SDFNMPC_ABI_VERSION 5
 
 enum {
     SDFNMPC_OK = 0,
@@ -62,13 +62,26 @@ enum {
 typedef struct sdfnmpc_ctx sdfnmpc_ctx;
 typedef struct sdfnmpc_net sdfnmpc_net;
 
-/* 'att' model constants (model/quad_rollpitchyawrate.py; config robot.limits / sensor / mpc) */
+#define SDFNMPC_POLY_DEG_MAX 6 /* braking-distance polynomial: degree bound ... */
+#define SDFNMPC_POLY_MAX 84    /* ... and its coefficient count (deg + 3 choose 3) */
+#define SDFNMPC_NHN_MAX 8      /* terminal constraint rows (soft <= 3, hard <= 6) */
+#define SDFNMPC_NHE 6          /* terminal extra functions hE (sdfnmpc_lin_args) */
+
+/* 'att' model constants (model/quad_rollpitchyawrate.py; config robot.limits / sensor / mpc) and the
+ * terminal ingredients of flags.recursive_feasibility / flags.stability (gen_model.py:72-149) */
 typedef struct {
     double gamma, roll, pitch, wz; /* robot.limits.{gamma, roll, pitch, wz}: u -> physical inputs */
     double g;                      /* gravity, 9.81 (model/base_model.py:10) */
     double B_p_C[3];               /* sensor.B_p_C (utils/config.py:43) */
     double B_R_C[9];               /* sensor.B_R_C, row-major (utils/config.py:44) */
     double fov_const_offset;       /* mpc.fov_const_offset (cost_const_helpers.py:65) */
+    int rec_feas;                  /* 1: the preparation phase evaluates the terminal extras hE[0..2] (below) */
+    int stability;                 /* 1: hE[3..5] = v_N, and the terminal residual y_N is scaled by the flag and
+                                      gains the row flag |v|^2 (quad_rollpitchyawrate.py:52-55, gen_model.py:
+                                      142-149): nyN = 5 */
+    int poly_deg;                  /* braking-distance polynomial degree (mpc.braking_dist.degree, <= 6) */
+    double poly[SDFNMPC_POLY_MAX]; /* its coefficients in polynomial_3variate's term order (utils/math.py:
+                                      307-314: total degree 0..deg, then x exponent a, then y exponent b) */
 } sdfnmpc_quad_model;
 
 /* Batched preparation phase: B instances x (N+1) shooting nodes, fp64, row-major C arrays.
@@ -88,9 +101,21 @@ typedef struct {
     double* Jy;       /* [B][N][14][11]  column-major */
     double* yN;       /* [B][4]          terminal residual */
     double* JyN;      /* [B][10][4]      column-major */
-    double* h;        /* [B][N+1][3]     [hfov, vfov, sdf] */
+    double* h;        /* [B][N+1][3]     the three node functions [hfov, vfov, sdf] in fixed columns: which
+                                            of them are rows of the OCP is the QP's constraint set
+                                            (sdfnmpc_qp_opts.nh / h_col) */
     double* Jh;       /* [B][N+1][10][3] column-major, d h / d x (d h / d u == 0) */
     float* sdf;       /* [B][N+1][4]     optional: (df, d df / d Co_p_B); NULL = internal buffer */
+    int nyN;          /* terminal residual rows: 4, or 5 with sdfnmpc_quad_model.stability (yN [B][nyN],
+                         JyN [B][10][nyN]) */
+    int no_sdf;       /* 1: no constraint or cost uses the network (enable_sdf False, or neither sdf_constraint,
+                         sdf_cost nor rec_feas): the SDF kernels are skipped, h[.][2] is not written and
+                         net may be NULL */
+    double* hE;       /* [B][6]          terminal extras (NULL unless rec_feas / stability): [-flag poly(v),
+                         flag atan2(E_y, E_x), flag atan2(E_z, |E_xy|), v_x, v_y, v_z] with E = Co_p_E, the
+                         camera-frame point at the braking distance ahead (gen_model.py:98-112); the
+                         rec_feas constraint value is h[N][2] + hE[0] (gen_model.py:94-95) */
+    double* JhE;      /* [B][10][6]      column-major d hE / d x_N */
 } sdfnmpc_lin_args;
 
 /* QP model data and solver options (defaults in sdf-nmpc_amd/model.py / ocp.py) */
@@ -112,23 +137,37 @@ typedef struct {
                               from the du found in sdfnmpc_qp_args.du on entry (the previous QP's solution --
                               the solver object keeps it between steps; zero after init), dx rolled out from
                               x0 under it, t / lambda by the cold start's rule; 0 = du = 0 (cold) */
+    /* The constraint set (gen_model.py:26-149 under flags.enable_sdf / sdf_constraint / vfov_constraint /
+     * recursive_feasibility / stability and sensor.hfov < 3.14; sdf-nmpc_amd/model.py builds it).
+     * Stage rows k < N: nh soft rows in the reference's order, row j = column h_col[j] of h / J_h, with
+     * bounds / slack weights lh[j], uh[j], zl[j], Zl[j] above.  Terminal rows: nhN rows, the first nsN soft
+     * (lhN / uhN, slack weights zlN / ZlN, not cost-scaled), the rest hard; row j's value is
+     * h[N][hN_col[j]] (if >= 0) + hE[hE_col[j]] (if >= 0), its Jacobian the same sum of columns. */
+    int nh;                /* 0..3 (3: [hfov, vfov, sdf], the default flags) */
+    int h_col[3];          /* increasing */
+    int nhN, nsN;          /* nhN <= SDFNMPC_NHN_MAX, nsN <= min(nhN, 3), nhN - nsN <= 6 */
+    int hN_col[SDFNMPC_NHN_MAX], hE_col[SDFNMPC_NHN_MAX];
+    double lhN[SDFNMPC_NHN_MAX], uhN[SDFNMPC_NHN_MAX], zlN[3], ZlN[3];
+    int nyN;               /* terminal residual rows (yNref / WN [B][nyN]): 4, or 5 with flags.stability */
 } sdfnmpc_qp_opts;
 
 /* Batched QP of the RTI feedback phase, built from sdfnmpc_linearize outputs. */
 typedef struct {
     int B, N;
     const double *xn, *AB, *y, *Jy, *yN, *JyN, *h, *Jh; /* sdfnmpc_lin_args outputs */
+    const double *hE, *JhE; /* sdfnmpc_lin_args outputs (NULL when no terminal row reads them) */
     const double* x;     /* [B][N+1][10] iterate the QP was built at */
     const double* u;     /* [B][N][4] */
     const double* x0;    /* [B][10] measured state (Ocp.solve x0) */
     const double* yref;  /* [B][N][ny] stage references (Ocp.solve y[k]) */
     const double* W;     /* [B][N][ny] diagonal weights (Ocp.solve W[k], set as np.diag) */
-    const double* yNref; /* [B][4] */
-    const double* WN;    /* [B][4] */
+    const double* yNref; /* [B][nyN] */
+    const double* WN;    /* [B][nyN] */
     const double* dt;    /* [N] */
     double* dx;          /* [B][N+1][10] solution: the RTI step */
     double* du;          /* [B][N][4] */
-    double* slack;       /* [B][N+1][3][2] optional: (sl, su) of the soft rows */
+    double* slack;       /* [B][N+1][3][2] optional: (sl, su) of the soft rows (row j of node k < N; terminal
+                            soft row j at node N; unused entries 0) */
     int* status;         /* [B] optional: 0 converged, 1 max_iter reached (acados status 2: the step is
                             kept), 2 numerical failure -- a NaN / Inf in the data (acados QP failure,
                             status 4: sdfnmpc_rti_apply given this array keeps the instance's iterate) */
@@ -169,8 +208,10 @@ typedef struct {
     double* p;             /* [B][N+1][np] OCP parameters */
     double* yref;          /* [B][N][ny] */
     double* W;             /* [B][N][ny] */
-    double* yNref;         /* [B][4] */
-    double* WN;            /* [B][4] */
+    double* yNref;         /* [B][nyN] */
+    double* WN;            /* [B][nyN] */
+    int nyN;               /* terminal residual rows: 4, or 5 with flags.stability (y[:nyN] / W[:nyN] of the
+                              last node, controller.py:141-142; 0 is taken as 4) */
 } sdfnmpc_ref_args;
 
 int sdfnmpc_abi_version(void);
@@ -210,6 +251,8 @@ long long sdfnmpc_qp_lds_bytes(int N);
  * registers allow four instances per CU); 0 when N does not fit one CU, -1 on bad arguments.  Replaces the reference's single acados solver per process
  * (controller.py:16 builds one Ocp): a batch larger than this is split over devices (shard.plan). */
 long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N);
+/* the same for the constraint set of opts (its rows change the LDS per instance; NULL: the default set) */
+long long sdfnmpc_qp_capacity_for(const sdfnmpc_ctx* ctx, int N, const sdfnmpc_qp_opts* opts);
 /* rows per SDF workgroup: 32 (2 workgroups / CU) or 64 (1 workgroup / CU); default 32 */
 int sdfnmpc_ctx_set_tile_rows(sdfnmpc_ctx* ctx, int rows);
 /* per-kernel HIP-event timing on the context stream (off by default) */
@@ -312,10 +355,11 @@ int sdfnmpc_memcpy(sdfnmpc_ctx* ctx, void* dst, const void* src, size_t bytes, i
 
 /* ---- the batched SQP-RTI solver object (owns its device workspace) ----
  * Fields (name: [B][nodes][width] fp64 unless noted): x [N+1][10], u [N][4], p [N+1][np], x0 [1][10],
- * yref / W [N][ny], yNref / WN [1][4], u0 [1][4], dx [N+1][10], du [N][4], the sdfnmpc_lin_args outputs
- * xn, AB, y, Jy, yN, JyN, h, Jh, res [1][2], slack [N+1][6] ((sl, su) per soft row), status / iters
- * [1][1] int32.  A field's device pointer may
- * be handed to the lower-level entry points (e.g. sdfnmpc_pack_refs or sdfnmpc_vae_encode writing p). */
+ * yref / W [N][ny], yNref / WN [1][nyN], u0 [1][4], dx [N+1][10], du [N][4], the sdfnmpc_lin_args outputs
+ * xn, AB, y, Jy, yN [1][nyN], JyN [1][10 nyN], h, Jh, hE [1][6], JhE [1][60], res [1][2], slack [N+1][6]
+ * ((sl, su) per soft row), status / iters [1][1] int32.  A field's device pointer may be handed to the
+ * lower-level entry points (e.g. sdfnmpc_pack_refs or sdfnmpc_vae_encode writing p).  The network may be
+ * NULL when the constraint set (qp.nh / h_col, qp.hN_col) and the cost (ny == 11) never read the SDF. */
 typedef struct sdfnmpc_solver sdfnmpc_solver;
 
 typedef struct {

@@ -15,6 +15,7 @@
  *                        forward sensitivities) == exact derivative of the RK4 map
  *   NLS residual ....... quad_rollpitchyawrate.py:48-55, utils/math.py:169-174
  *   constraints h ...... cost_const_helpers.py:48-75 (add_fov_const_trigo) + gen_model.py:46-70
+ *   terminal extras .... gen_model.py:72-149 (rec_feas braking row, fov at Co_p_E, stability), utils/math.py:294-321
  *   shooting grid ...... ocp.py:18-27 (numpy linspace / hstack / diff semantics)
  */
 #include <math.h>
@@ -275,6 +276,63 @@ void orc_quad_constr(const orc_quad* m, const double* x, const double* p, double
         for (int j = 0; j < 10; ++j) { Jh[j * 3 + 0] = hf.d[j]; Jh[j * 3 + 1] = vf.d[j]; Jh[j * 3 + 2] = 0.0; }
         for (int j = 0; j < 3; ++j)  /* d s / d W_p_B = flag * gdf * W_R_Co^T */
             Jh[j * 3 + 2] = flag * (gdf[0] * R[j * 3 + 0] + gdf[1] * R[j * 3 + 1] + gdf[2] * R[j * 3 + 2]);
+    }
+}
+
+/* Terminal extras of flags.recursive_feasibility / stability at node N (gen_model.py:72-149,
+ * quad_rollpitchyawrate.py:52-55, utils/math.py:294-321):
+ *   hE = [-flag poly(v), flag atan2(E_y, E_x), flag atan2(E_z, |E_xy|), v_x, v_y, v_z] with
+ *   E = Co_p_E = W_R_Co^T (p + poly(v) v / sqrt(|v|^2 + 1e-4) - W_p_Co) + B_R_C^T B_p_C + [fov_offset, 0, 0]
+ *   (braking_dist_flag with the flag forced to 1 inside Co_p_E, gen_model.py:86-87,110-112);
+ *   poly in polynomial_3variate's term order (total degree d, then x exponent a, then y exponent b).
+ * hE [6], JhE col-major [10][6].  With stability, yN5 = flag [p, q_e[3], |v|^2] and JyN5 [10][5]. */
+void orc_quad_term(const orc_quad* m, const double* x, const double* p, int deg, const double* poly, int rec_feas,
+                   int stability, double* hE, double* JhE, double* yN5, double* JyN5) {
+    dn X[10];
+    seed_xu(x, NULL, X, NULL);
+    const double flag = p[0];
+    dn H[6] = {dc(0.0), dc(0.0), dc(0.0), X[7], X[8], X[9]};
+    dn vv = dadd(dadd(dmul(X[7], X[7]), dmul(X[8], X[8])), dmul(X[9], X[9]));
+    if (rec_feas) {
+        dn pw[3][16];
+        for (int i = 0; i < 3; ++i) {
+            pw[i][0] = dc(1.0);
+            for (int a = 1; a <= deg; ++a) pw[i][a] = dmul(pw[i][a - 1], X[7 + i]);
+        }
+        dn pv = dc(0.0);
+        int q = 0;
+        for (int d = 0; d <= deg; ++d)
+            for (int a = 0; a <= d; ++a)
+                for (int b = 0; b <= d - a; ++b, ++q)
+                    pv = dadd(pv, dscl(dmul(dmul(pw[0][a], pw[1][b]), pw[2][d - a - b]), poly[q]));
+        H[0] = dscl(pv, -flag);
+        dn sc = ddiv(pv, dsqrt(dadd(vv, dc(1e-4))));
+        const double* R = p + 4;
+        dn e[3];
+        for (int i = 0; i < 3; ++i) e[i] = dsub(dadd(X[i], dmul(X[7 + i], sc)), dc(p[1 + i]));
+        double off[3];
+        for (int i = 0; i < 3; ++i)
+            off[i] = m->B_R_C[0 * 3 + i] * m->B_p_C[0] + m->B_R_C[1 * 3 + i] * m->B_p_C[1] + m->B_R_C[2 * 3 + i] * m->B_p_C[2];
+        dn E[3];
+        for (int i = 0; i < 3; ++i)
+            E[i] = dadd(dadd(dadd(dscl(e[0], R[0 * 3 + i]), dscl(e[1], R[1 * 3 + i])), dscl(e[2], R[2 * 3 + i])),
+                        dc(off[i] + (i == 0 ? m->fov_offset : 0.0)));
+        H[1] = dscl(datan2(E[1], E[0]), flag);
+        H[2] = dscl(datan2(E[2], dsqrt(dadd(dmul(E[0], E[0]), dmul(E[1], E[1])))), flag);
+    }
+    for (int i = 0; i < 6; ++i) {
+        if (hE) hE[i] = H[i].v;
+        if (JhE) for (int j = 0; j < 10; ++j) JhE[j * 6 + i] = H[i].d[j];
+    }
+    if (stability && (yN5 || JyN5)) {
+        double u0[4] = {0, 0, 0, 0}, yN[4], JyN[40];
+        orc_quad_cost(m, x, u0, p, NULL, NULL, yN, JyN);
+        for (int i = 0; i < 4; ++i) {
+            if (yN5) yN5[i] = flag * yN[i];
+            if (JyN5) for (int j = 0; j < 10; ++j) JyN5[j * 5 + i] = flag * JyN[j * 4 + i];
+        }
+        if (yN5) yN5[4] = flag * vv.v;
+        if (JyN5) for (int j = 0; j < 10; ++j) JyN5[j * 5 + 4] = flag * vv.d[j];
     }
 }
 

@@ -50,11 +50,12 @@ def lib():
         _lib.orc_quad_cost.argtypes = [P(Quad), P(d), P(d), P(d), P(d), P(d), P(d), P(d)]
         _lib.orc_quad_constr.argtypes = [P(Quad), P(d), P(d), d, P(d), P(d), P(d), P(d)]
         _lib.orc_shooting_grid.argtypes = [C.c_int, d, C.c_int, C.c_int, d, P(d), P(d)]
+        _lib.orc_quad_term.argtypes = [P(Quad), P(d), P(d), C.c_int, P(d), C.c_int, C.c_int, P(d), P(d), P(d), P(d)]
         _lib.orc_linearize_batch.argtypes = [P(Quad), P(Spec), P(f), P(f), P(f), C.c_int, C.c_int, C.c_int,
                                              P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d), P(d),
                                              P(d), P(d), P(f), C.c_int]
         _lib.orc_max_threads.restype = C.c_int
-        _lib.orc_qp_ipm_batch.argtypes = [C.c_int, C.c_int] + [P(d)] * 17 + [C.c_int, C.c_int, C.c_int, P(d), P(d),
+        _lib.orc_qp_ipm_batch.argtypes = [C.c_int, C.c_int] + [P(d)] * 19 + [C.c_int, C.c_int, C.c_int, P(d), P(d),
                                                                              P(d), P(C.c_int), P(C.c_int), P(d),
                                                                              C.c_int]
         _lib.orc_vae_preprocess.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_float,
@@ -137,6 +138,18 @@ def constr(m, x, p, df, gdf):
     return h, Jh.T.copy(), cpb
 
 
+def term_extras(m, x, p, model):
+    """Terminal extras of a model.Quad with recursive_feasibility / stability at one node (orc_quad_term):
+    hE [6], JhE [6][10] (row-major), and with stability yN [5], JyN [5][10]."""
+    x = np.ascontiguousarray(x, np.float64); p = np.ascontiguousarray(p, np.float64)
+    poly = np.ascontiguousarray(np.concatenate([model.poly, [0.0]]), np.float64)
+    hE = np.empty(6); JhE = np.empty((10, 6)); yN = np.empty(5); JyN = np.empty((10, 5))
+    lib().orc_quad_term(C.byref(m), _p(x, C.c_double), _p(p, C.c_double), int(model.poly_deg), _p(poly, C.c_double),
+                        int(model.rec_feas), int(model.stability), _p(hE, C.c_double), _p(JhE, C.c_double),
+                        _p(yN, C.c_double), _p(JyN, C.c_double))
+    return hE, JhE.T.copy(), yN, JyN.T.copy()
+
+
 def shooting_grid(N, T, uniform=True, n_short=2, dt_short=0.01):
     nodes = np.empty(N + 1); dt = np.empty(N)
     rc = lib().orc_shooting_grid(N, T, int(uniform), n_short, dt_short, _p(nodes, C.c_double), _p(dt, C.c_double))
@@ -151,8 +164,25 @@ def prng_uniform(seed, stream, n):
     return out
 
 
-def linearize_batch(m, net, x, u, p, dt, nthreads=1):
-    """Whole preparation phase on the CPU; layouts match include/sdfnmpc.h outputs."""
+def linearize_batch(m, net, x, u, p, dt, nthreads=1, model=None):
+    """Whole preparation phase on the CPU; layouts match include/sdfnmpc.h outputs.  model (model.Quad)
+    with recursive_feasibility / stability adds hE [B][6], JhE [B][10][6] and the nyN = 5 terminal
+    residual (yN [B][5], JyN [B][10][5])."""
+    out = _linearize_batch(m, net, x, u, p, dt, nthreads)
+    if model is not None and (model.rec_feas or model.stability):
+        B, N = out["xn"].shape[:2]
+        out["hE"], out["JhE"] = np.zeros((B, 6)), np.zeros((B, 10, 6))
+        yN5, JyN5 = np.zeros((B, 5)), np.zeros((B, 10, 5))
+        for b in range(B):
+            hE, JhE, y5, J5 = term_extras(m, x[b, N], p[b, N], model)
+            out["hE"][b], out["JhE"][b] = hE, JhE.T
+            yN5[b], JyN5[b] = y5, J5.T
+        if model.stability:
+            out["yN"], out["JyN"] = yN5, JyN5
+    return out
+
+
+def _linearize_batch(m, net, x, u, p, dt, nthreads=1):
     B, N1, _ = x.shape
     N = N1 - 1
     x = np.ascontiguousarray(x, np.float64); u = np.ascontiguousarray(u, np.float64)
@@ -167,7 +197,7 @@ def linearize_batch(m, net, x, u, p, dt, nthreads=1):
     return out
 
 
-QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", "W", "yNref", "WN")
+QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "hE", "JhE", "x", "u", "x0", "yref", "W", "yNref", "WN")
 
 
 # IPM starting point / step fraction of csrc/rti_qp.hip (QP_T0, QP_L0, QP_LC, QP_TAU_LO, QP_TAU_HI)
@@ -184,11 +214,22 @@ def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_sca
     """
     B, N = lin["xn"].shape[0], lin["xn"].shape[1]
     arrs = dict(lin)
+    arrs.setdefault("hE", np.zeros((B, 6)))
+    arrs.setdefault("JhE", np.zeros((B, 10, 6)))
     arrs.update(x=prob["x"], u=prob["u"], x0=x0, yref=prob["yref"], W=prob["W"], yNref=prob["yN"], WN=prob["WN"])
     arrs = {k: np.ascontiguousarray(arrs[k], dtype=np.float64) for k in QP_IN}
     dt = np.ascontiguousarray(prob["dt"], dtype=np.float64)
-    opts = np.concatenate([model.lbu, model.ubu, model.lh, model.uh, model.zl, model.Zl, [lm, tol, float(bool(lm_scaling))],
-                           [v for v in {**QP_START, **(start or {}), "ws": float(du_ws is not None)}.values()]]).astype(np.float64)
+    pad = lambda a, n, v=0.0: list(np.asarray(a, float)) + [v] * (n - len(a))
+    h_cols = list(getattr(model, "h_cols", [0, 1, 2]))
+    rows = getattr(model, "term_rows", [(c, -1, True, model.lh[i], model.uh[i], model.zl[i], model.Zl[i])
+                                        for i, c in enumerate(h_cols)])
+    cset = ([len(h_cols)] + pad(h_cols, 3) + [len(rows), sum(1 for r in rows if r[2])] + pad([r[0] for r in rows], 8, -1)
+            + pad([r[1] for r in rows], 8, -1) + pad([r[3] for r in rows], 8) + pad([r[4] for r in rows], 8)
+            + pad([r[5] for r in rows if r[2]], 3) + pad([r[6] for r in rows if r[2]], 3) + [arrs["WN"].shape[-1]])
+    opts = np.concatenate([model.lbu, model.ubu, pad(model.lh, 3), pad(model.uh, 3), pad(model.zl, 3), pad(model.Zl, 3),
+                           [lm, tol, float(bool(lm_scaling))],
+                           [v for v in {**QP_START, **(start or {}), "ws": float(du_ws is not None)}.values()],
+                           cset]).astype(np.float64)
     du0 = np.zeros((B, N, 4)) if du_ws is None else np.array(du_ws, dtype=np.float64).reshape(B, N, 4)
     out = dict(dx=np.zeros((B, N + 1, 10)), du=du0, slack=np.zeros((B, N + 1, 3, 2)),
                iters=np.zeros(B, np.int32), status=np.zeros(B, np.int32), res=np.zeros((B, 4)))

@@ -24,7 +24,7 @@
 #include <stdlib.h>
 #include <string.h>
 
-enum { NX = 10, NU = 4, NS = 3, NW = 14 };
+enum { NX = 10, NU = 4, NS = 3, NW = 14, NR = 8 /* rows per node at most (terminal: SDFNMPC_NHN_MAX) */ };
 
 typedef struct {
     double lbu[4], ubu[4], lh[3], uh[3], zl[3], Zl[3], lm, tol;
@@ -39,12 +39,19 @@ typedef struct {
      * du buffer on entry (the previous QP's solution) instead of 0; dx is the dynamics rollout from x0 under
      * that du, t / lambda follow the cold start's rule on the rows there */
     int ws;
+    /* the constraint set (include/sdfnmpc.h sdfnmpc_qp_opts): stage rows j < nh = column h_col[j] of h / J_h
+     * (bounds lh .. Zl above); terminal rows j < nhN (the first nsN soft) = h[N][hN_col[j]] + hE[hE_col[j]] */
+    int nh, h_col[3], nhN, nsN, hN_col[NR], hE_col[NR], nyN;
+    double lhN[NR], uhN[NR], zlN[3], ZlN[3];
 } qp_opts_c;
 
 typedef struct {                  /* stage k < N, or the terminal node k = N (x part only) */
     double A[NX][NX], Bm[NX][NU], c[NX];
     double H[NW][NW], g[NW];
-    double C[NS][NX], hl[NS], hu[NS];   /* soft rows: C dx + sl + hl >= 0, -C dx + su + hu >= 0 */
+    /* constraint rows j < nrow, the first nsoft soft: C dx + sl + hl >= 0, -C dx + su + hu >= 0 (slacks with
+     * L1 / L2 weights zl / Zl); the rest hard (terminal only): C dx + hl >= 0, -C dx + hu >= 0 */
+    double C[NR][NX], hl[NR], hu[NR], zl[NR], Zl[NR];
+    int nsoft, nrow;
     double dlo[NU], dup[NU];            /* box rows: du + dlo >= 0, -du + dup >= 0 */
     double s;                           /* cost scaling s_k */
 } stage_t;
@@ -79,10 +86,11 @@ static void chol_solve(int n, const double* L, double* x) {
     }
 }
 
-/* Rows (m = 8 N + 12 (N+1)), the order of rti_qp.hip: box rows 8 k + 4 up + i; soft rows
- * 8 N + 12 k + 4 j + q with q = 0 (h lower), 1 (h upper), 2 (sl >= 0), 3 (su >= 0). */
+/* Rows, the order of rti_qp.hip: box rows 8 k + 4 up + i; soft group e (stage groups k ns + j, then the
+ * terminal's soft rows) at 8 N + 4 e + q with q = 0 (h lower), 1 (h upper), 2 (sl >= 0), 3 (su >= 0); the
+ * hard terminal rows i at RH0 + 2 i (lower), + 1 (upper), RH0 = 8 N + 4 (N ns + nsN). */
 typedef struct {
-    int N, m;
+    int N, m, ns, rh0;            /* ns: soft rows of a stage k < N */
     const qp_opts_c* o;
     stage_t* st;
     double x0[NX];                /* dx_0 */
@@ -93,6 +101,8 @@ typedef struct {
     int gcount;                   /* Gondzio correctors kept (diagnostic) */
 } ipm_t;
 
+static int grp(const ipm_t* Q, int k, int j) { return (k < Q->N ? k * Q->ns : Q->N * Q->ns) + j; }
+
 static void rows_at(const ipm_t* Q, const double* dx, const double* du, const double* sl, const double* su, double* v) {
     const int N = Q->N;
     for (int k = 0; k < N; ++k)
@@ -101,14 +111,20 @@ static void rows_at(const ipm_t* Q, const double* dx, const double* du, const do
             v[8 * k + 4 + i] = -du[k * NU + i] + Q->st[k].dup[i];
         }
     for (int k = 0; k <= N; ++k)
-        for (int j = 0; j < NS; ++j) {
+        for (int j = 0; j < Q->st[k].nrow; ++j) {
             double cx = 0.0;
             for (int l = 0; l < NX; ++l) cx += Q->st[k].C[j][l] * dx[k * NX + l];
-            const int r = 8 * N + 12 * k + 4 * j;
-            v[r] = cx + Q->st[k].hl[j] + sl[k * NS + j];
-            v[r + 1] = -cx + Q->st[k].hu[j] + su[k * NS + j];
-            v[r + 2] = sl[k * NS + j];
-            v[r + 3] = su[k * NS + j];
+            if (j < Q->st[k].nsoft) {
+                const int e = grp(Q, k, j), r = 8 * N + 4 * e;
+                v[r] = cx + Q->st[k].hl[j] + sl[e];
+                v[r + 1] = -cx + Q->st[k].hu[j] + su[e];
+                v[r + 2] = sl[e];
+                v[r + 3] = su[e];
+            } else {
+                const int r = Q->rh0 + 2 * (j - Q->st[k].nsoft);
+                v[r] = cx + Q->st[k].hl[j];
+                v[r + 1] = -cx + Q->st[k].hu[j];
+            }
         }
 }
 
@@ -123,15 +139,23 @@ static void stage_terms(const ipm_t* Q, int k, const double* sig, const double* 
         for (int b = 0; b < NX; ++b) Qx[a * NX + b] = S->H[a][b];
         qx[a] = S->g[a];
     }
-    for (int j = 0; j < NS; ++j) {  /* eliminated slack pair */
-        const int r0 = 8 * N + 12 * k + 4 * j;
-        const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
-        const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
-        /* written without the cancellation of Hl - sig (sig -> inf on an active row); equal to
-         * sig (Hl - sig) / Hl and -(v + sig gl / Hl) + ... */
-        const double fw = sig[r0] * (Zs + sig[r0 + 2]) / Hl + sig[r0 + 1] * (Zs + sig[r0 + 3]) / Hu;
-        const double fg = -(v[r0] * (Zs + sig[r0 + 2]) + sig[r0] * (zs - v[r0 + 2])) / Hl +
-                          (v[r0 + 1] * (Zs + sig[r0 + 3]) + sig[r0 + 1] * (zs - v[r0 + 3])) / Hu;
+    (void)o;
+    for (int j = 0; j < S->nrow; ++j) {
+        double fw, fg;
+        if (j < S->nsoft) {  /* eliminated slack pair */
+            const int r0 = 8 * N + 4 * grp(Q, k, j);
+            const double Zs = S->s * S->Zl[j], zs = S->s * S->zl[j];
+            const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
+            /* written without the cancellation of Hl - sig (sig -> inf on an active row); equal to
+             * sig (Hl - sig) / Hl and -(v + sig gl / Hl) + ... */
+            fw = sig[r0] * (Zs + sig[r0 + 2]) / Hl + sig[r0 + 1] * (Zs + sig[r0 + 3]) / Hu;
+            fg = -(v[r0] * (Zs + sig[r0 + 2]) + sig[r0] * (zs - v[r0 + 2])) / Hl +
+                 (v[r0 + 1] * (Zs + sig[r0 + 3]) + sig[r0 + 1] * (zs - v[r0 + 3])) / Hu;
+        } else {  /* hard row: the two sides fold like box rows */
+            const int r = Q->rh0 + 2 * (j - S->nsoft);
+            fw = sig[r] + sig[r + 1];
+            fg = -v[r] + v[r + 1];
+        }
         for (int a = 0; a < NX; ++a) {
             for (int b = 0; b < NX; ++b) Qx[a * NX + b] += fw * S->C[j][a] * S->C[j][b];
             qx[a] += fg * S->C[j][a];
@@ -254,15 +278,16 @@ static void node_slacks(const ipm_t* Q, int k, const double* sig, const double* 
     const int N = Q->N;
     const qp_opts_c* o = Q->o;
     const stage_t* S = &Q->st[k];
-    for (int j = 0; j < NS; ++j) {
-        const int r0 = 8 * N + 12 * k + 4 * j;
-        const double Zs = S->s * o->Zl[j], zs = S->s * o->zl[j];
+    (void)o;
+    for (int j = 0; j < S->nsoft; ++j) {
+        const int e = grp(Q, k, j), r0 = 8 * N + 4 * e;
+        const double Zs = S->s * S->Zl[j], zs = S->s * S->zl[j];
         const double Hl = Zs + sig[r0] + sig[r0 + 2], Hu = Zs + sig[r0 + 1] + sig[r0 + 3];
         const double gl = zs - v[r0] - v[r0 + 2], gu = zs - v[r0 + 1] - v[r0 + 3];
         double cx = 0.0;
         for (int l = 0; l < NX; ++l) cx += S->C[j][l] * xk[l];
-        sl[k * NS + j] = -(gl + sig[r0] * cx) / Hl;
-        su[k * NS + j] = -(gu - sig[r0 + 1] * cx) / Hu;
+        sl[e] = -(gl + sig[r0] * cx) / Hl;
+        su[e] = -(gu - sig[r0 + 1] * cx) / Hu;
     }
 }
 
@@ -539,13 +564,15 @@ void orc_qp_trace(double* buf, int max_rows) { g_trace = buf; g_trace_max = buf 
 
 /* One instance.  Returns IPM iterations (status via *conv: 1 converged). */
 static int solve_one(int N, const double* xn, const double* AB, const double* y, const double* Jy, const double* yN,
-                     const double* JyN, const double* h, const double* Jh, const double* x, const double* u,
+                     const double* JyN, const double* h, const double* Jh, const double* hE, const double* JhE,
+                     const double* x, const double* u,
                      const double* x0, const double* yref, const double* W, const double* yNref, const double* WN,
                      const double* dtv, const qp_opts_c* o, int ny, double* dx, double* du, double* slack, int* conv,
                      double* res) {
-    const int N1 = N + 1, m = 8 * N + 12 * N1;
+    const int N1 = N + 1, nsl = N * o->nh + o->nsN;
+    const int m = 8 * N + 4 * nsl + 2 * (o->nhN - o->nsN);
     ipm_t Q;
-    Q.N = N; Q.m = m; Q.o = o;
+    Q.N = N; Q.m = m; Q.o = o; Q.ns = o->nh; Q.rh0 = 8 * N + 4 * nsl;
     Q.st = (stage_t*)calloc((size_t)N1, sizeof(stage_t));
     Q.P = (double*)malloc(sizeof(double) * (size_t)N1 * NX * NX);
     Q.p = (double*)malloc(sizeof(double) * (size_t)N1 * NX);
@@ -572,10 +599,36 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     for (int k = 0; k <= N; ++k) {
         stage_t* S = &Q.st[k];
         S->s = (o->cost_scaling && k < N) ? dtv[k] : 1.0;
-        for (int j = 0; j < NS; ++j) {
-            for (int l = 0; l < NX; ++l) S->C[j][l] = Jh[((size_t)k * NX + l) * NS + j];
-            S->hl[j] = h[(size_t)k * NS + j] - o->lh[j];
-            S->hu[j] = o->uh[j] - h[(size_t)k * NS + j];
+        if (k < N) {  /* stage rows: columns h_col of h / J_h */
+            S->nsoft = S->nrow = o->nh;
+            for (int j = 0; j < o->nh; ++j) {
+                const int c = o->h_col[j];
+                for (int l = 0; l < NX; ++l) S->C[j][l] = Jh[((size_t)k * NX + l) * NS + c];
+                S->hl[j] = h[(size_t)k * NS + c] - o->lh[j];
+                S->hu[j] = o->uh[j] - h[(size_t)k * NS + c];
+                S->zl[j] = o->zl[j];
+                S->Zl[j] = o->Zl[j];
+            }
+        } else {  /* terminal rows: sums of an h[N] column and an hE column */
+            S->nsoft = o->nsN;
+            S->nrow = o->nhN;
+            for (int j = 0; j < o->nhN; ++j) {
+                const int c1 = o->hN_col[j], c2 = o->hE_col[j];
+                double hv = 0.0;
+                for (int l = 0; l < NX; ++l) S->C[j][l] = 0.0;
+                if (c1 >= 0) {
+                    hv += h[(size_t)k * NS + c1];
+                    for (int l = 0; l < NX; ++l) S->C[j][l] += Jh[((size_t)k * NX + l) * NS + c1];
+                }
+                if (c2 >= 0) {
+                    hv += hE[c2];
+                    for (int l = 0; l < NX; ++l) S->C[j][l] += JhE[l * 6 + c2];
+                }
+                S->hl[j] = hv - o->lhN[j];
+                S->hu[j] = o->uhN[j] - hv;
+                S->zl[j] = j < o->nsN ? o->zlN[j] : 0.0;
+                S->Zl[j] = j < o->nsN ? o->ZlN[j] : 0.0;
+            }
         }
         if (k < N) {
             const double* ab = AB + (size_t)k * NW * NX;
@@ -613,11 +666,11 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         } else {
             for (int i = 0; i < NX; ++i) {
                 double gs = 0.0;
-                for (int a = 0; a < 4; ++a) gs += JyN[i * 4 + a] * WN[a] * (yN[a] - yNref[a]);
+                for (int a = 0; a < o->nyN; ++a) gs += JyN[i * o->nyN + a] * WN[a] * (yN[a] - yNref[a]);
                 S->g[i] = gs;
                 for (int j = 0; j < NX; ++j) {
                     double hs = 0.0;
-                    for (int a = 0; a < 4; ++a) hs += JyN[i * 4 + a] * WN[a] * JyN[j * 4 + a];
+                    for (int a = 0; a < o->nyN; ++a) hs += JyN[i * o->nyN + a] * WN[a] * JyN[j * o->nyN + a];
                     S->H[i][j] = hs + (i == j ? o->lm : 0.0);
                 }
             }
@@ -648,9 +701,9 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     for (int r = 0; r < m; ++r) {
         t[r] = rv[r] > o->t0 ? rv[r] : o->t0;
         lam[r] = o->l0;
-        if (r >= 8 * N) {
-            const int q = r - 8 * N, k = q / 12, j = (q - 12 * k) >> 2;
-            const double lj = o->lc * Q.st[k].s * o->zl[j];
+        if (r >= 8 * N && r < Q.rh0) {  /* soft group e's rows (hard rows start at l0) */
+            const int e = (r - 8 * N) >> 2, k = (Q.ns > 0 && e < N * Q.ns) ? e / Q.ns : N, j = e - grp(&Q, k, 0);
+            const double lj = o->lc * Q.st[k].s * Q.st[k].zl[j];
             if (lj > lam[r]) lam[r] = lj;
         }
         if (fabs(rv[r] - t[r]) > rp) rp = fabs(rv[r] - t[r]);
@@ -662,7 +715,7 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     double* d0 = (double*)calloc((size_t)m, sizeof(double));
     {
         double* zero = (double*)calloc((size_t)nz, sizeof(double));
-        rows_at(&Q, zero, zero + N1 * NX, zero + N1 * NX + N * NU, zero + N1 * NX + N * NU + N1 * NS, d0);
+        rows_at(&Q, zero, zero + N1 * NX, zero + N1 * NX + N * NU, zero + N1 * NX + N * NU + N1 * NS, d0);  /* sl, su: nsl <= N1 NS */
         free(zero);
     }
     int it = 0, fail = 0;
@@ -752,11 +805,13 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
     }
     memcpy(dx, zdx, sizeof(double) * N1 * NX);
     memcpy(du, zdu, sizeof(double) * N * NU);
-    if (slack)
-        for (int e = 0; e < N1 * NS; ++e) {
-            slack[2 * e] = zsl[e];
-            slack[2 * e + 1] = zsu[e];
-        }
+    if (slack)  /* [N+1][3][2] by (node, row) */
+        for (int k = 0; k <= N; ++k)
+            for (int j = 0; j < NS; ++j) {
+                const int live = j < Q.st[k].nsoft, e = live ? grp(&Q, k, j) : 0;
+                slack[(k * NS + j) * 2] = live ? zsl[e] : 0.0;
+                slack[(k * NS + j) * 2 + 1] = live ? zsu[e] : 0.0;
+            }
     if (!isfinite(mu + rp)) fail = 1;
     *conv = fail ? -1 : (cm < o->tol && rp < o->tol && gap < o->tol);
     if (res) { res[0] = cm; res[1] = rp; res[2] = Q.seg_dev; res[3] = Q.gcount; }
@@ -765,9 +820,11 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
 }
 
 /* Batched entry point (OpenMP over instances).  opts: lbu 4, ubu 4, lh 3, uh 3, zl 3, Zl 3, lm, tol,
- * lm_scaling, then the IPM start / step parameters t0, l0, lc, tau_lo, tau_hi.  status (rti_qp.hip's convention): 0 converged, 1 max_iter, 2 numerical failure. */
+ * lm_scaling, then the IPM start / step parameters t0, l0, lc, tau_lo, tau_hi, nseg, the Gondzio options,
+ * ws, and from opts[35] the constraint set (see the body).  status (rti_qp.hip's convention): 0 converged, 1 max_iter, 2 numerical failure. */
 void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const double* y, const double* Jy,
-                      const double* yN, const double* JyN, const double* h, const double* Jh, const double* x,
+                      const double* yN, const double* JyN, const double* h, const double* Jh, const double* hE,
+                      const double* JhE, const double* x,
                       const double* u, const double* x0, const double* yref, const double* W, const double* yNref,
                       const double* WN, const double* dt, const double* opts, int max_iter, int cost_scaling, int ny,
                       double* dx, double* du, double* slack, int* iters, int* status, double* res, int nthreads) {
@@ -785,17 +842,33 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
     o.nseg = (int)opts[28];
     o.gk = (int)opts[29]; o.ga = opts[30]; o.gd = opts[31]; o.gbmin = opts[32]; o.gbmax = opts[33];
     o.ws = opts[34] != 0.0;
+    /* the constraint set: opts[35 ..] = nh, h_col 3, nhN, nsN, hN_col 8, hE_col 8, lhN 8, uhN 8, zlN 3, ZlN 3, nyN */
+    const double* cs = opts + 35;
+    o.nh = (int)cs[0];
+    for (int j = 0; j < 3; ++j) o.h_col[j] = (int)cs[1 + j];
+    o.nhN = (int)cs[4];
+    o.nsN = (int)cs[5];
+    for (int j = 0; j < NR; ++j) {
+        o.hN_col[j] = (int)cs[6 + j];
+        o.hE_col[j] = (int)cs[14 + j];
+        o.lhN[j] = cs[22 + j];
+        o.uhN[j] = cs[30 + j];
+    }
+    for (int j = 0; j < 3; ++j) { o.zlN[j] = cs[38 + j]; o.ZlN[j] = cs[41 + j]; }
+    o.nyN = (int)cs[44];
     o.max_iter = max_iter;
     o.cost_scaling = cost_scaling;
     const int N1 = N + 1;
 #pragma omp parallel for schedule(dynamic) num_threads(nthreads > 0 ? nthreads : 1)
     for (int b = 0; b < B; ++b) {
         int conv = 0;
+        const int nyN = o.nyN;
         iters[b] = solve_one(N, xn + (size_t)b * N * NX, AB + (size_t)b * N * NW * NX, y + (size_t)b * N * 11,
-                             Jy + (size_t)b * N * NW * 11, yN + (size_t)b * 4, JyN + (size_t)b * 40,
-                             h + (size_t)b * N1 * NS, Jh + (size_t)b * N1 * NX * NS, x + (size_t)b * N1 * NX,
+                             Jy + (size_t)b * N * NW * 11, yN + (size_t)b * nyN, JyN + (size_t)b * 10 * nyN,
+                             h + (size_t)b * N1 * NS, Jh + (size_t)b * N1 * NX * NS, hE ? hE + (size_t)b * 6 : NULL,
+                             JhE ? JhE + (size_t)b * 60 : NULL, x + (size_t)b * N1 * NX,
                              u + (size_t)b * N * NU, x0 + (size_t)b * NX, yref + (size_t)b * N * ny,
-                             W + (size_t)b * N * ny, yNref + (size_t)b * 4, WN + (size_t)b * 4, dt, &o, ny,
+                             W + (size_t)b * N * ny, yNref + (size_t)b * nyN, WN + (size_t)b * nyN, dt, &o, ny,
                              dx + (size_t)b * N1 * NX, du + (size_t)b * N * NU,
                              slack ? slack + (size_t)b * N1 * NS * 2 : NULL, &conv, res ? res + 4 * b : NULL);
         status[b] = conv < 0 ? 2 : conv ? 0 : 1;

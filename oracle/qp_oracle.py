@@ -9,7 +9,8 @@ nonlinear constraints idxsh with L1/L2 slack penalties, input box constraints, x
      + sum_{k<=N} s_k (zl.sl_k + 1/2 Zl.sl_k^2 + zu.su_k + 1/2 Zu.su_k^2)
   s.t. dx_0 = x0 - xbar_0,  dx_{k+1} = A_k dx_k + B_k du_k + (xn_k - xbar_{k+1})
        lbu - ubar_k <= du_k <= ubu - ubar_k
-       lh - h_k - sl_k <= J_h,k dx_k <= uh - h_k + su_k,  sl_k, su_k >= 0
+       lh - h_k - sl_k <= J_h,k dx_k <= uh - h_k + su_k,  sl_k, su_k >= 0   (the soft rows of the constraint set)
+       lhN - h_N <= J_hN dx_N <= uhN - h_N                                 (hard terminal rows: rec_feas / stability)
   w_k = [dx_k; du_k], r_k = y_k - yref_k, s_k = cost scaling (acados default: dt_k for k < N, 1 at N)
 
 HPIPM's algorithm (Riccati-based IPM) is not reproducible here (acados is absent; parity at the
@@ -23,8 +24,11 @@ import numpy as np
 def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=None, lm_scaling=True):
     """Assemble the per-stage QP data of ONE instance from the linearisation outputs.
 
-    lin: dict with xn [N,10], AB [N,14,10], y [N,11], Jy [N,14,11], yN [4], JyN [10,4], h [N+1,3],
-    Jh [N+1,10,3] (the sdfnmpc_linearize layouts, column-major blocks).
+    lin: dict with xn [N,10], AB [N,14,10], y [N,11], Jy [N,14,11], yN [nyN], JyN [10,nyN], h [N+1,3],
+    Jh [N+1,10,3] (+ hE [6], JhE [10,6] when a terminal row reads them) -- the sdfnmpc_linearize layouts,
+    column-major blocks.  The constraint set is model's (model.Quad: h_cols, term_rows): stage k < N has
+    the soft rows h[k][h_cols]; the terminal node the rows of term_rows (soft first, then hard), each the
+    sum of an h[N] column and an hE column (gen_model.py:26-149).
     """
     N = xbar.shape[0] - 1
     s = np.concatenate([dt, [1.0]]) if scaling is None else np.asarray(scaling, float)
@@ -44,30 +48,63 @@ def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=Non
     lmk = lm * np.asarray(dt, float)[:N] if lm_scaling else np.full(N, float(lm))
     q["H"] = np.einsum("kai,ka,kaj->kij", Jy, W, Jy) * s[:N, None, None] + lmk[:, None, None] * np.eye(14)
     q["g"] = np.einsum("kai,ka,ka->ki", Jy, W, r) * s[:N, None]
-    JyN = lin["JyN"].T                                         # [4,10]
+    JyN = np.asarray(lin["JyN"]).T                             # [nyN,10]
     rN = lin["yN"] - yNref
     q["HN"] = JyN.T @ np.diag(WN) @ JyN * s[N] + lm * np.eye(10)
     q["gN"] = JyN.T @ (WN * rN) * s[N]
-    q["C"] = np.transpose(lin["Jh"], (0, 2, 1))               # [N+1,3,10]
-    q["hl"] = lin["h"] - model.lh                              # constant of the lower soft row
-    q["hu"] = model.uh - lin["h"]
+    # stage rows (soft)
+    hc = list(getattr(model, "h_cols", [0, 1, 2]))
+    q["ns"] = len(hc)
+    q["C"] = np.transpose(lin["Jh"][:N][:, :, hc], (0, 2, 1))  # [N,ns,10]
+    q["hl"] = lin["h"][:N][:, hc] - np.asarray(model.lh)      # constant of the lower soft row
+    q["hu"] = np.asarray(model.uh) - lin["h"][:N][:, hc]
+    q["zl"], q["Zl"] = np.asarray(model.zl, float), np.asarray(model.Zl, float)
+    # terminal rows
+    rows = getattr(model, "term_rows", None)
+    if rows is None:
+        rows = [(c, -1, True, model.lh[i], model.uh[i], model.zl[i], model.Zl[i]) for i, c in enumerate(hc)]
+    CN, hN = [], []
+    for c1, c2, soft, lo, hi, zl, Zl in rows:
+        cr, hv = np.zeros(10), 0.0
+        if c1 >= 0:
+            cr = cr + lin["Jh"][N][:, c1]
+            hv += lin["h"][N][c1]
+        if c2 >= 0:
+            cr = cr + lin["JhE"][:, c2]
+            hv += lin["hE"][c2]
+        CN.append(cr)
+        hN.append(hv)
+    q["nhN"] = len(rows)
+    q["nsN"] = sum(1 for r_ in rows if r_[2])
+    q["CN"] = np.array(CN).reshape(len(rows), 10)
+    q["hlN"] = np.array(hN) - np.array([r_[3] for r_ in rows])
+    q["huN"] = np.array([r_[4] for r_ in rows]) - np.array(hN)
+    q["zlN"] = np.array([r_[5] for r_ in rows if r_[2]], float)
+    q["ZlN"] = np.array([r_[6] for r_ in rows if r_[2]], float)
     q["ulo"] = model.lbu - ubar                                # du >= ulo
     q["uhi"] = model.ubu - ubar
     q["x0"] = x0 - xbar[0]
-    q["zl"], q["Zl"] = model.zl, model.Zl
     return q
 
 
+def _layout(q):
+    """Variable offsets: z = [dx_0..dx_N, du_0..du_{N-1}, sl (stage groups k ns + j, then terminal soft rows),
+    su (same)].  With the default set (3 soft rows everywhere) sl / su are the [N+1][3] arrays."""
+    N, nx, nu = q["N"], 10, 4
+    nsl = N * q["ns"] + q["nsN"]
+    o_du = (N + 1) * nx
+    o_sl = o_du + N * nu
+    o_su = o_sl + nsl
+    return dict(N=N, nsl=nsl, o_du=o_du, o_sl=o_sl, o_su=o_su, nz=o_su + nsl)
+
+
 def dense_problem(q):
-    """The QP of stage_qp as one dense problem: min 1/2 z'Hz + g'z s.t. E z = e, G z + d >= 0, with
-    z = [dx_0..dx_N, du_0..du_{N-1}, sl_0..sl_N, su_0..su_N]."""
-    N = q["N"]
-    nx, nu, ns = 10, 4, 3
+    """The QP of stage_qp as one dense problem: min 1/2 z'Hz + g'z s.t. E z = e, G z + d >= 0 (z: _layout)."""
+    L = _layout(q)
+    N, nx, nu, ns = q["N"], 10, 4, q["ns"]
     ix = lambda k: k * nx
-    iu = lambda k: (N + 1) * nx + k * nu
-    isl = lambda k: (N + 1) * nx + N * nu + k * ns
-    isu = lambda k: (N + 1) * nx + N * nu + (N + 1) * ns + k * ns
-    nz = (N + 1) * nx + N * nu + 2 * (N + 1) * ns
+    iu = lambda k: L["o_du"] + k * nu
+    nz = L["nz"]
     H = np.zeros((nz, nz)); g = np.zeros(nz)
     s = q["s"]
     for k in range(N):
@@ -76,12 +113,13 @@ def dense_problem(q):
         g[idx] += q["g"][k]
     H[ix(N):ix(N) + nx, ix(N):ix(N) + nx] += q["HN"]
     g[ix(N):ix(N) + nx] += q["gN"]
-    for k in range(N + 1):
-        for j in range(ns):
-            H[isl(k) + j, isl(k) + j] += s[k] * q["Zl"][j]
-            H[isu(k) + j, isu(k) + j] += s[k] * q["Zl"][j]
-            g[isl(k) + j] += s[k] * q["zl"][j]
-            g[isu(k) + j] += s[k] * q["zl"][j]
+    # soft groups: (node, C row, hl, hu, zl, Zl)
+    groups = [(k, q["C"][k, j], q["hl"][k, j], q["hu"][k, j], q["zl"][j], q["Zl"][j]) for k in range(N) for j in range(ns)]
+    groups += [(N, q["CN"][j], q["hlN"][j], q["huN"][j], q["zlN"][j], q["ZlN"][j]) for j in range(q["nsN"])]
+    for e, (k, C, hl, hu, zl, Zl) in enumerate(groups):
+        for o in (L["o_sl"] + e, L["o_su"] + e):
+            H[o, o] += s[k] * Zl
+            g[o] += s[k] * zl
     # equalities E z = e
     ne = (N + 1) * nx
     E = np.zeros((ne, nz)); e = np.zeros(ne)
@@ -98,22 +136,41 @@ def dense_problem(q):
         for i in range(nu):
             a = np.zeros(nz); a[iu(k) + i] = 1.0; rows.append(a); d.append(-q["ulo"][k, i])
             a = np.zeros(nz); a[iu(k) + i] = -1.0; rows.append(a); d.append(q["uhi"][k, i])
-    for k in range(N + 1):
-        for j in range(ns):
-            C = q["C"][k, j]
-            a = np.zeros(nz); a[ix(k):ix(k) + nx] = C; a[isl(k) + j] = 1.0; rows.append(a); d.append(q["hl"][k, j])
-            a = np.zeros(nz); a[ix(k):ix(k) + nx] = -C; a[isu(k) + j] = 1.0; rows.append(a); d.append(q["hu"][k, j])
-            a = np.zeros(nz); a[isl(k) + j] = 1.0; rows.append(a); d.append(0.0)
-            a = np.zeros(nz); a[isu(k) + j] = 1.0; rows.append(a); d.append(0.0)
-    G = np.array(rows); d = np.array(d)
+    for e_, (k, C, hl, hu, zl, Zl) in enumerate(groups):
+        a = np.zeros(nz); a[ix(k):ix(k) + nx] = C; a[L["o_sl"] + e_] = 1.0; rows.append(a); d.append(hl)
+        a = np.zeros(nz); a[ix(k):ix(k) + nx] = -C; a[L["o_su"] + e_] = 1.0; rows.append(a); d.append(hu)
+        a = np.zeros(nz); a[L["o_sl"] + e_] = 1.0; rows.append(a); d.append(0.0)
+        a = np.zeros(nz); a[L["o_su"] + e_] = 1.0; rows.append(a); d.append(0.0)
+    for j in range(q["nsN"], q["nhN"]):  # hard terminal rows
+        a = np.zeros(nz); a[ix(N):ix(N) + nx] = q["CN"][j]; rows.append(a); d.append(q["hlN"][j])
+        a = np.zeros(nz); a[ix(N):ix(N) + nx] = -q["CN"][j]; rows.append(a); d.append(q["huN"][j])
+    G = np.array(rows).reshape(len(rows), nz); d = np.array(d)
     return H, g, E, e, G, d
 
 
+def _slack_nodes(q, v):
+    """Soft-slack vector (group order) -> [N+1][3] by (node, row) (zeros where a node has fewer rows)."""
+    N, ns = q["N"], q["ns"]
+    out = np.zeros((N + 1, 3))
+    out[:N, :ns] = v[:N * ns].reshape(N, ns)
+    out[N, :q["nsN"]] = v[N * ns:]
+    return out
+
+
+def z_of(q, sol):
+    """The dense variable vector of a solution dict (dx, du, sl / su as [N+1][3] by node and row)."""
+    N, ns = q["N"], q["ns"]
+    def flat(a):
+        a = np.asarray(a)
+        return np.concatenate([a[:N, :ns].ravel(), a[N, :q["nsN"]]])
+    return np.concatenate([np.asarray(sol["dx"]).ravel(), np.asarray(sol["du"]).ravel(), flat(sol["sl"]), flat(sol["su"])])
+
+
 def _unpack(q, z):
-    N, nx, nu, ns = q["N"], 10, 4, 3
-    o1, o2, o3 = (N + 1) * nx, (N + 1) * nx + N * nu, (N + 1) * nx + N * nu + (N + 1) * ns
-    return {"dx": z[:o1].reshape(N + 1, nx), "du": z[o1:o2].reshape(N, nu), "sl": z[o2:o3].reshape(N + 1, ns),
-            "su": z[o3:].reshape(N + 1, ns)}
+    L = _layout(q)
+    N, nx, nu = q["N"], 10, 4
+    return {"dx": z[:L["o_du"]].reshape(N + 1, nx), "du": z[L["o_du"]:L["o_sl"]].reshape(N, nu),
+            "sl": _slack_nodes(q, z[L["o_sl"]:L["o_su"]]), "su": _slack_nodes(q, z[L["o_su"]:])}
 
 
 def polish(q, sol, act_tol=1e-7):
@@ -121,7 +178,7 @@ def polish(q, sol, act_tol=1e-7):
     equality-constrained QP is solved directly (one dense KKT solve, no barrier terms, so no late-IPM
     ill-conditioning).  Returns the polished solution and the KKT check (min dual, max row violation)."""
     H, g, E, e, G, d = dense_problem(q)
-    z0 = np.concatenate([sol["dx"].ravel(), sol["du"].ravel(), sol["sl"].ravel(), sol["su"].ravel()])
+    z0 = z_of(q, sol)
     act = (G @ z0 + d) < act_tol
     Ga, da = G[act], d[act]
     nz, ne, na = H.shape[0], E.shape[0], Ga.shape[0]
@@ -141,7 +198,7 @@ def polish_active_set(q, sol, act_tol=1e-7, max_swaps=200):
     vertices (weakly active rows the IPM leaves at slack ~1e-6) need this where a single threshold cut
     of the IPM point picks a wrong set."""
     H, g, E, e, G, d = dense_problem(q)
-    z0 = np.concatenate([sol["dx"].ravel(), sol["du"].ravel(), sol["sl"].ravel(), sol["su"].ravel()])
+    z0 = z_of(q, sol)
     act = (G @ z0 + d) < act_tol
     nz, ne = H.shape[0], E.shape[0]
     for _ in range(max_swaps):
@@ -167,14 +224,8 @@ def polish_active_set(q, sol, act_tol=1e-7, max_swaps=200):
 
 def solve_dense(q, tol=1e-11, max_iter=100):
     """Mehrotra IPM on the full KKT system.  Returns dict(dx [N+1,10], du [N,4], sl, su [N+1,3], iters)."""
-    N = q["N"]
-    nx, nu, ns = 10, 4, 3
-    ix = lambda k: k * nx
-    iu = lambda k: (N + 1) * nx + k * nu
-    isl = lambda k: (N + 1) * nx + N * nu + k * ns
-    isu = lambda k: (N + 1) * nx + N * nu + (N + 1) * ns + k * ns
-    nz = (N + 1) * nx + N * nu + 2 * (N + 1) * ns
-    ne = (N + 1) * nx
+    L = _layout(q)
+    nz, ne = L["nz"], (q["N"] + 1) * 10
     H, g, E, e, G, d = dense_problem(q)
     m = G.shape[0]
     z = np.zeros(nz)
@@ -223,9 +274,6 @@ def solve_dense(q, tol=1e-11, max_iter=100):
         z += a * dz; y += a * dy; t += a * dt_; lam += a * dl
     if best is not None:  # max_iter without meeting tol: the best iterate seen
         _, z, t, lam, it = best
-    dx = np.array([z[ix(k):ix(k) + nx] for k in range(N + 1)])
-    du = np.array([z[iu(k):iu(k) + nu] for k in range(N)])
-    sl = np.array([z[isl(k):isl(k) + ns] for k in range(N + 1)])
-    su = np.array([z[isu(k):isu(k) + ns] for k in range(N + 1)])
-    return {"dx": dx, "du": du, "sl": sl, "su": su, "iters": it, "mu": t @ lam / m,
-            "obj": 0.5 * z @ H @ z + g @ z}
+    out = _unpack(q, z)
+    out.update(iters=it, mu=t @ lam / m, obj=0.5 * z @ H @ z + g @ z)
+    return out

@@ -23,7 +23,7 @@ L4C_PATH = os.path.join(LIB_DIR, "libsdf_l4c.so")
 SYMBOLS = [
     "sdfnmpc_abi_version", "sdfnmpc_last_error", "sdfnmpc_ctx_create", "sdfnmpc_ctx_destroy",
     "sdfnmpc_ctx_set_stream", "sdfnmpc_ctx_use_null_stream", "sdfnmpc_ctx_stream", "sdfnmpc_ctx_synchronize", "sdfnmpc_ctx_set_tile_rows",
-    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_set_sdf_server", "sdfnmpc_ctx_sdf_server_stats", "sdfnmpc_ctx_qp_kernel", "sdfnmpc_qp_lds_bytes", "sdfnmpc_qp_capacity",
+    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_set_sdf_server", "sdfnmpc_ctx_sdf_server_stats", "sdfnmpc_ctx_qp_kernel", "sdfnmpc_qp_lds_bytes", "sdfnmpc_qp_capacity", "sdfnmpc_qp_capacity_for",
     "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
@@ -46,22 +46,32 @@ class SdfnmpcError(RuntimeError):
     pass
 
 
+POLY_MAX, NHN_MAX = 84, 8  # SDFNMPC_POLY_MAX, SDFNMPC_NHN_MAX
+
+
 class QuadModelC(C.Structure):
     _fields_ = [("gamma", C.c_double), ("roll", C.c_double), ("pitch", C.c_double), ("wz", C.c_double),
                 ("g", C.c_double), ("B_p_C", C.c_double * 3), ("B_R_C", C.c_double * 9),
-                ("fov_const_offset", C.c_double)]
+                ("fov_const_offset", C.c_double), ("rec_feas", C.c_int), ("stability", C.c_int),
+                ("poly_deg", C.c_int), ("poly", C.c_double * POLY_MAX)]
+
+
+LIN_PTRS = ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "sdf")
 
 
 class LinArgsC(C.Structure):
     _fields_ = [("B", C.c_int), ("N", C.c_int), ("np", C.c_int), ("latent_mode", C.c_int)] + [
-        (n, C.c_void_p) for n in ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "sdf")]
+        (n, C.c_void_p) for n in LIN_PTRS] + [("nyN", C.c_int), ("no_sdf", C.c_int), ("hE", C.c_void_p),
+                                             ("JhE", C.c_void_p)]
 
 
 class QpOptsC(C.Structure):
     _fields_ = [("lbu", C.c_double * 4), ("ubu", C.c_double * 4), ("lh", C.c_double * 3), ("uh", C.c_double * 3),
                 ("zl", C.c_double * 3), ("Zl", C.c_double * 3), ("lm", C.c_double), ("cost_scaling", C.c_int),
                 ("max_iter", C.c_int), ("tol", C.c_double), ("ny", C.c_int), ("lm_scaling", C.c_int),
-                ("warm_start", C.c_int)]
+                ("warm_start", C.c_int), ("nh", C.c_int), ("h_col", C.c_int * 3), ("nhN", C.c_int), ("nsN", C.c_int),
+                ("hN_col", C.c_int * NHN_MAX), ("hE_col", C.c_int * NHN_MAX), ("lhN", C.c_double * NHN_MAX),
+                ("uhN", C.c_double * NHN_MAX), ("zlN", C.c_double * 3), ("ZlN", C.c_double * 3), ("nyN", C.c_int)]
 
 
 class RefOptsC(C.Structure):
@@ -77,10 +87,10 @@ REF_OUT = ("p", "yref", "W", "yNref", "WN")
 class RefArgsC(C.Structure):
     _fields_ = [("B", C.c_int), ("N", C.c_int), ("np", C.c_int), ("ny", C.c_int), ("n_wp", C.c_int),
                 ("L", C.c_int), ("x0", C.c_void_p), ("x0_stride", C.c_int)] + [
-        (n, C.c_void_p) for n in REF_IN + REF_OUT]
+        (n, C.c_void_p) for n in REF_IN + REF_OUT] + [("nyN", C.c_int)]
 
 
-QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", "W", "yNref", "WN", "dt")
+QP_IN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "hE", "JhE", "x", "u", "x0", "yref", "W", "yNref", "WN", "dt")
 QP_OUT = ("dx", "du", "slack", "status", "iters", "res")
 
 
@@ -128,6 +138,7 @@ def load():
         "sdfnmpc_ctx_qp_kernel": (i, [vp, i, i]),
         "sdfnmpc_qp_lds_bytes": (C.c_longlong, [i]),
         "sdfnmpc_qp_capacity": (C.c_longlong, [vp, i]),
+        "sdfnmpc_qp_capacity_for": (C.c_longlong, [vp, i, P(QpOptsC)]),
         "sdfnmpc_ctx_enable_timing": (i, [vp, i]),
         "sdfnmpc_ctx_kernel_stats": (i, [vp, C.c_char_p, P(d), P(ll)]),
         "sdfnmpc_ctx_reset_stats": (i, [vp]),
@@ -168,7 +179,7 @@ def load():
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    if lib.sdfnmpc_abi_version() != 4:
+    if lib.sdfnmpc_abi_version() != 5:
         raise SdfnmpcError("libsdfnmpc.so ABI version mismatch")
     _lib = lib
     return lib
@@ -246,9 +257,11 @@ class Context:
         k = load().sdfnmpc_ctx_qp_kernel(self.h, N, B)
         return {1: "serial", 2: "segmented"}.get(k, "invalid")
 
-    def qp_capacity(self, N: int) -> int:
-        """Instances this device solves in one wave of QP workgroups at horizon N (sdfnmpc_qp_capacity)."""
-        n = int(load().sdfnmpc_qp_capacity(self.h, N))
+    def qp_capacity(self, N: int, opts: "QpOptsC" = None) -> int:
+        """Instances this device solves in one wave of QP workgroups at horizon N (sdfnmpc_qp_capacity; with
+        opts: for that constraint set, sdfnmpc_qp_capacity_for)."""
+        lib = load()
+        n = int(lib.sdfnmpc_qp_capacity(self.h, N) if opts is None else lib.sdfnmpc_qp_capacity_for(self.h, N, C.byref(opts)))
         if n < 0:
             raise SdfnmpcError(f"sdfnmpc_qp_capacity: bad arguments (N={N})")
         return n
@@ -359,30 +372,48 @@ class Net:
             pass
 
 
-def quad_model(cfg) -> QuadModelC:
+def quad_model(cfg, model=None) -> QuadModelC:
+    """Model constants of a config; ``model`` (model.Quad) adds the terminal extras of its flags
+    (recursive_feasibility: the braking polynomial; stability)."""
     lim = cfg.robot.limits
     R = np.asarray(cfg.sensor.B_R_C, dtype=np.float64).ravel()
-    return QuadModelC(float(lim.gamma), float(lim.roll), float(lim.pitch), float(lim.wz), 9.81,
-                      (C.c_double * 3)(*[float(v) for v in cfg.sensor.B_p_C]), (C.c_double * 9)(*R),
-                      float(cfg.mpc.fov_const_offset))
+    m = QuadModelC(float(lim.gamma), float(lim.roll), float(lim.pitch), float(lim.wz), 9.81,
+                   (C.c_double * 3)(*[float(v) for v in cfg.sensor.B_p_C]), (C.c_double * 9)(*R),
+                   float(cfg.mpc.fov_const_offset))
+    if model is not None:
+        m.rec_feas, m.stability = int(model.rec_feas), int(model.stability)
+        m.poly_deg = int(model.poly_deg)
+        for i, c in enumerate(model.poly):
+            m.poly[i] = float(c)
+    return m
 
 
-def linearize(ctx: Context, net: Net, model: QuadModelC, B: int, N: int, np_: int, bufs: dict, latent_mode=0):
-    """Enqueue the batched preparation phase.  bufs: device tensors named as sdfnmpc_lin_args."""
-    a = LinArgsC(B, N, np_, latent_mode, *[_ptr(bufs.get(k)) for k in
-                                           ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh",
-                                            "sdf")])
-    _check(load().sdfnmpc_linearize(ctx.h, net.h, C.byref(model), C.byref(a)))
+def lin_args(B: int, N: int, np_: int, bufs: dict, latent_mode=0, nyN=4, no_sdf=False) -> LinArgsC:
+    return LinArgsC(B, N, np_, latent_mode, *[_ptr(bufs.get(k)) for k in LIN_PTRS], int(nyN), int(bool(no_sdf)),
+                    _ptr(bufs.get("hE")), _ptr(bufs.get("JhE")))
+
+
+def linearize(ctx: Context, net, model: QuadModelC, B: int, N: int, np_: int, bufs: dict, latent_mode=0, nyN=4,
+              no_sdf=False):
+    """Enqueue the batched preparation phase.  bufs: device tensors named as sdfnmpc_lin_args (net may be
+    None with no_sdf)."""
+    a = lin_args(B, N, np_, bufs, latent_mode, nyN, no_sdf)
+    _check(load().sdfnmpc_linearize(ctx.h, None if net is None else net.h, C.byref(model), C.byref(a)))
 
 
 def qp_opts(model, lm=10.0, cost_scaling=True, max_iter=100, tol=1e-8, lm_scaling=True, warm_start=False) -> QpOptsC:
-    """QP data of the 'att' model (model.Quad) + solver options (ocp.py:113-120 defaults).  lm_scaling: the
-    Levenberg-Marquardt term is lm dt_k at stages k < N and lm at N (acados' Ts-scaled term).  warm_start:
-    HPIPM's primal warm start (ocp.py:116) -- the IPM starts from the du buffer's entry values."""
-    v = lambda a, n: (C.c_double * n)(*[float(x) for x in a])
+    """QP data of the 'att' model (model.Quad: bounds, the constraint set of its flags) + solver options
+    (ocp.py:113-120 defaults).  lm_scaling: the Levenberg-Marquardt term is lm dt_k at stages k < N and lm at
+    N (acados' Ts-scaled term).  warm_start: HPIPM's primal warm start (ocp.py:116) -- the IPM starts from
+    the du buffer's entry values."""
+    v = lambda a, n: (C.c_double * n)(*([float(x) for x in a] + [0.0] * (n - len(a))))
+    iv = lambda a, n: (C.c_int * n)(*([int(x) for x in a] + [-1] * (n - len(a))))
+    rows = model.term_rows
     return QpOptsC(v(model.lbu, 4), v(model.ubu, 4), v(model.lh, 3), v(model.uh, 3), v(model.zl, 3),
                    v(model.Zl, 3), float(lm), int(bool(cost_scaling)), int(max_iter), float(tol), int(model.ny),
-                   int(bool(lm_scaling)), int(bool(warm_start)))
+                   int(bool(lm_scaling)), int(bool(warm_start)), int(model.nh), iv(model.h_cols, 3), int(model.nhN),
+                   int(model.nsN), iv([r[0] for r in rows], NHN_MAX), iv([r[1] for r in rows], NHN_MAX),
+                   v(model.lhN, NHN_MAX), v(model.uhN, NHN_MAX), v(model.zlN, 3), v(model.ZlN, 3), int(model.nyN))
 
 
 def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
@@ -391,15 +422,14 @@ def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
     _check(load().sdfnmpc_qp_solve(ctx.h, C.byref(opts), C.byref(a)))
 
 
-def rti_prepare(ctx: Context, net: Net, model: QuadModelC, opts: QpOptsC, B: int, N: int, np_: int, bufs: dict,
-                latent_mode=0):
+def rti_prepare(ctx: Context, net, model: QuadModelC, opts: QpOptsC, B: int, N: int, np_: int, bufs: dict,
+                latent_mode=0, no_sdf=False):
     """Enqueue the RTI preparation phase acados-style: linearisation + the QP's stage records (everything
     but x0).  bufs: device tensors named as sdfnmpc_lin_args and sdfnmpc_qp_args."""
-    la = LinArgsC(B, N, np_, latent_mode, *[_ptr(bufs.get(k)) for k in
-                                            ("x", "u", "p", "dt", "xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh",
-                                             "sdf")])
+    la = lin_args(B, N, np_, bufs, latent_mode, opts.nyN, no_sdf)
     qa = QpArgsC(B, N, *[_ptr(bufs.get(k)) for k in QP_IN + QP_OUT])
-    _check(load().sdfnmpc_rti_prepare(ctx.h, net.h, C.byref(model), C.byref(la), C.byref(opts), C.byref(qa)))
+    _check(load().sdfnmpc_rti_prepare(ctx.h, None if net is None else net.h, C.byref(model), C.byref(la),
+                                      C.byref(opts), C.byref(qa)))
 
 
 def qp_feedback(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
@@ -434,11 +464,12 @@ def ref_opts(cfg, mode: int) -> RefOptsC:
                     v(cfg.sensor.B_p_C, 3), v(cfg.sensor.B_R_C, 9))
 
 
-def pack_refs(ctx: Context, opts: RefOptsC, B: int, N: int, np_: int, ny: int, bufs: dict, n_wp: int = 0, L: int = 0):
+def pack_refs(ctx: Context, opts: RefOptsC, B: int, N: int, np_: int, ny: int, bufs: dict, n_wp: int = 0, L: int = 0,
+              nyN: int = 4):
     """Enqueue sdfnmpc_pack_refs.  bufs: device tensors named as sdfnmpc_ref_args (x0 [B][stride])."""
     x0 = bufs.get("x0")
     stride = int(x0.shape[-1]) if x0 is not None else 0
-    a = RefArgsC(B, N, np_, ny, n_wp, L, _ptr(x0), stride, *[_ptr(bufs.get(k)) for k in REF_IN + REF_OUT])
+    a = RefArgsC(B, N, np_, ny, n_wp, L, _ptr(x0), stride, *[_ptr(bufs.get(k)) for k in REF_IN + REF_OUT], int(nyN))
     _check(load().sdfnmpc_pack_refs(ctx.h, C.byref(opts), C.byref(a)))
 
 
@@ -559,14 +590,15 @@ class Solver:
 
     INT_FIELDS = ("status", "iters")
 
-    def __init__(self, ctx: Context, net: Net, model: QuadModelC, qp: QpOptsC, B: int, N: int, np_: int, ny: int,
+    def __init__(self, ctx: Context, net, model: QuadModelC, qp: QpOptsC, B: int, N: int, np_: int, ny: int,
                  dt, latent_mode: int = 0):
+        """net may be None when the constraint set and the cost never read the SDF (model.Quad.need_sdf)."""
         self.ctx, self.net, self.B, self.N, self.np, self.ny = ctx, net, int(B), int(N), int(np_), int(ny)
         self._dt = np.ascontiguousarray(dt, dtype=np.float64)
         o = SolverOptsC(self.B, self.N, self.np, self.ny, int(latent_mode),
                         self._dt.ctypes.data_as(C.POINTER(C.c_double)), model, qp)
         h = C.c_void_p()
-        _check(load().sdfnmpc_solver_create(ctx.h, net.h, C.byref(o), C.byref(h)))
+        _check(load().sdfnmpc_solver_create(ctx.h, None if net is None else net.h, C.byref(o), C.byref(h)))
         self.h = h
         self._shapes = {}
         self.u0 = np.zeros((self.B, 4))

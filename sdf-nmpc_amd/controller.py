@@ -31,11 +31,14 @@ from .model import Quad
 class Nmpc:
     """Wrapper around the NMPC controller with range image-based collision prediction (batched)."""
 
-    def __init__(self, cfg, rebuild=False, batch: int = 1, device: int = 0, weights=None, ocp=None):
+    def __init__(self, cfg, rebuild=False, batch: int = 1, device: int = 0, weights=None, ocp=None,
+                 braking_coeffs=None):
+        """braking_coeffs: the braking-distance polynomial of flags.recursive_feasibility (default: the
+        config's mpc.braking_dist.coeff_file under the cache dir, as gen_model.py:76-77 loads it)."""
         from .ocp import Ocp
 
         self.cfg = cfg
-        self.model = Quad(cfg)
+        self.model = getattr(ocp, "model", None) or Quad(cfg, braking_coeffs=braking_coeffs)
         self.T = cfg.mpc.T
         self.N = int(cfg.mpc.N)
         self.B = int(batch)
@@ -188,8 +191,14 @@ class Nmpc:
         return paths[0] if self.B == 1 else paths
 
     def eval(self, k):
-        """The model's evaluation vector at node k: the SDF value with flag = 1 (gen_model.py:64,
-        controller.py:128-133), at the current iterate, computed by the HIP SDF kernel."""
+        """The model's evaluation vector at node k (controller.py:125-130, base_model.py:119-125): [0] without
+        flags.enable_sdf; else the SDF value with flag = 1 (gen_model.py:64, computed by the HIP SDF kernel),
+        and with recursive_feasibility the braking distance poly(v) and sdf - poly(v), flag = 1
+        (gen_model.py:116-117)."""
+        m = self.model
+        if not m.enable_sdf:
+            return [0] if self.B == 1 else np.zeros((self.B, 1))
+        from .model import poly_eval
         idx = self.cfg.mpc.p_idx
         x = self.ocp.download("x")[:, k]
         p = self.p if self.B > 1 else self.p[None]
@@ -197,7 +206,11 @@ class Nmpc:
         W_R_Co = pk[:, idx.W_R_Co].reshape(-1, 3, 3)
         Co_p_B = np.einsum("bji,bj->bi", W_R_Co, x[:, :3] - pk[:, idx.W_p_Co])
         df, _ = self.ocp.net.eval_host(np.concatenate([Co_p_B, pk[:, idx.latent:]], axis=1), want_grad=False)
-        return df[:1] if self.B == 1 else df[:, None]
+        out = df[:, None]
+        if m.rec_feas:
+            bd, _ = poly_eval(m.poly, m.poly_deg, x[:, 7:10])
+            out = np.concatenate([out, bd[:, None], (df - bd)[:, None]], axis=1)
+        return out[0] if self.B == 1 else out
 
     # ---- device-side parameter packing (csrc/ref_pack.hip)
     def _dev(self, a):
@@ -244,7 +257,7 @@ class Nmpc:
         for k in ("p", "yref", "W", "yNref", "WN"):
             args[k] = self.ocp.field(k)
         _lib.pack_refs(self.ocp.ctx, _lib.ref_opts(self.cfg, code), Bn, self.N, self.model.np, self.model.ny, args,
-                       n_wp=n_wp)
+                       n_wp=n_wp, nyN=self.model.nyN)
         self.ocp.ctx.synchronize()  # the temporary inputs are freed on return
         self._clean("q_d", "yref", "W", "yNref", "WN")
 
@@ -283,7 +296,8 @@ class Nmpc:
                 else:  # another device: through the host, once per array
                     host[k] = _download(v, Bn, cols[k])
                     args[k] = _lib.DeviceArray.from_numpy(part.ctx, np.ascontiguousarray(host[k][lo:part.hi]))
-            _lib.pack_refs(part.ctx, _lib.ref_opts(self.cfg, -1), nb, self.N, self.model.np, self.model.ny, args, L=L)
+            _lib.pack_refs(part.ctx, _lib.ref_opts(self.cfg, -1), nb, self.N, self.model.np, self.model.ny, args, L=L,
+                           nyN=self.model.nyN)
         for part in parts:
             part.ctx.synchronize()
         self._clean("pose", "latent", *(("flag",) if flag is not None else ()))

@@ -121,6 +121,7 @@ struct sdfnmpc_ctx {
         bool sdf_row_patch = false;  // the feedback's QP kernel copies the sdf row of C^T into them
         int ny = 0, cost_scaling = 0, lm_scaling = 0;  // the qp options the records were packed under
         double lm = 0.0;
+        long long cset = 0;  // and their constraint set (cset_key)
     } prep;
 };
 
@@ -335,6 +336,14 @@ extern "C" int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel) {
 // the serial kernel at N = 40, 24 % at N = 60, equal at N = 30, 30 % slower at N = 20 where the three
 // couplings outweigh five-node segments), the serial one otherwise (one wavefront per instance: at
 // B = 1024 it fills every SIMD once and is 1.6x faster than four wavefronts per instance)
+// the segmented kernel covers the default row set (h = [hfov, vfov, sdf] at every node); any other
+// constraint set runs on the serial kernel
+static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, QpRows q) {
+    const QpRows d = qp_rows_default();
+    if (q.ns != d.ns || q.nhN != d.nhN || q.nsN != d.nsN) return (ctx && N >= 1 && B >= 0) ? SDFNMPC_QP_SERIAL : -1;
+    return sdfnmpc_ctx_qp_kernel(ctx, N, B);
+}
+
 extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B) {
     if (!ctx || N < 1 || B < 0) return -1;
     if (ctx->qp_kernel == SDFNMPC_QP_SERIAL || !rti_qp_seg_supported(N)) return SDFNMPC_QP_SERIAL;
@@ -353,18 +362,26 @@ extern "C" long long sdfnmpc_qp_lds_bytes(int N) {
 // Instances the context's device solves in one wave of QP workgroups: every CU holds as many
 // instances as its LDS fits (the QP keeps each instance's iterate, duals and record window in LDS;
 // rti_qp.hip: one 64-lane workgroup per instance, rti_qp_seg.hip: one workgroup of NSEG waves).
-extern "C" long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N) {
+static int qp_cset_check(const sdfnmpc_qp_opts* o);
+static QpRows qp_rows_of(const sdfnmpc_qp_opts* o);
+static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, QpRows q);
+
+extern "C" long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N) { return sdfnmpc_qp_capacity_for(ctx, N, nullptr); }
+
+extern "C" long long sdfnmpc_qp_capacity_for(const sdfnmpc_ctx* ctx, int N, const sdfnmpc_qp_opts* o) {
     if (!ctx || N < 1) return -1;
     if (ctx->n_cu <= 0 || ctx->lds_per_cu == 0) return -1;
+    if (o && qp_cset_check(o)) return -1;
+    const QpRows rows = o ? qp_rows_of(o) : qp_rows_default();
     // a batch that fills the device: the kernel AUTO picks above SDFNMPC_QP_SEG_AUTO_MAX_B
-    const bool seg = sdfnmpc_ctx_qp_kernel(ctx, N, 1 << 30) == SDFNMPC_QP_SEGMENTED;
-    const size_t per = seg ? qp_seg_lds_bytes(N) : qp_lds_bytes(N);
+    const bool seg = qp_kernel_for(ctx, N, 1 << 30, rows) == SDFNMPC_QP_SEGMENTED;
+    const size_t per = seg ? qp_seg_lds_bytes(N) : qp_lds_bytes(N, rows);
     if (per == 0 || per > ctx->lds_per_cu) return 0;  // the horizon does not fit one CU's LDS
     // the runtime's occupancy of the kernel (LDS, registers and waves at once): the serial kernel's 375
     // registers allow one wave per SIMD, four instances per CU, whatever the LDS would admit; the segmented
     // kernel's __launch_bounds__ two or three workgroups per CU
     ScopedDevice sd(ctx->device);
-    const int occ = seg ? rti_qp_seg_blocks_per_cu(N) : rti_qp_blocks_per_cu(N);
+    const int occ = seg ? rti_qp_seg_blocks_per_cu(N) : rti_qp_blocks_per_cu(N, rows);
     const long long by_lds = (long long)(ctx->lds_per_cu / per);
     return (long long)ctx->n_cu * std::min<long long>(by_lds, occ > 0 ? occ : 0);
 }
@@ -1280,14 +1297,23 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
 // follows the join.
 static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
                     const sdfnmpc_lin_args* a, const QpArgs* pk) {
-    if (!ctx || !net || !mdl || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
-    if (a->B < 0 || a->N < 1 || a->np < 17 + net->host.L || (a->latent_mode != 0 && a->latent_mode != 1))
+    if (!ctx || !mdl || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
+    const bool no_sdf = a->no_sdf != 0;
+    if (!net && !no_sdf) return fail(SDFNMPC_E_ARG, "NULL network (only allowed with lin_args.no_sdf)");
+    if (a->B < 0 || a->N < 1 || a->np < 17 + (net ? net->host.L : 0) || (a->latent_mode != 0 && a->latent_mode != 1))
         return fail(SDFNMPC_E_ARG, "bad B/N/np/latent_mode");
+    const int nyN = a->nyN == 0 ? 4 : a->nyN;
+    if (nyN != 4 && nyN != 5) return fail(SDFNMPC_E_ARG, "lin_args.nyN must be 4 or 5");
+    if ((nyN == 5) != (mdl->stability != 0)) return fail(SDFNMPC_E_ARG, "nyN == 5 exactly with model.stability");
+    if (mdl->rec_feas && (mdl->poly_deg < 0 || mdl->poly_deg > SDFNMPC_POLY_DEG_MAX))
+        return fail(SDFNMPC_E_ARG, "model.poly_deg must be 0..6");
+    if ((mdl->rec_feas || mdl->stability) && (!a->hE || !a->JhE))
+        return fail(SDFNMPC_E_ARG, "rec_feas / stability need lin_args.hE and JhE");
     if (a->B == 0) return SDFNMPC_OK;
     if (!a->x || !a->u || !a->p || !a->dt || !a->xn || !a->AB || !a->y || !a->Jy || !a->yN || !a->JyN || !a->h ||
         !a->Jh)
         return fail(SDFNMPC_E_ARG, "NULL array in sdfnmpc_lin_args");
-    if (net->device != ctx->device) return fail(SDFNMPC_E_ARG, "net and ctx are on different devices");
+    if (net && net->device != ctx->device) return fail(SDFNMPC_E_ARG, "net and ctx are on different devices");
     ScopedDevice sd(ctx->device);
     const long long rows = (long long)a->B * (a->N + 1);
     float4* sdf4 = (float4*)a->sdf;
@@ -1296,7 +1322,7 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
         sdf4 = (float4*)ctx->sdf4.p;
     }
     const int n_inst = a->latent_mode == 0 ? a->B : (int)rows;
-    if (!net->wide) HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
+    if (!no_sdf && !net->wide) HIPCHK(ctx->c13.ensure((size_t)n_inst * C13_STRIDE * sizeof(float)));
     // dynamics / cost / FOV constraints (independent of the network): forked onto the low-priority
     // aux stream so they fill the CUs the SDF kernel leaves idle (its tail), joined at the end
     LinArgs la{};
@@ -1307,9 +1333,17 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
     for (int i = 0; i < 3; ++i)  // B_R_C^T B_p_C + [fov_const_offset, 0, 0]
         la.m.fov_off[i] = mdl->B_R_C[0 * 3 + i] * mdl->B_p_C[0] + mdl->B_R_C[1 * 3 + i] * mdl->B_p_C[1] +
                           mdl->B_R_C[2 * 3 + i] * mdl->B_p_C[2] + (i == 0 ? mdl->fov_const_offset : 0.0);
-    la.m.max_df = net->host.max_df;
+    la.m.max_df = net ? net->host.max_df : 1.0;
+    for (int i = 0; i < 9; ++i) la.m.B_R_C[i] = mdl->B_R_C[i];
+    la.m.rec_feas = mdl->rec_feas ? 1 : 0;
+    la.m.stability = mdl->stability ? 1 : 0;
+    la.m.poly_deg = mdl->poly_deg;
+    for (int i = 0; i < SDFNMPC_POLY_MAX; ++i) la.m.poly[i] = mdl->poly[i];
+    la.hE = a->hE;
+    la.JhE = a->JhE;
+    la.nyN = nyN;
     QpArgs pa{};
-    const bool split = pk && pk->ny == 11 && !ctx->serial_prep;  // pack beside the SDF kernel
+    const bool split = pk && pk->ny == 11 && !ctx->serial_prep && !no_sdf;  // pack beside the SDF kernel
     if (pk) {
         pa = *pk;
         pa.pack_part = split ? 1 : 0;
@@ -1331,6 +1365,10 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
         return SDFNMPC_OK;
     };
     int rc;
+    if (no_sdf) {  // no constraint or cost reads the network: the linearisation alone, then the pack
+        HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }, ctx->stream));
+        return finish_pack();
+    }
     if (ctx->lin_first && (rc = fork_lin())) return rc;
     // 2. latent hoisting (latent = p[.][17:] as fp32)
     const long long stride = a->latent_mode == 0 ? (long long)(a->N + 1) * a->np : (long long)a->np;
@@ -1387,6 +1425,31 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
 
 // ------------------------------------------------------------------------------------------------
 // batched QP (feedback phase) and RTI step
+// the constraint set of sdfnmpc_qp_opts (include/sdfnmpc.h): counts, columns and their order
+static int qp_cset_check(const sdfnmpc_qp_opts* o) {
+    if (o->nh < 0 || o->nh > 3) return fail(SDFNMPC_E_ARG, "qp opts: nh must be 0..3");
+    for (int j = 0; j < o->nh; ++j)
+        if (o->h_col[j] < 0 || o->h_col[j] > 2 || (j && o->h_col[j] <= o->h_col[j - 1]))
+            return fail(SDFNMPC_E_ARG, "qp opts: h_col must be increasing columns 0..2");
+    if (o->nhN < 0 || o->nhN > SDFNMPC_NHN_MAX || o->nsN < 0 || o->nsN > 3 || o->nsN > o->nhN || o->nhN - o->nsN > 6)
+        return fail(SDFNMPC_E_ARG, "qp opts: terminal rows nhN <= 8 with nsN <= 3 soft and <= 6 hard");
+    for (int j = 0; j < o->nhN; ++j) {
+        if (o->hN_col[j] < -1 || o->hN_col[j] > 2 || o->hE_col[j] < -1 || o->hE_col[j] >= SDFNMPC_NHE ||
+            (o->hN_col[j] < 0 && o->hE_col[j] < 0))
+            return fail(SDFNMPC_E_ARG, "qp opts: terminal row j needs hN_col in -1..2 / hE_col in -1..5, not both -1");
+        if (!(o->lhN[j] <= o->uhN[j])) return fail(SDFNMPC_E_ARG, "qp opts: terminal bounds lhN > uhN");
+    }
+    if (o->nyN != 4 && o->nyN != 5) return fail(SDFNMPC_E_ARG, "qp opts: nyN must be 4 or 5");
+    return SDFNMPC_OK;
+}
+static QpRows qp_rows_of(const sdfnmpc_qp_opts* o) { return QpRows{o->nh, o->nhN, o->nsN}; }
+// the network is read by a constraint row (stage h_col or terminal hN_col == 2) or the sdf cost
+static bool qp_needs_sdf(const sdfnmpc_qp_opts* o) {
+    bool need = o->ny == 12;
+    for (int j = 0; j < o->nh; ++j) need = need || o->h_col[j] == 2;
+    for (int j = 0; j < o->nhN; ++j) need = need || o->hN_col[j] == 2;
+    return need;
+}
 // validation and kernel arguments shared by sdfnmpc_qp_solve / sdfnmpc_rti_prepare / sdfnmpc_qp_feedback
 // (sizes the workspace; the caller holds the device scope)
 static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* a, QpArgs& q) {
@@ -1397,13 +1460,19 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
     if (o->lm <= 0.0 || o->max_iter < 1 || !(o->tol > 0.0))
         return fail(SDFNMPC_E_ARG, "qp opts: lm > 0 (strict convexity), max_iter >= 1, tol > 0 required");
     if (o->ny != 11 && o->ny != 12) return fail(SDFNMPC_E_ARG, "qp opts: ny must be 11 or 12 (sdf_cost)");
-    if (qp_lds_bytes(a->N) > ctx->lds_per_cu) return fail(SDFNMPC_E_UNSUPPORTED, "horizon too long for the LDS-resident QP");
+    if (int rc = qp_cset_check(o)) return rc;
+    bool term_e = false;
+    for (int j = 0; j < o->nhN; ++j) term_e = term_e || o->hE_col[j] >= 0;
+    if (term_e && (!a->hE || !a->JhE)) return fail(SDFNMPC_E_ARG, "qp args: terminal rows read hE / JhE (NULL)");
+    if (qp_lds_bytes(a->N, qp_rows_of(o)) > ctx->lds_per_cu)
+        return fail(SDFNMPC_E_UNSUPPORTED, "horizon too long for the LDS-resident QP");
     HIPCHK(ctx->qpw.ensure((size_t)a->B * qp_work_doubles(a->N) * sizeof(double)));
     const bool own_st = !a->status || !a->iters || !a->res;
     if (own_st) HIPCHK(ctx->qpst.ensure((size_t)a->B * (2 * sizeof(int) + 2 * sizeof(double))));
     q = QpArgs{};
     q.B = a->B; q.N = a->N;
     q.xn = a->xn; q.AB = a->AB; q.y = a->y; q.Jy = a->Jy; q.yN = a->yN; q.JyN = a->JyN; q.h = a->h; q.Jh = a->Jh;
+    q.hE = a->hE; q.JhE = a->JhE;
     q.x = a->x; q.u = a->u; q.x0 = a->x0; q.yref = a->yref; q.W = a->W; q.yNref = a->yNref; q.WN = a->WN; q.dt = a->dt;
     q.dx = a->dx; q.du = a->du; q.slack = a->slack;
     double* stbuf = (double*)ctx->qpst.p;
@@ -1416,13 +1485,31 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
     q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling; q.ny = o->ny;
     q.lm_scaling = o->lm_scaling;
     q.warm_start = o->warm_start ? 1 : 0;
+    q.nh = o->nh; q.nhN = o->nhN; q.nsN = o->nsN; q.nyN = o->nyN;
+    q.sdf_row = -1;
+    for (int j = 0; j < 3; ++j) {
+        q.h_col[j] = j < o->nh ? o->h_col[j] : 0;
+        if (j < o->nh && o->h_col[j] == 2) q.sdf_row = j;
+        q.zlN[j] = o->zlN[j]; q.ZlN[j] = o->ZlN[j];
+    }
+    for (int j = 0; j < QP_NHN; ++j) {
+        q.hN_col[j] = j < o->nhN ? o->hN_col[j] : -1;
+        q.hE_col[j] = j < o->nhN ? o->hE_col[j] : -1;
+        q.lhN[j] = o->lhN[j]; q.uhN[j] = o->uhN[j];
+    }
     return SDFNMPC_OK;
+}
+
+// what the stage / terminal records depend on besides H, g: the stage rows' columns and the terminal residual width
+static long long cset_key(const QpArgs& q) {
+    return q.nh | (long long)q.h_col[0] << 4 | (long long)q.h_col[1] << 8 | (long long)q.h_col[2] << 12 |
+           (long long)q.nyN << 16;
 }
 
 // the IPM kernel of this context and horizon: the segmented one (four wavefronts per instance,
 // rti_qp_seg.hip) where it supports N, unless the context asks for the serial one (rti_qp.hip)
 static hipError_t qp_launch(sdfnmpc_ctx* ctx, const QpArgs& q) {
-    if (sdfnmpc_ctx_qp_kernel(ctx, q.N, q.B) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
+    if (qp_kernel_for(ctx, q.N, q.B, QpRows{q.nh, q.nhN, q.nsN}) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
     return launch_rti_qp(q, ctx->stream);
 }
 
@@ -1440,7 +1527,9 @@ extern "C" int sdfnmpc_qp_solve(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, cons
 
 extern "C" int sdfnmpc_rti_prepare(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
                                    const sdfnmpc_lin_args* la, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* qa) {
-    if (!ctx || !net || !mdl || !la || !o || !qa) return fail(SDFNMPC_E_ARG, "NULL argument");
+    if (!ctx || !mdl || !la || !o || !qa) return fail(SDFNMPC_E_ARG, "NULL argument");
+    if (la->no_sdf && qp_needs_sdf(o)) return fail(SDFNMPC_E_ARG, "rti_prepare: lin_args.no_sdf, but the QP reads the sdf");
+    if ((la->nyN == 0 ? 4 : la->nyN) != o->nyN) return fail(SDFNMPC_E_ARG, "rti_prepare: lin_args.nyN != qp opts nyN");
     ctx->prep.valid = false;
     if (la->B != qa->B || la->N != qa->N) return fail(SDFNMPC_E_ARG, "rti_prepare: lin and qp args differ in B / N");
     if (la->xn != qa->xn || la->AB != qa->AB || la->y != qa->y || la->Jy != qa->Jy || la->yN != qa->yN ||
@@ -1452,7 +1541,7 @@ extern "C" int sdfnmpc_rti_prepare(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, con
     if (int rc = qp_build(ctx, o, qa, q)) return rc;
     if (int rc = lin_impl(ctx, net, mdl, la, &q)) return rc;
     ctx->prep.valid = true;
-    ctx->prep.sdf_row_patch = q.ny == 11 && !ctx->serial_prep;  // lin_impl's split: records lack the sdf row
+    ctx->prep.sdf_row_patch = q.ny == 11 && !ctx->serial_prep && !la->no_sdf;  // lin_impl's split: no sdf row in the records
     ctx->prep.B = qa->B;
     ctx->prep.N = qa->N;
     ctx->prep.xn = qa->xn;
@@ -1461,6 +1550,7 @@ extern "C" int sdfnmpc_rti_prepare(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, con
     ctx->prep.lm = q.lm;
     ctx->prep.cost_scaling = q.cost_scaling;
     ctx->prep.lm_scaling = q.lm_scaling;
+    ctx->prep.cset = cset_key(q);
     return SDFNMPC_OK;
 }
 
@@ -1474,8 +1564,9 @@ extern "C" int sdfnmpc_qp_feedback(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, c
     if (int rc = qp_build(ctx, o, a, q)) return rc;
     if (q.work != ctx->prep.work) return fail(SDFNMPC_E_ARG, "qp_feedback: workspace moved since rti_prepare");
     if (q.ny != ctx->prep.ny || q.lm != ctx->prep.lm || q.cost_scaling != ctx->prep.cost_scaling ||
-        q.lm_scaling != ctx->prep.lm_scaling)  // the stage records hold H, g packed under the prepare's options
-        return fail(SDFNMPC_E_ARG, "qp_feedback: ny / lm / cost_scaling / lm_scaling differ from sdfnmpc_rti_prepare's");
+        q.lm_scaling != ctx->prep.lm_scaling || cset_key(q) != ctx->prep.cset)  // the stage records hold H, g, C^T
+        // packed under the prepare's options
+        return fail(SDFNMPC_E_ARG, "qp_feedback: ny / lm / cost scaling / the constraint set differ from sdfnmpc_rti_prepare's");
     ctx->prep.valid = false;  // one feedback per preparation, as in acados' SQP-RTI
     q.sdf_row_patch = ctx->prep.sdf_row_patch ? 1 : 0;
     HIPCHK(timed(ctx, "rti_qp", [&] { return qp_launch(ctx, q); }));
@@ -1497,6 +1588,8 @@ extern "C" int sdfnmpc_pack_refs(sdfnmpc_ctx* ctx, const sdfnmpc_ref_opts* o, co
     ScopedDevice sd(ctx->device);
     RefPackArgs r{};
     r.B = a->B; r.N = a->N; r.np_ = a->np; r.ny = a->ny; r.n_wp = a->n_wp; r.L = a->L;
+    r.nyN = a->nyN == 0 ? 4 : a->nyN;
+    if (r.nyN != 4 && r.nyN != 5) return fail(SDFNMPC_E_ARG, "pack_refs: nyN must be 4 or 5");
     r.mode = o->mode; r.yaw_mode = o->yaw_mode; r.st_enable = o->st_enable; r.st_mode = o->st_mode;
     r.st_dang = o->st_dang; r.align_off = o->align_off; r.dmin = o->dmin; r.vref = o->vref; r.wzref = o->wzref;
     r.T = o->T;

@@ -151,16 +151,71 @@ __global__ __launch_bounds__(256, LIN_WAVES) void linearize_kernel(LinArgs A) {
             if (t == i) A.y[s * 11 + i] = Y[i].v;
         }
     } else {
-        // ---- terminal residual y_N = [p, q_e[3]]
+        // ---- terminal residual y_N = [p, q_e[3]]; with flags.stability scaled by the flag, plus the
+        //      stability cost row flag |v|^2 (quad_rollpitchyawrate.py:52-55, gen_model.py:142-149)
         const double* pr = A.p + r * A.np;
         const dd qe3 = qerr3(X, pr + 13);
-        const dd Y[4] = {X[0], X[1], X[2], qe3};
+        const int nyN = A.nyN;
+        const double fl = m.stability ? pr[0] : 1.0;
+        const dd Y[5] = {X[0] * fl, X[1] * fl, X[2] * fl, qe3 * fl, ((X[7] * X[7] + X[8] * X[8]) + X[9] * X[9]) * pr[0]};
         if (t < 10) {
-            double* J = A.JyN + (b * 10 + t) * 4;
+            double* J = A.JyN + (b * 10 + t) * nyN;
 #pragma unroll
-            for (int i = 0; i < 4; ++i) J[i] = Y[i].t;
+            for (int i = 0; i < 5; ++i)
+                if (i < nyN) J[i] = Y[i].t;
         }
-        if (t < 4) A.yN[b * 4 + t] = Y[t].v;
+#pragma unroll
+        for (int i = 0; i < 5; ++i)
+            if (t == i && i < nyN) A.yN[b * nyN + i] = Y[i].v;
+        if (m.rec_feas | m.stability) {
+            // ---- terminal extras (gen_model.py:81-121): -flag poly(v), the fov functions at
+            //      Co_p_E = W_R_Co^T (p + poly(v) v / sqrt(|v|^2 + 1e-4) - W_p_Co) + B_R_C^T B_p_C + [off, 0, 0]
+            //      (braking_dist_flag with the flag forced to 1, gen_model.py:86-87,110), and v
+            dd H[6] = {C(0.0), C(0.0), C(0.0), X[7], X[8], X[9]};
+            if (m.rec_feas) {
+                const int deg = m.poly_deg;
+                dd pw[3][7];  // v_i^a, a <= 6
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    pw[i][0] = C(1.0);
+#pragma unroll
+                    for (int a = 1; a < 7; ++a) pw[i][a] = pw[i][a - 1] * X[7 + i];
+                }
+                dd poly = C(0.0);
+                int q = 0;  // polynomial_3variate's order (utils/math.py:307-314)
+                for (int d = 0; d <= deg; ++d)
+                    for (int a = 0; a <= d; ++a)
+                        for (int bb = 0; bb <= d - a; ++bb, ++q) {
+                            dd pa = C(1.0), pb = C(1.0), pc = C(1.0);
+#pragma unroll
+                            for (int e = 0; e < 7; ++e) {
+                                if (e == a) pa = pw[0][e];
+                                if (e == bb) pb = pw[1][e];
+                                if (e == d - a - bb) pc = pw[2][e];
+                            }
+                            poly = poly + ((pa * pb) * pc) * m.poly[q];
+                        }
+                H[0] = -(poly * pr[0]);
+                const dd nrm = dsqrt(((X[7] * X[7] + X[8] * X[8]) + X[9] * X[9]) + C(1e-4));
+                const dd sc = poly / nrm;
+                const double* R = pr + 4;
+                const dd e0 = (X[0] + X[7] * sc) - C(pr[1]), e1 = (X[1] + X[8] * sc) - C(pr[2]),
+                         e2 = (X[2] + X[9] * sc) - C(pr[3]);
+                const dd cx = (e0 * R[0] + e1 * R[3]) + e2 * R[6] + C(m.fov_off[0]);
+                const dd cy = (e0 * R[1] + e1 * R[4]) + e2 * R[7] + C(m.fov_off[1]);
+                const dd cz = (e0 * R[2] + e1 * R[5]) + e2 * R[8] + C(m.fov_off[2]);
+                H[1] = datan2(cy, cx) * pr[0];
+                H[2] = datan2(cz, dsqrt(cx * cx + cy * cy)) * pr[0];
+            }
+            if (t < 10) {
+                double* J = A.JhE + (b * 10 + t) * 6;
+#pragma unroll
+                for (int i = 0; i < 6; ++i) J[i] = H[i].t;
+            }
+#pragma unroll
+            for (int i = 0; i < 6; ++i)
+                if (t == i) A.hE[b * 6 + i] = H[i].v;
+        }
     }
 
     // ---- constraints h = [hfov, vfov, sdf] (cost_const_helpers.py:48-75, gen_model.py:46-61)

@@ -9,6 +9,7 @@ constexpr int RP_MAX_WP = 32;  // waypoints per instance
 
 struct RefPackArgs {
     int B, N, np_, ny, n_wp, L;
+    int nyN;  // terminal residual rows (4, or 5 with flags.stability)
     int mode;                      // 0 gen_ref_list_wps, 1 gen_ref_joystick, 2 from_x0, -1 latent / flag only
     int yaw_mode;                  // path samples: 0 identity, 1 'ref', 2 'align', 3 x0 quaternion ('curent')
     int st_enable, st_mode;        // stop-and-turn; st_mode 0 current yaw, 1 'topic', 2 'align'

@@ -206,9 +206,9 @@ __global__ __launch_bounds__(64) void ref_pack_kernel(RefPackArgs A) {
                 wk[i] = A.wrow[i];
             }
         } else {
-            for (int i = 0; i < 4; ++i) {
-                A.yNref[(size_t)b * 4 + i] = yr[i];
-                A.WN[(size_t)b * 4 + i] = A.wrow[i];
+            for (int i = 0; i < A.nyN; ++i) {  // yN = y[:nyN], WN = W[:nyN] (controller.py:141-142)
+                A.yNref[(size_t)b * A.nyN + i] = yr[i];
+                A.WN[(size_t)b * A.nyN + i] = A.wrow[i];
             }
         }
     }

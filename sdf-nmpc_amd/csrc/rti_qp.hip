@@ -84,29 +84,35 @@ struct Smem {
     ldsd *t, *lam;                 // [m] inequality slacks / duals
     ldsd *dx, *dxc;                // iterate dx; sweep solution (x of predictor, then corrector)
     ldsd *du, *dua, *duc;          // iterate du; affine / corrector du
-    ldsd *cxa, *cxc;               // C dx of the affine / corrector solution
+    ldsd *cxa, *cxc;               // C dx of the affine / corrector solution, per group
     ldsd* win;                     // committed stream window
     ldsd* fsave;                   // [A~|b~ K|k_ff] of nodes < PD
     ldsd *zero, *junk;             // 48 doubles that stay 0 (zero rows for strided reads); a store sink
-    ldsd *uu, *hv, *skv;           // u (box constants), h, cost scaling per node
-    ldsd *fw, *fg, *bd, *bv;       // soft folds [N+1][3] (w, gamma), box terms [N][4] (diag, v)
-    ldsd* cst;                     // lbu 4 | ubu 4 | lh 3 | uh 3 | zl 3 | Zl 3 (lane-indexed kernel arguments
-                                   // would be vector loads that wait behind the record stream)
+    ldsd *uu, *hv, *skv;           // u (box constants), h per group, cost scaling per node
+    ldsd *fw, *fg, *bd, *bv;       // folds per group (w, gamma), box terms [N][4] (diag, v)
+    ldsd* cst;                     // lbu 4 | ubu 4 | (lh, uh, zl, Zl) of stage rows 0..2 | of terminal rows 0..7
+                                   // (lane-indexed kernel arguments would be vector loads that wait behind the
+                                   // record stream)
+    ldsd* ctN;                     // terminal C rows [nhN][10]
 };
+constexpr int CST_ROW = 8, CST_TERM = 8 + 4 * 3;  // group constants: stage row j at CST_ROW + 4 j, terminal CST_TERM + 4 j
 
-__device__ __forceinline__ Smem carve(ldsd* q, int N) {  // mirrors qp_lds_doubles()
+// groups: e < N NSS are stage groups (node e / NSS, row e % NSS); then the nhN terminal rows (soft first)
+template <int NSS>
+__device__ __forceinline__ Smem carve(ldsd* q, int N, QpRows rw) {  // mirrors qp_lds_doubles()
     Smem s;
     auto take = [&](int n) { ldsd* r = q; q += (n + 1) & ~1; return r; };
-    const int m = 8 * N + 12 * (N + 1), N1 = N + 1;
+    const int m = rw.rows(N), N1 = N + 1, G = rw.groups(N);
     s.t = take(m); s.lam = take(m);
     s.dx = take(N1 * NX); s.dxc = take(N1 * NX);
     s.du = take(N * NU); s.dua = take(N * NU); s.duc = take(N * NU);
-    s.cxa = take(N1 * NS); s.cxc = take(N1 * NS);
+    s.cxa = take(G); s.cxc = take(G);
     s.win = take(SLOT * 64); s.fsave = take(PD * F_FW);
     s.zero = take(48); s.junk = take(2);
-    s.uu = take(N * NU); s.hv = take(N1 * NS); s.skv = take(N1);
-    s.fw = take(N1 * NS); s.fg = take(N1 * NS); s.bd = take(N * NU); s.bv = take(N * NU);
-    s.cst = take(20);
+    s.uu = take(N * NU); s.hv = take(G); s.skv = take(N1);
+    s.fw = take(G); s.fg = take(G); s.bd = take(N * NU); s.bv = take(N * NU);
+    s.cst = take(8 + 4 * (3 + QP_NHN));
+    s.ctN = take(rw.nhN * 10);
     return s;
 }
 
@@ -121,6 +127,7 @@ struct FConst {
     unsigned spc[3], sab[3], sk_;
 };
 
+template <int NSS>
 __device__ __forceinline__ FConst fconst(int lane) {
     FConst f;
     const int g = lane >> 4, c = lane & 15;
@@ -135,8 +142,8 @@ __device__ __forceinline__ FConst fconst(int lane) {
         f.h_i[r] = opaque((a < 14 && c < 14) ? R_H + tri14(lo, hi) : (a < 14 && c == 14) ? R_G + a : R_Z);
     }
     // fold operands: A = C[c][g] (g < 3), B = w_g C[c][g] (c < 10) | gamma_g (c = 14)
-    f.cgi = opaque((c < NX && g < NS) ? R_CT + g * 10 + c : R_Z);
-    f.gj = g < NS ? g : 0;
+    f.cgi = opaque((c < NX && g < NSS) ? R_CT + g * 10 + c : R_Z);
+    f.gj = g < NSS ? g : 0;
     // closed loop: [A | c][a][c] at ab01 + 4 r (r = 0, 1), ab2; A operand B[a = c][g] at bmi
     const bool xcol = c < NX || c == 14;  // columns of [P | p], [A | c], [K | k_ff]
     const int xo = c < NX ? c : 10;       // their column in the 11-wide factor-record rows
@@ -207,7 +214,13 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
         const int g = lane >> 4, c = lane & 15;
         // sdf cost (gen_model.py:65-66); h[2] is read only then (pack_part 1 runs beside the SDF kernel)
         const double ts = ny > 11 ? 1.0 - 0.5 * A.h[((size_t)b * N1 + k) * 3 + 2] : 0.0;
-        const int nct = A.pack_part == 1 ? 20 : 30;  // C^T entries written here (rows j < 2 | all)
+        // C^T row j = J_h column h_col[j] (j < nh; zero rows past it); with pack_part 1 the sdf row is left to
+        // rti_qp_kernel (sdf_row_patch)
+        const int skip_row = A.pack_part == 1 ? A.sdf_row : -1;
+        auto ct_val = [&](int q) -> double {  // C^T entry q = 10 j + l
+            const int j = q / 10;
+            return j < A.nh ? Jh[(q - 10 * j) * 3 + A.h_col[j < 3 ? j : 0]] : 0.0;
+        };
         d4 D = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
         for (int st = 0; st < 3; ++st) {
@@ -232,15 +245,13 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
             const int e = 128 + lane;
             if (e < R_C) Rk[e] = AB[e];
             else if (e < R_G) Rk[e] = xn[e - R_C] - xb1[e - R_C];
-            else if (e >= R_CT && e < R_CT + nct) {
-                const int q = e - R_CT, j = q / 10;
-                Rk[e] = Jh[(q - 10 * j) * 3 + j];
+            else if (e >= R_CT && (e - R_CT) / 10 != skip_row) {
+                Rk[e] = ct_val(e - R_CT);
             }
         }
         for (int e = 192 + lane; e < REC; e += 64) {
             if (e < R_H) {
-                const int q = e - R_CT, j = q / 10;
-                if (q < nct) Rk[e] = Jh[(q - 10 * j) * 3 + j];
+                if ((e - R_CT) / 10 != skip_row) Rk[e] = ct_val(e - R_CT);
             } else if (e >= R_H + 105) {
                 Rk[e] = 0.0;
             }
@@ -253,24 +264,39 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
             else if (a < 14 && c == 14) Rk[R_G + a] = D[q];
         }
     } else {
-        const double* J = A.JyN + (size_t)b * 40;  // [10][4]
-        const double* Wn = A.WN + (size_t)b * 4;
-        const double* yn = A.yN + (size_t)b * 4;
-        const double* rn = A.yNref + (size_t)b * 4;
-        const int nct = A.pack_part == 1 ? 20 : 30;
+        // terminal record: H_N = J_N^T W_N J_N + lm I, g_N, and C^T of terminal rows 0..2 (rti_qp_seg.hip reads
+        // them; rti_qp_kernel assembles every terminal row from J_h / J_hE itself); with pack_part 1 a row that
+        // reads the sdf column is left to the QP kernel's sdf_row_patch
+        const int nyN = A.nyN;
+        auto ctN_val = [&](int q, bool& skip) -> double {
+            const int j = q / 10, l = q - 10 * j;
+            int c1 = -1, c2 = -1;
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if (i == j && i < A.nhN) { c1 = A.hN_col[i]; c2 = A.hE_col[i]; }
+            double v = 0.0;
+            if (c1 >= 0) v += Jh[l * 3 + c1];
+            if (c2 >= 0) v += A.JhE[((size_t)b * 10 + l) * 6 + c2];
+            skip = A.pack_part == 1 && c1 == 2;
+            return v;
+        };
+        const double* J = A.JyN + (size_t)b * 10 * nyN;  // [10][nyN]
+        const double* Wn = A.WN + (size_t)b * nyN;
+        const double* yn = A.yN + (size_t)b * nyN;
+        const double* rn = A.yNref + (size_t)b * nyN;
         for (int e = lane; e < REC; e += 64) {
-            if (e >= R_CT + nct && e < R_H) continue;  // the sdf row: rti_qp_kernel copies it (sdf_row_patch)
             double v = 0.0;
             if (e >= R_G && e < R_G + 10) {
                 const int a = e - R_G;
-                for (int i = 0; i < 4; ++i) v += J[a * 4 + i] * Wn[i] * (yn[i] - rn[i]);
-            } else if (e >= R_CT && e < R_H) {
-                const int q = e - R_CT, j = q / 10;
-                v = Jh[(q - 10 * j) * 3 + j];
+                for (int i = 0; i < nyN; ++i) v += J[a * nyN + i] * Wn[i] * (yn[i] - rn[i]);
             } else if (e >= R_H && e < R_H + 55) {
                 const int a = c_tri.a10[e - R_H], c = c_tri.c10[e - R_H];
-                for (int i = 0; i < 4; ++i) v += J[a * 4 + i] * Wn[i] * J[c * 4 + i];
+                for (int i = 0; i < nyN; ++i) v += J[a * nyN + i] * Wn[i] * J[c * nyN + i];
                 v += (a == c ? A.lm : 0.0);
+            } else if (e >= R_CT && e < R_H) {
+                bool skip = false;
+                v = ctN_val(e - R_CT, skip);
+                if (skip) continue;
             }
             Rk[e] = v;
         }
@@ -301,12 +327,29 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
 #ifndef QP_LB_WAVES  // diagnostic: minimum waves per SIMD the register allocation must allow
 #define QP_LB_WAVES 1
 #endif
+template <int NSS, bool HARD>  // stage soft rows (0..3); hard terminal rows present (rec_feas / stability)
 __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     extern __shared__ __align__(16) double lds_q[];
     STAMP_DECL
+    constexpr int NS = NSS;  // this kernel's stage rows (shadows qpd::NS, the width of the h / J_h arrays)
     const int b = blockIdx.x, lane = threadIdx.x;
-    const int N = A.N, N1 = N + 1, m = 8 * N + 12 * N1;
-    const Smem s = carve((ldsd*)lds_q, N);
+    const int N = A.N, N1 = N + 1;
+    const QpRows rw{NSS, A.nhN, A.nsN};
+    const int m = rw.rows(N);
+    const int NGS = N * NSS;          // stage groups
+    const int NG1 = NGS + A.nsN;      // soft groups (stage, then terminal)
+    const int NHH = HARD ? A.nhN - A.nsN : 0;  // hard terminal rows: rows RH0 + 2 i (lower), + 1 (upper); group NG1 + i
+    const int RH0 = 8 * N + 4 * NG1;
+    const int nhN = A.nhN;
+    const Smem s = carve<NSS>((ldsd*)lds_q, N, rw);
+    // node and row of soft group e (stage groups first, then the terminal's)
+    auto gnode = [&](int e) -> int {
+        if constexpr (NSS == 0) return N;
+        else return e < NGS ? e / NSS : N;
+    };
+    auto gcst = [&](int e) -> const ldsd* {  // (lh, uh, zl, Zl) of group e
+        return e < NGS ? s.cst + CST_ROW + 4 * (e - gnode(e) * NSS) : s.cst + CST_TERM + 4 * (e - NGS);
+    };
     ldsd* const win = s.win;
     const double* R = A.work + (size_t)b * qp_work_doubles(N);  // [N+1][REC] stage records
     double* F = A.work + (size_t)b * qp_work_doubles(N) + (size_t)N1 * REC;  // [N+1][FREC]
@@ -326,7 +369,33 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         if (__builtin_amdgcn_ballot_w64(!fin) != 0)
             for (int e = lane; e < N * NU; e += 64) s.du[e] = 0.0;
     }
-    for (int e = lane; e < N1 * NS; e += 64) s.hv[e] = A.h[(size_t)b * N1 * NS + e];
+    // h per group: stage group (k, j) = h[k][h_col[j]]; terminal row j = h[N][hN_col[j]] + hE[hE_col[j]]
+    {
+        int hc[3];
+#pragma unroll
+        for (int j = 0; j < 3; ++j) hc[j] = A.h_col[j];
+        for (int e = lane; e < NGS; e += 64) {
+            const int k = gnode(e), j = e - k * NSS;
+            s.hv[e] = A.h[((size_t)b * N1 + k) * 3 + (j == 0 ? hc[0] : j == 1 ? hc[1] : hc[2])];
+        }
+    }
+    {
+        // terminal rows: values and C rows (lane 10 j + l: row j, entry l), sums of an h[N] and an hE column
+        const double* hN = A.h + ((size_t)b * N1 + N) * 3;
+        const double* JhN = A.Jh + ((size_t)b * N1 + N) * 30;
+        for (int e = lane; e < nhN * 10; e += 64) {
+            const int j = e / 10, l = e - 10 * j;
+            int c1 = -1, c2 = -1;
+#pragma unroll
+            for (int q = 0; q < QP_NHN; ++q)
+                if (q == j) { c1 = A.hN_col[q]; c2 = A.hE_col[q]; }
+            double v = 0.0, cv = 0.0;
+            if (c1 >= 0) { v += hN[c1]; cv += JhN[l * 3 + c1]; }
+            if (c2 >= 0) { v += A.hE[(size_t)b * 6 + c2]; cv += A.JhE[((size_t)b * 10 + l) * 6 + c2]; }
+            s.ctN[e] = cv;
+            if (l == 0) s.hv[NGS + j] = v;
+        }
+    }
     {
         double v = 0.0;  // constant indices: scalar loads of the kernel arguments
 #pragma unroll
@@ -336,19 +405,27 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         }
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            if (lane == 8 + j) v = A.lh[j];
-            if (lane == 11 + j) v = A.uh[j];
-            if (lane == 14 + j) v = A.zl[j];
-            if (lane == 17 + j) v = A.Zl[j];
+            if (lane == CST_ROW + 4 * j) v = A.lh[j];
+            if (lane == CST_ROW + 4 * j + 1) v = A.uh[j];
+            if (lane == CST_ROW + 4 * j + 2) v = A.zl[j];
+            if (lane == CST_ROW + 4 * j + 3) v = A.Zl[j];
         }
-        if (lane < 20) s.cst[lane] = v;
+#pragma unroll
+        for (int j = 0; j < QP_NHN; ++j) {
+            if (lane == CST_TERM + 4 * j) v = A.lhN[j];
+            if (lane == CST_TERM + 4 * j + 1) v = A.uhN[j];
+            if (lane == CST_TERM + 4 * j + 2) v = j < 3 ? A.zlN[j < 3 ? j : 0] : 0.0;
+            if (lane == CST_TERM + 4 * j + 3) v = j < 3 ? A.ZlN[j < 3 ? j : 0] : 0.0;
+        }
+        if (lane < CST_TERM + 4 * QP_NHN) s.cst[lane] = v;
     }
     for (int e = lane; e < N1; e += 64) s.skv[e] = (A.cost_scaling && e < N) ? A.dt[e] : 1.0;
-    if (A.sdf_row_patch) {  // records packed beside the SDF kernel (pack_part 1): their sdf row of C^T
+    if (A.sdf_row_patch && A.sdf_row >= 0) {  // records packed beside the SDF kernel (pack_part 1): their sdf row of C^T
         double* Rw = A.work + (size_t)b * qp_work_doubles(N);
-        for (int e = lane; e < N1 * NX; e += 64) {
+        const int ro = R_CT + 10 * A.sdf_row;
+        for (int e = lane; e < N * NX; e += 64) {
             const int k = e / NX, l = e - k * NX;
-            Rw[(size_t)k * REC + R_CT + 20 + l] = A.Jh[((size_t)b * N1 + k) * 30 + l * 3 + 2];
+            Rw[(size_t)k * REC + ro + l] = A.Jh[((size_t)b * N1 + k) * 30 + l * 3 + 2];
         }
         __threadfence_block();  // stored before any lane of the wave streams the records
     }
@@ -398,7 +475,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     // Factor rows of nodes < PD come from fsave (written late in the backward sweeps).
     double chain = 0.0;  // p_{k+1} of the corrector sweep in lanes 0..9
     auto fw_stage = [&](auto Kc, int k, const int lane) {
-        const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 17;
+        const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 14 + NS;
         const int fcj = fc ? lane - 14 : 0;
         constexpr int K = decltype(Kc)::value;
         ldsd* const dxo = K == 0 ? s.dx : s.dxc;
@@ -440,10 +517,28 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             a1 = fma(row[2 * l + 1], xv[l].y, a1);
         }
         const double z = a0 + a1;
-        ldsd* dst = fc ? cxo + k * NS + fcj
+        // the terminal node's rows are formed after the sweep (term_cx): any row set, C rows from LDS
+        ldsd* dst = (fc && k < N) ? cxo + k * NS + fcj
                   : (k < N && fx) ? dxo + (k + 1) * NX + lane
                   : (K != 0 && k < N && fu) ? duo + k * NU + lane - NX : s.junk;
         *dst = z;
+    };
+
+    // C dx_N of the terminal rows into cxo[NGS + j] (after a forward sweep): lane j < nhN, the fw_stage's
+    // two-chain order (even / odd entries)
+    auto term_cx = [&](ldsd* cxo, const ldsd* dxv) {
+        if (lane < nhN) {
+            const ldsd* cr = s.ctN + 10 * lane;
+            const ldsd* xr = dxv + N * NX;
+            double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+            for (int l = 0; l < NX / 2; ++l) {
+                a0 = fma(cr[2 * l], xr[2 * l], a0);
+                a1 = fma(cr[2 * l + 1], xr[2 * l + 1], a1);
+            }
+            cxo[NGS + lane] = a0 + a1;
+        }
+        wave_sync();
     };
 
     // ------------------------------------------------------------ backward stage, factor
@@ -469,7 +564,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             sab[r] = f.sab[r];
         }
         const unsigned sk_ = f.sk_;
-        const double m14 = c == 14 ? 1.0 : 0.0, mg3 = g < NS ? 1.0 : 0.0;
+        const double m14 = c == 14 ? 1.0 : 0.0, mg3 = g < NS ? 1.0 : 0.0;  // fold lanes: stage rows g < NS
         double bxm[2], bvm[2], mg[4];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
@@ -485,18 +580,25 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         const double v0_bd = c == NX + g ? 1.0 : 0.0, v0_bv = c == 14 ? 1.0 : 0.0;
 
         const int k = N - q;
-        const double cg = win[cgi];
-        const double fb = mg3 * fma(s.fw[k * NS + gj], cg, m14 * s.fg[k * NS + gj]);
-        if constexpr (FIRST) {  // [P_N | p_N] = [H_N | g_N] + fold
+        if constexpr (FIRST) {  // [P_N | p_N] = [H_N | g_N] + fold of the terminal rows (C from LDS, K = 4 per MFMA)
             d4 T;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int a = g + 4 * r, lo = a < c ? a : c, hi = a < c ? c : a;
                 T[r] = win[(a < NX && c < NX) ? R_H + tri10(lo, hi) : (a < NX && c == 14) ? R_G + a : R_Z];
             }
-            Pa = mfma(cg, fb, T);
+            Pa = T;
+            for (int t0 = 0; t0 < nhN; t0 += 4) {
+                const int jr = t0 + g;
+                const bool live = jr < nhN;
+                const double cg = (live && c < NX) ? s.ctN[10 * (live ? jr : 0) + (c < NX ? c : 0)] : 0.0;
+                const double fb = live ? fma(s.fw[NGS + jr], cg, m14 * s.fg[NGS + jr]) : 0.0;
+                Pa = mfma(cg, fb, Pa);
+            }
             return;
         }
+        const double cg = win[cgi];
+        const double fb = mg3 * fma(s.fw[k * NS + gj], cg, m14 * s.fg[k * NS + gj]);
         const unsigned sko = (unsigned)k * (FREC * 8u);
         FSTAMP(8, Pa[0]);
         // ---- W = P G (K = 10: k-steps 0..2); column 14 -> P c, then + p
@@ -615,12 +717,14 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         const int k = N - q;
         FSTAMP(7, mfx);
         double off = *bc_g;
-#pragma unroll
-        for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * bc_ct[10 * j];
-        if constexpr (FIRST) {  // p_N = g_N + sum_j gamma_j C_j^T
+        if constexpr (FIRST) {  // p_N = g_N + sum_j gamma_j C_j^T over the terminal rows (C from LDS)
+            const ldsd* ct = fx ? s.ctN + lane : s.zero;
+            for (int j = 0; j < nhN; ++j) off += s.fg[NGS + j] * ct[fx ? 10 * j : 0];
             chain = off;
             return;
         }
+#pragma unroll
+        for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * bc_ct[10 * j];
         // ---- every LDS read of the stage first (one round trip), the chain input p_{k+1} last
         double bvv[NU], guw[NU], kk[NU], row[NX];
         {  // the uniform box and g~_u terms as 16-byte reads (both blocks are 16-byte aligned)
@@ -685,55 +789,66 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     // (sweep 0), then the rows
     auto rows_init = [&]() -> double {
     double rp = 0.0;
-    for (int r = lane; r < m; r += 64) {
+    for (int r = lane; r < RH0; r += 64) {
         double v, l0 = L0;
         if (r < 8 * N) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
             v = box_d(k, i, up) + (up ? -s.du[k * NU + i] : s.du[k * NU + i]);
         } else {
-            const int q = r - 8 * N, k = q / 12, w = q - 12 * k, j = w >> 2, kind = w & 3;
-            const double h = s.hv[k * 3 + j];
-            v = kind == 0 ? s.cxa[k * NS + j] + (h - s.cst[8 + j]) : kind == 1 ? -s.cxa[k * NS + j] + (s.cst[11 + j] - h) : 0.0;
-            l0 = fmax(L0, LC * s.skv[k] * s.cst[14 + j]);
+            const int e = (r - 8 * N) >> 2, kind = (r - 8 * N) & 3, k = gnode(e);
+            const ldsd* gc = gcst(e);
+            const double h = s.hv[e];
+            v = kind == 0 ? s.cxa[e] + (h - gc[0]) : kind == 1 ? -s.cxa[e] + (gc[1] - h) : 0.0;
+            l0 = fmax(L0, LC * s.skv[k] * gc[2]);
         }
         const double t = fmax(v, T0);
         s.t[r] = t;
         s.lam[r] = l0;
         rp = fmax(rp, fabs(v - t));
     }
+    if constexpr (HARD) for (int r = RH0 + lane; r < m; r += 64) {  // hard terminal rows: lower, upper
+        const int i = (r - RH0) >> 1, up = (r - RH0) & 1, e = NG1 + i;
+        const ldsd* gc = gcst(e);
+        const double v = up ? -s.cxa[e] + (gc[1] - s.hv[e]) : s.cxa[e] + (s.hv[e] - gc[0]);
+        const double t = fmax(v, T0);
+        s.t[r] = t;
+        s.lam[r] = L0;
+        rp = fmax(rp, fabs(v - t));
+    }
     return wmax(rp);
     };
 
-    // soft group (k, j) = rows (hl, hu, sl, su): barrier weights, v's, eliminated slack block.
+    // soft group e = rows (hl, hu, sl, su): barrier weights, v's, eliminated slack block.
     // Divisions are reciprocal multiplications (rcp_nr: v_rcp_f64 + two Newton steps), one per
     // denominator.
     struct Grp {
         double s1, s2, s3, s4, v1, v2, v3, v4, Hl, Hu, iHl, iHu, gl, gu;
     };
-    auto group = [&](int k, int j, int phase, double sigmu) -> Grp {
+    auto group = [&](int e, int phase, double sigmu) -> Grp {
         Grp g;
-        const int r0 = 8 * N + 12 * k + 4 * j;
-        const double sk = s.skv[k];
+        const int r0 = 8 * N + 4 * e;
+        const double sk = s.skv[gnode(e)];
+        const ldsd* gc = gcst(e);
         const double t1 = s.t[r0], t2 = s.t[r0 + 1], t3 = s.t[r0 + 2], t4 = s.t[r0 + 3];
         const double l1 = s.lam[r0], l2 = s.lam[r0 + 1], l3 = s.lam[r0 + 2], l4 = s.lam[r0 + 3];
         const double it1 = rcp_nr(t1), it2 = rcp_nr(t2), it3 = rcp_nr(t3), it4 = rcp_nr(t4);
         g.s1 = l1 * it1; g.s3 = l2 * it2; g.s2 = l3 * it3; g.s4 = l4 * it4;
-        const double h = s.hv[k * 3 + j];
-        g.v1 = g.s1 * (t1 - (h - s.cst[8 + j]));
-        g.v3 = g.s3 * (t2 - (s.cst[11 + j] - h));
+        const double h = s.hv[e];
+        g.v1 = g.s1 * (t1 - (h - gc[0]));
+        g.v3 = g.s3 * (t2 - (gc[1] - h));
         g.v2 = g.s2 * t3;
         g.v4 = g.s4 * t4;
-        const double Zs = sk * s.cst[17 + j], zs = sk * s.cst[14 + j];
+        const double Zs = sk * gc[3], zs = sk * gc[2];
         g.Hl = Zs + g.s1 + g.s2;
         g.Hu = Zs + g.s3 + g.s4;
         g.iHl = rcp_nr(g.Hl);
         g.iHu = rcp_nr(g.Hu);
         if (phase) {  // corrector: affine deltas of the four rows, recomputed from the affine solution
-            const double cxa = s.cxa[k * NS + j];
+            const double cxa = s.cxa[e];
             const double sla = -((zs - g.v1 - g.v2) + g.s1 * cxa) * g.iHl;
             const double sua = -((zs - g.v3 - g.v4) - g.s3 * cxa) * g.iHu;
-            const double d1 = cxa + (h - s.cst[8 + j]) + sla - t1;
-            const double d2 = -cxa + (s.cst[11 + j] - h) + sua - t2;
+            const double d1 = cxa + (h - gc[0]) + sla - t1;
+            const double d2 = -cxa + (gc[1] - h) + sua - t2;
             const double d3 = sla - t3, d4 = sua - t4;
             g.v1 -= (d1 * (-g.s1 * d1 - l1) - sigmu) * it1;
             g.v3 -= (d2 * (-g.s3 * d2 - l2) - sigmu) * it2;
@@ -754,16 +869,39 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         }
         return v;
     };
-    // all nodes at once, before a backward sweep: fw = w_j (factor only), fg = gamma_j, box diag / v
+    // hard terminal row i, side up: the constant d of t = +-C dx + d, and the value at C dx = cxs
+    auto hard_d = [&](int i, int up) -> double {
+        const int e = NG1 + i;
+        const ldsd* gc = gcst(e);
+        return up ? gc[1] - s.hv[e] : s.hv[e] - gc[0];
+    };
+    auto hard_v = [&](int i, int up, int phase, double sigmu) -> double {  // box_v of a hard row
+        const int r = RH0 + 2 * i + up;
+        const double t = s.t[r], l = s.lam[r], it = rcp_nr(t), sg = l * it, d = hard_d(i, up);
+        double v = sg * (t - d);
+        if (phase) {
+            const double cxa = s.cxa[NG1 + i];
+            const double da = (up ? -cxa : cxa) + d - t;
+            v -= (da * (-sg * da - l) - sigmu) * it;
+        }
+        return v;
+    };
+    // all groups at once, before a backward sweep: fw = w (factor only), fg = gamma, box diag / v
     auto terms = [&](int phase, double sigmu) {
-        for (int e = lane; e < N1 * NS; e += 64) {
-            const int k = e / NS, j = e - NS * k;
-            const Grp g = group(k, j, phase, sigmu);
+        for (int e = lane; e < NG1; e += 64) {
+            const Grp g = group(e, phase, sigmu);
             // fold of the eliminated slack pair, written without the cancellation of H - s1 (H = Zs + s1 + s2
             // with s1 -> inf on an active row):  w = s1 (Zs + s2) / Hl + ...,  gamma = -(v1 + s1 gl / Hl) + ...
-            const double Zs = s.skv[k] * s.cst[17 + j], zs = s.skv[k] * s.cst[14 + j];
+            const ldsd* gc = gcst(e);
+            const double sk = s.skv[gnode(e)];
+            const double Zs = sk * gc[3], zs = sk * gc[2];
             if (!phase) s.fw[e] = g.s1 * (Zs + g.s2) * g.iHl + g.s3 * (Zs + g.s4) * g.iHu;
             s.fg[e] = -(g.v1 * (Zs + g.s2) + g.s1 * (zs - g.v2)) * g.iHl + (g.v3 * (Zs + g.s4) + g.s3 * (zs - g.v4)) * g.iHu;
+        }
+        if (HARD && lane < NHH) {  // hard rows fold like box rows: w = sigma_l + sigma_u, gamma = -v_l + v_u
+            const int r = RH0 + 2 * lane;
+            if (!phase) s.fw[NG1 + lane] = s.lam[r] * rcp_nr(s.t[r]) + s.lam[r + 1] * rcp_nr(s.t[r + 1]);
+            s.fg[NG1 + lane] = -hard_v(lane, 0, phase, sigmu) + hard_v(lane, 1, phase, sigmu);
         }
         for (int e = lane; e < N * NU; e += 64) {
             const int k = e >> 2, i = e & 3;
@@ -774,12 +912,13 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     };
 
 
-    // row values of a soft group (k, j) at an LQR solution with C dx = cxs, and its slacks
-    auto soft_vals = [&](const Grp& g, int k, int j, double cxs, double* v) {
-        const double h = s.hv[k * 3 + j];
+    // row values of soft group e at an LQR solution with C dx = cxs, and its slacks
+    auto soft_vals = [&](const Grp& g, int e, double cxs, double* v) {
+        const double h = s.hv[e];
+        const ldsd* gc = gcst(e);
         const double sl = -(g.gl + g.s1 * cxs) * g.iHl, su = -(g.gu - g.s3 * cxs) * g.iHu;
-        v[0] = cxs + (h - s.cst[8 + j]) + sl;
-        v[1] = -cxs + (s.cst[11 + j] - h) + su;
+        v[0] = cxs + (h - gc[0]) + sl;
+        v[1] = -cxs + (gc[1] - h) + su;
         v[2] = sl;
         v[3] = su;
     };
@@ -806,12 +945,25 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             const double dt = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
             bound(t, l, dt, -(l * rcp_nr(t)) * dt - l);
         }
+        // hard rows (lane 2 i + up)
+        auto hard_dir = [&](int r, double& dt, double& dl) {
+            const int i = (r - RH0) >> 1, up = (r - RH0) & 1;
+            const double t = s.t[r], l = s.lam[r], cxa = s.cxa[NG1 + i];
+            dt = (up ? -cxa : cxa) + hard_d(i, up) - t;
+            dl = -(l * rcp_nr(t)) * dt - l;
+        };
+        if constexpr (HARD)
+            for (int r = RH0 + lane; r < m; r += 64) {
+                double dt, dl;
+                hard_dir(r, dt, dl);
+                bound(s.t[r], s.lam[r], dt, dl);
+            }
         // affine direction of the four rows of soft group e: dt = val(z_a) - t, dl = -(lambda / t) dt - lambda
         auto soft_dir = [&](int e, double* dt, double* dl) {
-            const int k = e / NS, j = e % NS, r0 = 8 * N + 4 * e;
-            const Grp g = group(k, j, 0, 0.0);
+            const int r0 = 8 * N + 4 * e;
+            const Grp g = group(e, 0, 0.0);
             double v[4];
-            soft_vals(g, k, j, s.cxa[e], v);
+            soft_vals(g, e, s.cxa[e], v);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q];
@@ -824,14 +976,14 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
             for (int gi = 0; gi < GPL; ++gi) {
                 const int e = lane + 64 * gi;
-                if (e < N1 * NS) {
+                if (e < NG1) {
                     soft_dir(e, sdt[gi], sdl[gi]);
 #pragma unroll
                     for (int q = 0; q < 4; ++q) bound(s.t[8 * N + 4 * e + q], s.lam[8 * N + 4 * e + q], sdt[gi][q], sdl[gi][q]);
                 }
             }
         } else {
-            for (int e = lane; e < N1 * NS; e += 64) {
+            for (int e = lane; e < NG1; e += 64) {
                 soft_dir(e, sdt[0], sdl[0]);
 #pragma unroll
                 for (int q = 0; q < 4; ++q) bound(s.t[8 * N + 4 * e + q], s.lam[8 * N + 4 * e + q], sdt[0][q], sdl[0][q]);
@@ -845,6 +997,12 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             const double dt = (up ? -s.dua[k * NU + i] : s.dua[k * NU + i]) + box_d(k, i, up) - t;
             lmua += (t + aa * dt) * (l + aa * (-(l * rcp_nr(t)) * dt - l));
         }
+        if constexpr (HARD)
+            for (int r = RH0 + lane; r < m; r += 64) {
+                double dt, dl;
+                hard_dir(r, dt, dl);
+                lmua += (s.t[r] + aa * dt) * (s.lam[r] + aa * dl);
+            }
         auto soft_mu = [&](int e, const double* dt, const double* dl) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
@@ -856,10 +1014,10 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
             for (int gi = 0; gi < GPL; ++gi) {
                 const int e = lane + 64 * gi;
-                if (e < N1 * NS) soft_mu(e, sdt[gi], sdl[gi]);
+                if (e < NG1) soft_mu(e, sdt[gi], sdl[gi]);
             }
         } else {
-            for (int e = lane; e < N1 * NS; e += 64) {
+            for (int e = lane; e < NG1; e += 64) {
                 double dt[4], dl[4];
                 soft_dir(e, dt, dl);
                 soft_mu(e, dt, dl);
@@ -871,15 +1029,15 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         // the stop test needs, which keeps lambda / t -- and the Riccati data -- bounded
         return fmax(sig * mu, 1e-2 * A.tol);
     };
+    const int gpl = (NG1 + 63) / 64;
     auto rows_pred = [&]() -> double {
-        const int gp = (N1 * NS + 63) / 64;
-        if (gp == 1) return rows_pred_t(IC<1>{});
-        if (gp == 2) return rows_pred_t(IC<2>{});
-        if (gp == 3) return rows_pred_t(IC<3>{});
+        if (gpl == 1) return rows_pred_t(IC<1>{});
+        if (gpl == 2) return rows_pred_t(IC<2>{});
+        if (gpl == 3) return rows_pred_t(IC<3>{});
         return rows_pred_t(IC<0>{});
     };
     // corrector rows: step length, update of (t, lambda, du, dx), mu and the primal residual.
-    // GPL > 0: every lane owns at most GPL soft groups (3 (N+1) <= 64 GPL); their directions (dt, dl) --
+    // GPL > 0: every lane owns at most GPL soft groups (NG1 <= 64 GPL); their directions (dt, dl) --
     // the expensive part, two group evaluations with six reciprocals each -- are computed once, kept in
     // registers between the step-length pass and the update pass.  GPL == 0: the generic loops recompute.
     auto rows_update_t = [&](auto GPLc, double sigmu) {
@@ -899,12 +1057,27 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             const double it = rcp_nr(t), sg = l * it;
             bound(t, l, dt, -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it);
         }
+        auto hard_dir = [&](int r, double& dt, double& dl) {
+            const int i = (r - RH0) >> 1, up = (r - RH0) & 1;
+            const double t = s.t[r], l = s.lam[r], d = hard_d(i, up);
+            const double cc = s.cxc[NG1 + i], ca = s.cxa[NG1 + i];
+            dt = (up ? -cc : cc) + d - t;
+            const double dta = (up ? -ca : ca) + d - t;
+            const double it = rcp_nr(t), sg = l * it;
+            dl = -sg * dt - l - (dta * (-sg * dta - l) - sigmu) * it;
+        };
+        if constexpr (HARD)
+            for (int r = RH0 + lane; r < m; r += 64) {
+                double dt, dl;
+                hard_dir(r, dt, dl);
+                bound(s.t[r], s.lam[r], dt, dl);
+            }
         auto soft_dir = [&](int e, double* dt, double* dl) {
-            const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
-            const Grp ga = group(k, j, 0, 0.0), gc = group(k, j, 1, sigmu);
+            const int r0 = 8 * N + 4 * e;
+            const Grp ga = group(e, 0, 0.0), gc = group(e, 1, sigmu);
             double va[4], vc[4];
-            soft_vals(ga, k, j, s.cxa[e], va);
-            soft_vals(gc, k, j, s.cxc[e], vc);
+            soft_vals(ga, e, s.cxa[e], va);
+            soft_vals(gc, e, s.cxc[e], vc);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const double t = s.t[r0 + q], l = s.lam[r0 + q];
@@ -919,7 +1092,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
 #pragma unroll
             for (int gi = 0; gi < GPL; ++gi) {
                 const int e = lane + 64 * gi;
-                if (e < N1 * NS) {
+                if (e < NG1) {
                     soft_dir(e, sdt[gi], sdl[gi]);
                     const int r0 = 8 * N + 4 * e;
 #pragma unroll
@@ -927,7 +1100,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
                 }
             }
         } else {
-            for (int e = lane; e < N1 * NS; e += 64) {
+            for (int e = lane; e < NG1; e += 64) {
                 soft_dir(e, sdt[0], sdl[0]);
                 const int r0 = 8 * N + 4 * e;
 #pragma unroll
@@ -951,33 +1124,45 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             s.t[r] = tn;
             s.lam[r] = ln;
         }
-        auto soft_upd = [&](int e, const double* dt, const double* dl) {
-            const int r0 = 8 * N + 4 * e;
-            double tn[4], ln[4];
+        {
+            double hdt = 0.0, hdl = 0.0;  // hard rows: one per lane (2 NHH <= 12 < 64)
+            const int r = RH0 + lane;
+            if (HARD && r < m) hard_dir(r, hdt, hdl);
+            auto soft_upd = [&](int e, const double* dt, const double* dl) {
+                const int r0 = 8 * N + 4 * e;
+                double tn[4], ln[4];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                tn[q] = s.t[r0 + q] + al * dt[q];
-                ln[q] = s.lam[r0 + q] + al * dl[q];
-                lmu += tn[q] * ln[q];
-                lcm = fmax(lcm, tn[q] * ln[q]);
-            }
+                for (int q = 0; q < 4; ++q) {
+                    tn[q] = s.t[r0 + q] + al * dt[q];
+                    ln[q] = s.lam[r0 + q] + al * dl[q];
+                    lmu += tn[q] * ln[q];
+                    lcm = fmax(lcm, tn[q] * ln[q]);
+                }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                s.t[r0 + q] = tn[q];
-                s.lam[r0 + q] = ln[q];
-            }
-        };
-        if constexpr (GPL > 0) {
+                for (int q = 0; q < 4; ++q) {
+                    s.t[r0 + q] = tn[q];
+                    s.lam[r0 + q] = ln[q];
+                }
+            };
+            if constexpr (GPL > 0) {
 #pragma unroll
-            for (int gi = 0; gi < GPL; ++gi) {
-                const int e = lane + 64 * gi;
-                if (e < N1 * NS) soft_upd(e, sdt[gi], sdl[gi]);
+                for (int gi = 0; gi < GPL; ++gi) {
+                    const int e = lane + 64 * gi;
+                    if (e < NG1) soft_upd(e, sdt[gi], sdl[gi]);
+                }
+            } else {
+                for (int e = lane; e < NG1; e += 64) {
+                    double dt[4], dl[4];
+                    soft_dir(e, dt, dl);
+                    soft_upd(e, dt, dl);
+                }
             }
-        } else {
-            for (int e = lane; e < N1 * NS; e += 64) {
-                double dt[4], dl[4];
-                soft_dir(e, dt, dl);
-                soft_upd(e, dt, dl);
+            if (HARD && r < m) {
+                const double tn = s.t[r] + al * hdt, ln = s.lam[r] + al * hdl;
+                lmu += tn * ln;
+                lcm = fmax(lcm, tn * ln);
+                s.t[r] = tn;
+                s.lam[r] = ln;
             }
         }
         for (int e = lane; e < N1 * NX; e += 64) s.dx[e] += al * (s.dxc[e] - s.dx[e]);
@@ -987,7 +1172,6 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         rp *= (1.0 - al);
         gap *= (1.0 - al);
     };
-    const int gpl = (N1 * NS + 63) / 64;
     auto rows_update = [&](double sigmu) {
         if (gpl == 1) rows_update_t(IC<1>{}, sigmu);
         else if (gpl == 2) rows_update_t(IC<2>{}, sigmu);
@@ -1018,7 +1202,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         // to this sweep's preheader and live only during the sweep (not across the whole solve); the
         // factor sweep's are built up front (fconst) and pinned in registers
         const auto ln = [&] {
-            if constexpr (K == 1) return fconst(opaque(lane));
+            if constexpr (K == 1) return fconst<NSS>(opaque(lane));
             else return opaque(lane);
         }();
         using T_ = IC<1>;
@@ -1052,6 +1236,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
 
     each_slot([&](auto Sc) { issue(IC<0>{}, ring[decltype(Sc)::value], decltype(Sc)::value); });
     sweep(IC<0>{});
+    term_cx(s.cxa, s.dx);
     STAMP(1);
     rp = rows_init();
     {
@@ -1074,6 +1259,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         if (lane < NX) s.dxc[lane] = s.dx[lane];
         wave_sync();
         sweep(IC<2>{});
+        term_cx(s.cxa, s.dxc);
         STAMP(3);
         const double sigmu = rows_pred();
         RSTAMP(8);
@@ -1084,6 +1270,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         if (lane < NX) s.dxc[lane] = s.dx[lane];
         wave_sync();
         sweep(IC<4>{});
+        term_cx(s.cxc, s.dxc);
         STAMP(3);
         rows_update(sigmu);
         RSTAMP(9);
@@ -1095,11 +1282,12 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     // ------------------------------------------------------------ outputs
     for (int e = lane; e < N1 * NX; e += 64) A.dx[(size_t)b * N1 * NX + e] = s.dx[e];
     for (int e = lane; e < N * NU; e += 64) A.du[(size_t)b * N * NU + e] = s.du[e];
-    if (A.slack)  // slacks = the t of rows sl >= 0, su >= 0 (equal to the iterate's sl, su up to r_p)
-        for (int e = lane; e < N1 * NS; e += 64) {
-            const int k = e / NS, j = e % NS, r0 = 8 * N + 12 * k + 4 * j;
-            A.slack[((size_t)b * N1 * NS + e) * 2] = s.t[r0 + 2];
-            A.slack[((size_t)b * N1 * NS + e) * 2 + 1] = s.t[r0 + 3];
+    if (A.slack)  // slacks = the t of rows sl >= 0, su >= 0 (equal to the iterate's sl, su up to r_p); [N+1][3][2]
+        for (int e = lane; e < N1 * 3; e += 64) {
+            const int k = e / 3, j = e - 3 * k;
+            const int g = k < N ? (j < NS ? k * NS + j : -1) : (j < A.nsN ? NGS + j : -1);
+            A.slack[((size_t)b * N1 * 3 + e) * 2] = g >= 0 ? s.t[8 * N + 4 * g + 2] : 0.0;
+            A.slack[((size_t)b * N1 * 3 + e) * 2 + 1] = g >= 0 ? s.t[8 * N + 4 * g + 3] : 0.0;
         }
     if (lane == 0) {
         A.iters[b] = it;
@@ -1144,23 +1332,43 @@ hipError_t launch_rti_qp_pack(const QpArgs& a, hipStream_t s) {
     return hipGetLastError();
 }
 
-int rti_qp_blocks_per_cu(int N) {
-    // every limit at once (LDS per instance, the 375-register allocation: one wave per SIMD, waves per CU),
-    // as the runtime applies them
-    const size_t lds = qp_lds_bytes(N);
-    if (hipFuncSetAttribute((const void*)rti_qp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess)
-        return 0;
+// the kernel instantiation of a stage row count
+template <bool HARD>
+static const void* rti_qp_fn_h(int nh) {
+    switch (nh) {
+        case 0: return (const void*)rti_qp_kernel<0, HARD>;
+        case 1: return (const void*)rti_qp_kernel<1, HARD>;
+        case 2: return (const void*)rti_qp_kernel<2, HARD>;
+        default: return (const void*)rti_qp_kernel<3, HARD>;
+    }
+}
+// the kernel instantiation of a row set
+static const void* rti_qp_fn(QpRows q) { return q.nhN > q.nsN ? rti_qp_fn_h<true>(q.ns) : rti_qp_fn_h<false>(q.ns); }
+
+int rti_qp_blocks_per_cu(int N, QpRows q) {
+    // every limit at once (LDS per instance, the register allocation: one wave per SIMD, waves per CU), as the
+    // runtime applies them
+    const size_t lds = qp_lds_bytes(N, q);
+    const void* fn = rti_qp_fn(q);
+    if (hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds) != hipSuccess) return 0;
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rti_qp_kernel, 64, lds) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, 64, lds) != hipSuccess) return 0;
     return n;
 }
 
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
-    const size_t lds = qp_lds_bytes(a.N);
-    hipError_t e = hipFuncSetAttribute((const void*)rti_qp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (a.nh < 0 || a.nh > 3 || a.nhN < 0 || a.nhN > QP_NHN || a.nsN < 0 || a.nsN > 3 || a.nsN > a.nhN ||
+        a.nhN - a.nsN > 6)
+        return hipErrorInvalidValue;
+    const QpRows q{a.nh, a.nhN, a.nsN};
+    const size_t lds = qp_lds_bytes(a.N, q);
+    const void* fn = rti_qp_fn(q);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(rti_qp_kernel, dim3(a.B), dim3(64), lds, s, a);
+    void* args[] = {(void*)&a};
+    e = hipLaunchKernel(fn, dim3(a.B), dim3(64), args, lds, s);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 

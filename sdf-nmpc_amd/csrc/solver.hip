@@ -79,14 +79,15 @@ struct sdfnmpc_solver {
     const sdfnmpc_net* net = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
-    int B = 0, N = 0, np = 0, ny = 0, latent_mode = 0;
+    int B = 0, N = 0, np = 0, ny = 0, nyN = 4, latent_mode = 0;
+    bool no_sdf = false;  // no constraint row or cost reads the network
     sdfnmpc_quad_model model{};
     sdfnmpc_qp_opts qp{};
     std::vector<void*> allocs;
     double *x = nullptr, *u = nullptr, *p = nullptr, *x0 = nullptr, *yref = nullptr, *W = nullptr, *yNref = nullptr,
            *WN = nullptr, *dt = nullptr, *xn = nullptr, *AB = nullptr, *y = nullptr, *Jy = nullptr, *yN = nullptr,
            *JyN = nullptr, *h = nullptr, *Jh = nullptr, *dx = nullptr, *du = nullptr, *res = nullptr, *u0 = nullptr,
-           *slack = nullptr;
+           *slack = nullptr, *hE = nullptr, *JhE = nullptr;
     int *status = nullptr, *iters = nullptr;
     // pinned host memory: step outputs and the upload staging arena (reset after every wait)
     double* h_u0 = nullptr;
@@ -166,12 +167,19 @@ struct SolverDevice {
 
 extern "C" int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_solver_opts* o,
                                      sdfnmpc_solver** out) {
-    if (!ctx || !net || !o || !out) return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_solver_create");
+    if (!ctx || !o || !out) return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_solver_create");
     *out = nullptr;
     if (o->B < 1 || o->N < 1 || o->np < 17 || (o->ny != 11 && o->ny != 12) || !o->dt ||
         (o->latent_mode != 0 && o->latent_mode != 1) || o->qp.ny != o->ny)
         return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "solver opts: B, N >= 1, np >= 17, ny in {11, 12} == qp.ny, dt required");
-    if (o->np < 17 + sdfnmpc_net_size_latent(net))  // the stage parameters end with the network's latent
+    if (o->qp.nyN != 4 && o->qp.nyN != 5)
+        return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "solver opts: qp.nyN must be 4 or 5");
+    bool need_sdf = o->ny == 12;  // the constraint set or the cost reads the network
+    for (int j = 0; j < o->qp.nh && j < 3; ++j) need_sdf = need_sdf || o->qp.h_col[j] == 2;
+    for (int j = 0; j < o->qp.nhN && j < SDFNMPC_NHN_MAX; ++j) need_sdf = need_sdf || o->qp.hN_col[j] == 2;
+    if (need_sdf && !net)
+        return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, "solver: the constraint set / cost reads the SDF but the network is NULL");
+    if (net && o->np < 17 + sdfnmpc_net_size_latent(net))  // the stage parameters end with the network's latent
         return sdfnmpc_solver_fail_(SDFNMPC_E_ARG, ("solver opts: np = " + std::to_string(o->np) + " < 17 + latent size " +
                                                     std::to_string(sdfnmpc_net_size_latent(net)) + " of this network").c_str());
     auto* s = new sdfnmpc_solver();
@@ -180,6 +188,8 @@ extern "C" int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, c
     s->device = sdfnmpc_ctx_device(ctx);
     s->stream = (hipStream_t)sdfnmpc_ctx_stream(ctx);
     s->B = o->B; s->N = o->N; s->np = o->np; s->ny = o->ny; s->latent_mode = o->latent_mode;
+    s->nyN = o->qp.nyN;
+    s->no_sdf = !need_sdf;
     s->model = o->model;
     s->qp = o->qp;
     SolverDevice sd(s->device);
@@ -187,10 +197,11 @@ extern "C" int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, c
     hipError_t e = hipSuccess;
     auto A = [&](auto** p, size_t n) { if (e == hipSuccess) e = s->alloc(p, n); };
     A(&s->x, B * N1 * 10); A(&s->u, B * N * 4); A(&s->p, B * N1 * o->np); A(&s->x0, B * 10);
-    A(&s->yref, B * N * o->ny); A(&s->W, B * N * o->ny); A(&s->yNref, B * 4); A(&s->WN, B * 4); A(&s->dt, N);
-    A(&s->xn, B * N * 10); A(&s->AB, B * N * 140); A(&s->y, B * N * 11); A(&s->Jy, B * N * 154); A(&s->yN, B * 4);
-    A(&s->JyN, B * 40); A(&s->h, B * N1 * 3); A(&s->Jh, B * N1 * 30); A(&s->dx, B * N1 * 10); A(&s->du, B * N * 4);
-    A(&s->res, B * 2); A(&s->slack, B * N1 * 6);
+    const size_t nyN = s->nyN;
+    A(&s->yref, B * N * o->ny); A(&s->W, B * N * o->ny); A(&s->yNref, B * nyN); A(&s->WN, B * nyN); A(&s->dt, N);
+    A(&s->xn, B * N * 10); A(&s->AB, B * N * 140); A(&s->y, B * N * 11); A(&s->Jy, B * N * 154); A(&s->yN, B * nyN);
+    A(&s->JyN, B * 10 * nyN); A(&s->h, B * N1 * 3); A(&s->Jh, B * N1 * 30); A(&s->dx, B * N1 * 10); A(&s->du, B * N * 4);
+    A(&s->res, B * 2); A(&s->slack, B * N1 * 6); A(&s->hE, B * 6); A(&s->JhE, B * 60);
     // [u0 (B x 4 doubles) | status (B ints) | iters (B ints)] contiguous on both sides: one copy back per step
     A(&s->u0, B * 5);
     if (e == hipSuccess) {
@@ -208,14 +219,15 @@ extern "C" int sdfnmpc_solver_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, c
         delete s;
         return sdfnmpc_solver_fail_(SDFNMPC_E_HIP, (std::string("solver buffers: ") + hipGetErrorString(e)).c_str());
     }
-    const int n = (int)N, n1 = (int)N1, d = 8;
+    const int n = (int)N, n1 = (int)N1, d = 8, w = (int)nyN;
     s->fields = {{"x", s->x, n1, 10, d},       {"u", s->u, n, 4, d},          {"p", s->p, n1, o->np, d},
                  {"x0", s->x0, 1, 10, d},      {"yref", s->yref, n, o->ny, d}, {"W", s->W, n, o->ny, d},
-                 {"yNref", s->yNref, 1, 4, d}, {"WN", s->WN, 1, 4, d},         {"u0", s->u0, 1, 4, d},
+                 {"yNref", s->yNref, 1, w, d}, {"WN", s->WN, 1, w, d},         {"u0", s->u0, 1, 4, d},
                  {"dx", s->dx, n1, 10, d},     {"du", s->du, n, 4, d},         {"xn", s->xn, n, 10, d},
                  {"AB", s->AB, n, 140, d},     {"y", s->y, n, 11, d},          {"Jy", s->Jy, n, 154, d},
-                 {"yN", s->yN, 1, 4, d},       {"JyN", s->JyN, 1, 40, d},      {"h", s->h, n1, 3, d},
-                 {"Jh", s->Jh, n1, 30, d},     {"res", s->res, 1, 2, d},       {"slack", s->slack, n1, 6, d},  {"status", s->status, 1, 1, 4},
+                 {"yN", s->yN, 1, w, d},       {"JyN", s->JyN, 1, 10 * w, d},  {"h", s->h, n1, 3, d},
+                 {"Jh", s->Jh, n1, 30, d},     {"hE", s->hE, 1, 6, d},         {"JhE", s->JhE, 1, 60, d},
+                 {"res", s->res, 1, 2, d},     {"slack", s->slack, n1, 6, d},  {"status", s->status, 1, 1, 4},
                  {"iters", s->iters, 1, 1, 4}};
     *out = s;
     return SDFNMPC_OK;
@@ -320,9 +332,11 @@ extern "C" int sdfnmpc_solver_step(sdfnmpc_solver* s) {
     la.B = s->B; la.N = s->N; la.np = s->np; la.latent_mode = s->latent_mode;
     la.x = s->x; la.u = s->u; la.p = s->p; la.dt = s->dt;
     la.xn = s->xn; la.AB = s->AB; la.y = s->y; la.Jy = s->Jy; la.yN = s->yN; la.JyN = s->JyN; la.h = s->h; la.Jh = s->Jh;
+    la.nyN = s->nyN; la.no_sdf = s->no_sdf ? 1 : 0; la.hE = s->hE; la.JhE = s->JhE;
     sdfnmpc_qp_args qa{};
     qa.B = s->B; qa.N = s->N;
     qa.xn = s->xn; qa.AB = s->AB; qa.y = s->y; qa.Jy = s->Jy; qa.yN = s->yN; qa.JyN = s->JyN; qa.h = s->h; qa.Jh = s->Jh;
+    qa.hE = s->hE; qa.JhE = s->JhE;
     qa.x = s->x; qa.u = s->u; qa.x0 = s->x0; qa.yref = s->yref; qa.W = s->W; qa.yNref = s->yNref; qa.WN = s->WN;
     qa.dt = s->dt; qa.dx = s->dx; qa.du = s->du; qa.slack = s->slack; qa.status = s->status; qa.iters = s->iters;
     qa.res = s->res;

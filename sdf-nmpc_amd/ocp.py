@@ -139,7 +139,7 @@ class Ocp:
                                                           cfg.mpc.control_loop_time * 1e-3)
         if build:
             build_solver(weights=weights)
-        self.cmodel = _lib.quad_model(cfg)
+        self.cmodel = _lib.quad_model(cfg, model)
         # QP data of the model + solver options (ocp.py:113-120: LM regularisation, <= 100 iterations)
         # qp_warm_start: HPIPM's primal warm start (ocp.py:116 sets qp_solver_warm_start = 1): each QP starts
         # from the previous one's du.  Off by default: on the C3 problem in closed loop it leaves the mean
@@ -147,9 +147,9 @@ class Ocp:
         self.qp_opts = _lib.qp_opts(model, lm=float(cfg.mpc.lm_reg if lm is None else lm), max_iter=qp_iter_max,
                                     tol=qp_tol, lm_scaling=lm_scaling, warm_start=qp_warm_start)
         devs = list(devices) if devices else [device]
-        if ctx is None:  # the first device's context sizes the plan (sdfnmpc_qp_capacity)
+        if ctx is None:  # the first device's context sizes the plan (sdfnmpc_qp_capacity_for: this constraint set)
             c0 = _lib.Context(devs[0])
-            self.plan = shard.plan(B, c0.qp_capacity(N), len(devs))
+            self.plan = shard.plan(B, c0.qp_capacity(N, self.qp_opts), len(devs))
         else:
             c0, self.plan = ctx, [(0, 0, B)]
         # one QP kernel for the whole batch (AUTO picks by batch size: include/sdfnmpc.h), so the split over
@@ -160,7 +160,9 @@ class Ocp:
             c = c0 if slot == 0 else _lib.Context(devs[slot])
             if qp_kind is not None:
                 c.set_qp_kernel(qp_kind)
-            n = net if (net is not None and slot == 0) else load_net(c, cfg, weights)
+            # the network only with flags.enable_sdf (gen_model.py:26-39); the solver evaluates it only where a
+            # constraint row or the cost reads it (Nmpc.eval reads it too)
+            n = (net if (net is not None and slot == 0) else load_net(c, cfg, weights)) if model.enable_sdf else None
             s = _lib.Solver(c, n, self.cmodel, self.qp_opts, hi - lo, N, model.np, model.ny, self.dt)
             self.parts.append(_Part(lo, hi, c, n, s, ctx is None, n is not net))
         self.ctx, self.net = self.parts[0].ctx, self.parts[0].net
@@ -238,7 +240,7 @@ class Ocp:
     def close(self):
         for p in self.parts:
             p.solver.close()
-            if p.own_net:
+            if p.own_net and p.net is not None:
                 p.net.close()
             if p.own_ctx:
                 p.ctx.close()

@@ -53,7 +53,7 @@ def rk4(x, u, dt, lim):
     return x + dt / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
 
 
-def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None, sdf_cost: bool = False):
+def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None, sdf_cost: bool = False, nyN: int = 4):
     rng = np.random.default_rng(seed)
     lim = cfg.robot.limits
     L = int(cfg.nn.size_latent)
@@ -93,8 +93,8 @@ def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None, sd
     yref[..., 4:7] = vref[:, None, :]
     Wrow = np.concatenate([w.pos, [w.att[2]], w.vel, w.att[:2], w.rates[2:], [w.acc]]).astype(float)
     W = np.broadcast_to(Wrow, (B, N, 11)).copy()
-    yN = yref[:, -1, :4].copy()
-    WN = W[:, -1, :4].copy()
+    yN = yref[:, -1, :nyN].copy()  # Nmpc.set_ref at the last node: y[:nyN], W[:nyN] (controller.py:141-142)
+    WN = W[:, -1, :nyN].copy()
     if sdf_cost:  # flags.sdf_cost: 12th residual (1 - s/2)^4 with reference 0 and weight 20 (model.Quad.extra_W)
         yref = np.concatenate([yref, np.zeros((B, N, 1))], axis=-1)
         W = np.concatenate([W, np.full((B, N, 1), 20.0)], axis=-1)
@@ -123,3 +123,19 @@ def depth_images(B: int, H: int = 270, W: int = 480, seed: int = 0, kind: str = 
     if kind == "mm":
         return np.round(out * 1000.0).astype(np.uint16)
     return out.astype(np.float32)
+
+
+def braking_coeffs(deg: int = 4, seed: int = 0, a_brake: float = 6.32, d0: float = 0.05, noise: float = 2e-3):
+    """Synthetic braking-distance polynomial in polynomial_3variate's term order (utils/math.py:307-314):
+    d(v) = d0 + |v|^2 / (2 a_brake) plus seeded small terms on every monomial, so every coefficient is
+    exercised (the reference loads a fitted file, default.yaml:70-72, which is absent here)."""
+    from .model import poly_terms
+    rng = np.random.default_rng(seed)
+    t = poly_terms(deg)
+    c = rng.normal(0, noise, len(t))
+    for i, (a, b, e) in enumerate(t):
+        if (a, b, e) == (0, 0, 0):
+            c[i] += d0
+        if sorted((a, b, e)) == [0, 0, 2]:
+            c[i] += 0.5 / a_brake
+    return c

@@ -34,6 +34,8 @@ What is pinned to what:
                           means in fp32 and fp64, sampled preprocessed pixels, per-stage channel sums.
   * wide_golden.npz    -- the reference's own ``NeuralDF`` at config C5's widths [1024,1024,512,256]
                           (SIREN-init seed 0): df and d df / d pos in fp32 and fp64.
+  * flags_golden.npz   -- the flag space (flags_golden below): polynomial_3variate's term order / values,
+                          stability.get_r_tilde_max, set_ref with the stability terminal row.
   * params_golden.npz  -- the reference's own ``Nmpc.set_latent`` / ``Nmpc.set_ref`` /
                           ``Quad.formate_ref`` (controller.py:50-54,133-142, quad_rollpitchyawrate.py:
                           62-65) called unbound on small stand-in objects; ``Config`` from the
@@ -647,10 +649,102 @@ def scene_golden(n=256):
     print("scene_golden.npz", {k: v.shape for k, v in out.items()})
 
 
+def flags_golden():
+    """The flag space of default.yaml:16-23 (gen_model.py:26-149):
+      * poly/*      -- polynomial_3variate (utils/math.py:294-321) run from the reference with casadi replaced
+                       by a numeric stand-in: SX.sym('x') is a fixed numeric point, vertcat concatenates,
+                       sum1 sums (and records its argument, the term vector), Function is inert.  At the
+                       point (2, 3, 5) the terms 2^a 3^b 5^c give the exponents of every term in the
+                       reference's order; with given coefficients, the polynomial's values at sample v.
+      * rtilde/*    -- stability.get_r_tilde_max (utils/stability.py:44-75: sympy solve + scipy SLSQP) itself,
+                       np.random seeded before each call (its start point is np.random.uniform), on the
+                       reference Config with the weights it reads (mpc.weights.{acc, att}) set to set_const_on's.
+      * setref5/*   -- Nmpc.set_ref at the terminal node with nyN = 5 (flags.stability adds a terminal cost
+                       row, gen_model.py:149): WN = W[:5], yN = y[:5] (controller.py:141-142).
+    """
+    from sdf_nmpc.controller import Nmpc
+    from sdf_nmpc.model.quad_rollpitchyawrate import Quad as RQuad
+    from sdf_nmpc.utils import stability as rstab
+    from sdf_nmpc.utils.reference import Ref
+    out = {}
+    cs = rmath.cs
+    state = {"point": None, "terms": None}
+
+    class _SX:
+        @staticmethod
+        def sym(name, n, m=1):
+            return np.array(state["point"], float) if name == "x" else np.ones(n)
+
+    def _sum1(v):
+        state["terms"] = np.asarray(v, float).copy()
+        return float(np.sum(v))
+
+    saved = {k: getattr(cs, k, None) for k in ("SX", "vertcat", "sum1", "Function")}
+    cs.SX = _SX
+    cs.vertcat = lambda *a: np.concatenate([np.atleast_1d(np.asarray(v, float)) for v in a])
+    cs.sum1 = _sum1
+    cs.Function = lambda *a, **k: None
+    try:
+        rng = np.random.default_rng(5)
+        for deg in (0, 1, 2, 3, 4, 5, 6):
+            state["point"] = [2.0, 3.0, 5.0]
+            rmath.polynomial_3variate(deg, np.ones((deg + 1) * (deg + 2) * (deg + 3) // 6))
+            t = state["terms"]
+            exps = []
+            for v in t:
+                e = []
+                for pr in (2, 3, 5):
+                    c = 0
+                    while round(v) % pr == 0:
+                        v /= pr
+                        c += 1
+                    e.append(c)
+                exps.append(e)
+            out[f"poly/deg{deg}/exps"] = np.array(exps, np.int64)
+            coeffs = rng.normal(size=len(t))
+            vs = rng.uniform(-4, 4, (16, 3))
+            vals = []
+            for v in vs:
+                state["point"] = v
+                rmath.polynomial_3variate(deg, coeffs)
+                vals.append(float(np.sum(state["terms"])))
+            out[f"poly/deg{deg}/coeffs"] = coeffs
+            out[f"poly/deg{deg}/v"] = vs
+            out[f"poly/deg{deg}/val"] = np.array(vals)
+    finally:
+        for k, v in saved.items():
+            if v is None:
+                delattr(cs, k)
+            else:
+                setattr(cs, k, v)
+    cfg = Config(os.path.join(REF, "sdf_nmpc/config/default.yaml"))
+    on = cfg.mpc.weights.set_const_on
+    cfg.mpc.weights.acc, cfg.mpc.weights.att = on.acc, list(on.att)
+    for i, (N, T) in enumerate(((20, 1.5), (40, 1.5), (30, 2.0))):
+        cfg.mpc.N, cfg.mpc.T = N, T
+        for seed in (0, 1, 2):
+            np.random.seed(seed)
+            out[f"rtilde/N{N}_T{T}/seed{seed}"] = np.array(float(rstab.get_r_tilde_max(cfg)))
+    # set_ref with nyN = 5
+    N = 20
+    st = types.SimpleNamespace(cfg=CFG, N=N, p=np.zeros((N + 1, 145)), y=np.zeros((N, 11)), W=np.zeros((N, 11)),
+                               yN=np.zeros(5), WN=np.zeros(5), model=types.SimpleNamespace(nyN=5, extra_W=np.array([])))
+    st.model.formate_ref = types.MethodType(RQuad.formate_ref, st.model)
+    r = Ref(CFG)
+    r.p, r.q, r.v, r.wz = np.array([1.0, -2.0, 3.0]), rmath.euler2quat(np.array([0, 0, 0.7])), np.array([0.5, -1.0, 2.0]), 0.3
+    ws = r.W_on
+    r.Wp, r.Wq, r.Wv, r.Ww, r.Wa = ws.Wp, ws.Wq, ws.Wv, ws.Ww, ws.Wa
+    Nmpc.set_ref(st, r, N)
+    out["setref5/yN"], out["setref5/WN"] = st.yN.copy(), st.WN.copy()
+    out["setref5/ref"] = np.concatenate([r.p, r.q, r.v, [r.wz], ws.Wp, ws.Wq, ws.Wv, ws.Ww, [ws.Wa]])
+    np.savez_compressed(os.path.join(HERE, "flags_golden.npz"), **out)
+    print("flags_golden.npz", len(out))
+
+
 if __name__ == "__main__":
     only = sys.argv[1:]
     for name, fn in (("sdf", sdf_golden), ("lin", lin_golden), ("grid", grid_golden), ("params", params_golden),
                      ("ts", ts_golden), ("refgen", refgen_golden), ("vae", vae_golden), ("wide", wide_golden), ("sdfc3", sdfc3_golden),
-                     ("variants", variants_golden), ("scene", scene_golden)):
+                     ("variants", variants_golden), ("scene", scene_golden), ("flags", flags_golden)):
         if not only or name in only:
             fn()

@@ -13,7 +13,7 @@ int main(int argc, char** argv) {
   for (int i=0;i<16;++i){ std::vector<double> h(sizes[i]); fread(h.data(),8,sizes[i],f); hipMalloc(&d[i],8*sizes[i]); hipMemcpy(d[i],h.data(),8*sizes[i],hipMemcpyHostToDevice);} 
   double opt[22]; fread(opt, 8, 22, f); fclose(f);
   QpArgs q{}; q.B=B; q.N=N; q.xn=d[0];q.AB=d[1];q.y=d[2];q.Jy=d[3];q.yN=d[4];q.JyN=d[5];q.h=d[6];q.Jh=d[7];q.x=d[8];q.u=d[9];q.x0=d[10];q.yref=d[11];q.W=d[12];q.yNref=d[13];q.WN=d[14];q.dt=d[15];
-  for(int i=0;i<4;++i){q.lbu[i]=opt[i];q.ubu[i]=opt[4+i];} for(int i=0;i<3;++i){q.lh[i]=opt[8+i];q.uh[i]=opt[11+i];q.zl[i]=opt[14+i];q.Zl[i]=opt[17+i];}
+  for(int i=0;i<4;++i){q.lbu[i]=opt[i];q.ubu[i]=opt[4+i];} for(int i=0;i<3;++i){q.lh[i]=opt[8+i];q.uh[i]=opt[11+i];q.zl[i]=opt[14+i];q.Zl[i]=opt[17+i];} qp_default_rows(q);
   q.lm=opt[20]; q.tol=opt[21]; q.max_iter=100; q.cost_scaling=1; q.lm_scaling=1; q.ny=11;
   hipMalloc(&q.dx,8*B*(N+1)*10); hipMalloc(&q.du,8*B*N*4); hipMalloc(&q.status,4*B); hipMalloc(&q.iters,4*B); hipMalloc(&q.res,16*B);
   hipMalloc(&q.work,8*B*qp_work_doubles(N)); hipMalloc(&q.stamps,8*B*16);
