@@ -29,7 +29,9 @@ extern "C" {
 typedef double sdf_l4c_real;
 typedef long long sdf_l4c_int;
 
-/* f: [Co_p_B(3); latent(128)] (131 x 1) -> df (1 x 1) */
+/* f: [Co_p_B(3); latent(L)] ((3 + L) x 1) -> df (1 x 1); L = the loaded network's size_latent (128 for
+ * the deployed net, gen_model.py:39,60 / network/neural_df.py:16; any L <= 1024).  The sparsity queries
+ * load the network first, so the patterns carry its width. */
 int sdf_l4c(const sdf_l4c_real** arg, sdf_l4c_real** res, sdf_l4c_int* iw, sdf_l4c_real* w, int mem);
 sdf_l4c_int sdf_l4c_n_in(void);
 sdf_l4c_int sdf_l4c_n_out(void);
@@ -43,7 +45,7 @@ void sdf_l4c_release(int mem);
 void sdf_l4c_incref(void);
 void sdf_l4c_decref(void);
 
-/* Jacobian: (in (131x1), out (1x1)) -> d out / d in (1 x 131, dense) */
+/* Jacobian: (in ((3+L)x1), out (1x1)) -> d out / d in (1 x (3+L), dense) */
 int jac_sdf_l4c(const sdf_l4c_real** arg, sdf_l4c_real** res, sdf_l4c_int* iw, sdf_l4c_real* w, int mem);
 sdf_l4c_int jac_sdf_l4c_n_in(void);
 sdf_l4c_int jac_sdf_l4c_n_out(void);
@@ -51,7 +53,7 @@ const sdf_l4c_int* jac_sdf_l4c_sparsity_in(sdf_l4c_int i);
 const sdf_l4c_int* jac_sdf_l4c_sparsity_out(sdf_l4c_int i);
 int jac_sdf_l4c_work(sdf_l4c_int* sz_arg, sdf_l4c_int* sz_res, sdf_l4c_int* sz_iw, sdf_l4c_int* sz_w);
 
-/* Adjoint: (in (131x1), out (1x1), adj_out (1x1)) -> adj_out * d out / d in (131 x 1) */
+/* Adjoint: (in ((3+L)x1), out (1x1), adj_out (1x1)) -> adj_out * d out / d in ((3+L) x 1) */
 int adj1_sdf_l4c(const sdf_l4c_real** arg, sdf_l4c_real** res, sdf_l4c_int* iw, sdf_l4c_real* w, int mem);
 sdf_l4c_int adj1_sdf_l4c_n_in(void);
 sdf_l4c_int adj1_sdf_l4c_n_out(void);

@@ -2,8 +2,10 @@
 //
 // Replaces the L4CasADi-generated libtorch library (gen_model.py:38-39).  acados calls sdf_l4c then
 // jac_sdf_l4c on the same input for every shooting node, so the forward call
-// computes value AND full 1x131 gradient in one device launch and the Jacobian/adjoint calls are
-// served from a per-thread cache keyed on the exact input bits.
+// computes value AND full 1 x (3 + L) gradient in one device launch and the Jacobian/adjoint calls are
+// served from a per-thread cache keyed on the exact input bits.  The input width is the loaded network's:
+// 3 + size_latent (gen_model.py:60 feeds vertcat(Co_p_B, latent); neural_df.py:16), 131 for the deployed
+// net, any latent up to 1024 otherwise.
 #include <dlfcn.h>
 
 #include <atomic>
@@ -11,24 +13,24 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/sdf_l4c.h"
 #include "../../include/sdfnmpc.h"
 
 namespace {
 
-constexpr int D = 131;  // 3 + latent 128
-
 std::mutex g_mu;
 sdfnmpc_ctx* g_ctx = nullptr;
 sdfnmpc_net* g_net = nullptr;
+std::atomic<int> g_D{0};              // 3 + size_latent of the loaded network (0: not loaded)
 std::string g_err;                    // guarded by g_mu
 std::atomic<unsigned long long> g_gen{1};  // bumped by every sdf_l4c_configure: invalidates all caches
 
 // per-thread cache of the last input (acados calls sdf_l4c then jac_sdf_l4c on the same input); an
 // entry is valid only for the configuration generation it was computed under
-thread_local double t_in[D];
-thread_local double t_df = 0.0, t_grad[D];
+thread_local std::vector<double> t_in, t_grad;
+thread_local double t_df = 0.0;
 thread_local unsigned long long t_gen = 0;
 thread_local std::string t_err;
 
@@ -63,34 +65,45 @@ int init_locked(const char* path, int device) {
         g_ctx = nullptr;
         return -1;
     }
-    if (sdfnmpc_net_size_latent(g_net) != D - 3) {
-        g_err = "sdf_l4c: network latent size != 128";
-        return -1;
-    }
+    g_D.store(3 + sdfnmpc_net_size_latent(g_net));
     return 0;
+}
+
+// the input width, loading the network on first use (CasADi asks for the sparsity before any call);
+// 0 when no network could be loaded (the error is in sdf_l4c_last_error)
+int width() {
+    const int d = g_D.load();
+    if (d) return d;
+    std::lock_guard<std::mutex> lk(g_mu);
+    return init_locked(nullptr, -1) ? 0 : g_D.load();
 }
 
 // value + gradient for one input, cached per thread
 int eval(const double* in) {
     if (!in) return 1;
-    if (t_gen == g_gen.load() && memcmp(in, t_in, sizeof t_in) == 0) return 0;
+    const int D = width();
+    if (!D) return 1;
+    if (t_gen == g_gen.load() && (int)t_in.size() == D && memcmp(in, t_in.data(), D * sizeof(double)) == 0) return 0;
     std::lock_guard<std::mutex> lk(g_mu);
     if (init_locked(nullptr, -1)) return 1;
     const unsigned long long gen = g_gen.load();
-    if (sdfnmpc_sdf_eval_host(g_ctx, g_net, 1, in, &t_df, t_grad) != SDFNMPC_OK) {
+    const int d = g_D.load();  // the network may have changed since width() (sdf_l4c_configure)
+    t_grad.resize(d);
+    if (sdfnmpc_sdf_eval_host(g_ctx, g_net, 1, in, &t_df, t_grad.data()) != SDFNMPC_OK) {
         g_err = std::string("sdf_l4c: ") + sdfnmpc_last_error();
         t_gen = 0;
         return 1;
     }
-    memcpy(t_in, in, sizeof t_in);
+    t_in.assign(in, in + d);
     t_gen = gen;
     return 0;
 }
 
-// CasADi compressed-column sparsity patterns
+// CasADi compressed-column sparsity patterns of width D: dense D x 1 input, 1 x 1 output, dense 1 x D
+// Jacobian.  Kept per width for the life of the library (CasADi keeps the pointers it is handed).
 struct Sp {
-    long long in[2 + 2 + D], scalar[2 + 2 + 1], row[2 + D + 1 + D];
-    Sp() {
+    std::vector<long long> in, scalar, row;
+    explicit Sp(int D) : in(4 + D), scalar(5), row(2 + D + 1 + D) {
         in[0] = D; in[1] = 1; in[2] = 0; in[3] = D;
         for (int i = 0; i < D; ++i) in[4 + i] = i;
         scalar[0] = 1; scalar[1] = 1; scalar[2] = 0; scalar[3] = 1; scalar[4] = 0;
@@ -99,10 +112,20 @@ struct Sp {
         for (int j = 0; j < D; ++j) row[2 + D + 1 + j] = 0;
     }
 };
-const Sp& sp() {
-    static Sp s;
-    return s;
+const Sp* sp() {
+    static std::mutex mu;
+    static std::vector<Sp*> all;  // never freed: pointers handed out stay valid
+    const int D = width();
+    if (!D) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    for (Sp* s : all)
+        if ((int)s->in[0] == D) return s;
+    all.push_back(new Sp(D));
+    return all.back();
 }
+const long long* sp_in() { const Sp* s = sp(); return s ? s->in.data() : nullptr; }
+const long long* sp_scalar() { const Sp* s = sp(); return s ? s->scalar.data() : nullptr; }
+const long long* sp_row() { const Sp* s = sp(); return s ? s->row.data() : nullptr; }
 
 }  // namespace
 
@@ -119,6 +142,7 @@ int sdf_l4c_configure(const char* weights_path, int device) {
         sdfnmpc_ctx_destroy(g_ctx);
         g_ctx = nullptr;
     }
+    g_D.store(0);
     return init_locked(weights_path, device) ? 1 : 0;
 }
 const char* sdf_l4c_last_error(void) {  // a per-thread copy taken under the lock
@@ -135,8 +159,8 @@ int sdf_l4c(const double** arg, double** res, long long*, double*, int) {
 }
 long long sdf_l4c_n_in(void) { return 1; }
 long long sdf_l4c_n_out(void) { return 1; }
-const long long* sdf_l4c_sparsity_in(long long i) { return i == 0 ? sp().in : nullptr; }
-const long long* sdf_l4c_sparsity_out(long long i) { return i == 0 ? sp().scalar : nullptr; }
+const long long* sdf_l4c_sparsity_in(long long i) { return i == 0 ? sp_in() : nullptr; }
+const long long* sdf_l4c_sparsity_out(long long i) { return i == 0 ? sp_scalar() : nullptr; }
 int sdf_l4c_work(long long* a, long long* r, long long* iw, long long* w) {
     if (a) *a = 1;
     if (r) *r = 1;
@@ -154,13 +178,13 @@ void sdf_l4c_decref(void) {}
 // ---- jac_f
 int jac_sdf_l4c(const double** arg, double** res, long long*, double*, int) {
     if (!arg || !res || eval(arg[0])) return 1;
-    if (res[0]) memcpy(res[0], t_grad, sizeof t_grad);
+    if (res[0]) memcpy(res[0], t_grad.data(), t_grad.size() * sizeof(double));
     return 0;
 }
 long long jac_sdf_l4c_n_in(void) { return 2; }
 long long jac_sdf_l4c_n_out(void) { return 1; }
-const long long* jac_sdf_l4c_sparsity_in(long long i) { return i == 0 ? sp().in : (i == 1 ? sp().scalar : nullptr); }
-const long long* jac_sdf_l4c_sparsity_out(long long i) { return i == 0 ? sp().row : nullptr; }
+const long long* jac_sdf_l4c_sparsity_in(long long i) { return i == 0 ? sp_in() : (i == 1 ? sp_scalar() : nullptr); }
+const long long* jac_sdf_l4c_sparsity_out(long long i) { return i == 0 ? sp_row() : nullptr; }
 int jac_sdf_l4c_work(long long* a, long long* r, long long* iw, long long* w) {
     if (a) *a = 2;
     if (r) *r = 1;
@@ -174,15 +198,15 @@ int adj1_sdf_l4c(const double** arg, double** res, long long*, double*, int) {
     if (!arg || !res || eval(arg[0])) return 1;
     const double seed = arg[2] ? arg[2][0] : 0.0;
     if (res[0])
-        for (int i = 0; i < D; ++i) res[0][i] = seed * t_grad[i];
+        for (size_t i = 0; i < t_grad.size(); ++i) res[0][i] = seed * t_grad[i];
     return 0;
 }
 long long adj1_sdf_l4c_n_in(void) { return 3; }
 long long adj1_sdf_l4c_n_out(void) { return 1; }
 const long long* adj1_sdf_l4c_sparsity_in(long long i) {
-    return i == 0 ? sp().in : ((i == 1 || i == 2) ? sp().scalar : nullptr);
+    return i == 0 ? sp_in() : ((i == 1 || i == 2) ? sp_scalar() : nullptr);
 }
-const long long* adj1_sdf_l4c_sparsity_out(long long i) { return i == 0 ? sp().in : nullptr; }
+const long long* adj1_sdf_l4c_sparsity_out(long long i) { return i == 0 ? sp_in() : nullptr; }
 int adj1_sdf_l4c_work(long long* a, long long* r, long long* iw, long long* w) {
     if (a) *a = 3;
     if (r) *r = 1;

@@ -53,7 +53,10 @@ def rk4(x, u, dt, lim):
     return x + dt / 6 * (k1 + 2 * k2 + 2 * k3 + k4)
 
 
-def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None, sdf_cost: bool = False, nyN: int = 4):
+def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None, sdf_cost: bool = False, nyN: int = 4,
+                 v_forward: bool = False):
+    """v_forward: v0 along the camera's view (the body yaw) instead of U(+-3)^3, so the braking point of
+    flags.recursive_feasibility (gen_model.py:106-112) lies in the field of view, as in flight."""
     rng = np.random.default_rng(seed)
     lim = cfg.robot.limits
     L = int(cfg.nn.size_latent)
@@ -63,6 +66,10 @@ def make_problem(cfg, B: int, N: int, seed: int = 0, np_: int = 145, dt=None, sd
     eul = np.stack([rng.uniform(-0.3, 0.3, B), rng.uniform(-0.3, 0.3, B), rng.uniform(-np.pi, np.pi, B)], -1)
     q0 = euler2quat(eul)
     v0 = rng.uniform(-3, 3, (B, 3))
+    if v_forward:
+        vb = np.stack([rng.uniform(0.5, 2.5, B), rng.uniform(-0.4, 0.4, B), rng.uniform(-0.3, 0.3, B)], -1)
+        cy, sy = np.cos(eul[:, 2]), np.sin(eul[:, 2])
+        v0 = np.stack([cy * vb[:, 0] - sy * vb[:, 1], sy * vb[:, 0] + cy * vb[:, 1], vb[:, 2]], -1)
     x0 = np.concatenate([p0, q0, v0], -1)
     latent = rng.normal(size=(B, L))
     # current iterate: hover thrust + small perturbations, rolled out

@@ -1,0 +1,211 @@
+"""The flag space of default.yaml:16-23 on the GPU (gen_model.py:26-149): for every flag set of
+tests/flag_sets.py the preparation phase (linearize.hip + the SDF kernels only where a row or the cost reads
+the network) against the oracle, the QP kernel (the stage row count as a template parameter, soft / hard
+terminal rows) against the structured C IPM and the exact QP solution, the acados-style phase split, and the
+whole controller (Nmpc / Ocp over the solver object) against the oracle pipeline."""
+import numpy as np
+import pytest
+
+import flag_sets as F
+from sdf_nmpc_amd import _lib, synth, weights as W
+
+pytestmark = pytest.mark.gpu
+
+QP_TOL = 1e-8
+ORC_ATOL = 5e-6   # GPU vs the C restatement of the same IPM (same iterations; rounding differences)
+LIN_RTOL = 1e-9   # fp64 linearisation
+
+LIN = ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "hE", "JhE")
+OUT = LIN + ("dx", "du", "slack", "status", "iters", "res")
+
+
+def _config(name, N):
+    """The flag set's config at horizon N.  With recursive_feasibility the braking row's lower bound is
+    robot.size.xy (gen_model.py:118): the synthetic SIREN network has df ~ 0 everywhere (every point 'in'
+    an obstacle), so the hard row would demand ~0.8 of braking distance no input sequence can give; at
+    size.xy = -0.45 it is active on part of the batch and feasible."""
+    over = dict(robot__size__xy=-0.45) if F.FLAG_SETS[name][0].get("flags__recursive_feasibility") else {}
+    return F.config(name, mpc__N=N, **over)
+
+
+def _setup(gpu_ctx, name, B, N, seed, noise=0.05):
+    import torch
+    cfg = _config(name, N)
+    q = F.quad(name, cfg)
+    dev = torch.device("cuda", gpu_ctx.device)
+    # v0 along the camera's view: the braking point of the rec_feas rows lies in the field of view
+    prob = synth.make_problem(cfg, B, N, seed=seed, sdf_cost=q.sdf_cost, nyN=q.nyN, v_forward=True)
+    x0 = prob["x"][:, 0] + np.random.default_rng(seed).normal(0, noise, (B, 10))
+    t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
+         dict(x=prob["x"], u=prob["u"], p=prob["p"], dt=prob["dt"], x0=x0, yref=prob["yref"], W=prob["W"],
+              yNref=prob["yN"], WN=prob["WN"]).items()}
+    sh = dict(xn=(B, N, 10), AB=(B, N, 14, 10), y=(B, N, 11), Jy=(B, N, 14, 11), yN=(B, q.nyN), JyN=(B, 10, q.nyN),
+              h=(B, N + 1, 3), Jh=(B, N + 1, 10, 3), hE=(B, 6), JhE=(B, 10, 6), dx=(B, N + 1, 10), du=(B, N, 4),
+              slack=(B, N + 1, 3, 2), res=(B, 2))
+    for k, s in sh.items():
+        t[k] = torch.full(s, float("nan"), dtype=torch.float64, device=dev)
+    t["status"] = torch.full((B,), -1, dtype=torch.int32, device=dev)
+    t["iters"] = torch.full((B,), -1, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    return cfg, q, prob, x0, t
+
+
+def _net(gpu_ctx, q):
+    return _lib.Net.siren(gpu_ctx, 0) if q.enable_sdf else None
+
+
+def _np(t, keys):
+    return {k: t[k].cpu().numpy() for k in keys}
+
+
+@pytest.mark.parametrize("name", list(F.FLAG_SETS))
+def test_linearisation_per_flag_set(gpu_ctx, oracle_lib, name):
+    """sdfnmpc_linearize with the flag set's terminal extras (hE: braking row add-on, fov at Co_p_E, v_N),
+    residual width (nyN 5 with the flag-scaled stability residual) and no network where nothing reads it."""
+    B, N = 6, 20
+    cfg, q, prob, x0, t = _setup(gpu_ctx, name, B, N, seed=11)
+    _lib.linearize(gpu_ctx, _net(gpu_ctx, q), _lib.quad_model(cfg, q), B, N, q.np, t, nyN=q.nyN, no_sdf=not q.need_sdf)
+    gpu_ctx.synchronize()
+    got = _np(t, LIN)
+    onet = oracle_lib.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
+    ref = oracle_lib.linearize_batch(oracle_lib.quad_model(cfg), onet, prob["x"], prob["u"], prob["p"], prob["dt"], model=q)
+    for k in ("xn", "AB", "y", "Jy", "yN", "JyN"):
+        np.testing.assert_allclose(got[k], ref[k], rtol=LIN_RTOL, atol=1e-12 * max(1.0, np.abs(ref[k]).max()), err_msg=k)
+    for c in (0, 1):  # the fov functions are computed for every set (cheap), whichever are rows
+        np.testing.assert_allclose(got["h"][..., c], ref["h"][..., c], rtol=LIN_RTOL, atol=1e-12)
+        np.testing.assert_allclose(got["Jh"][..., c], ref["Jh"][..., c], rtol=LIN_RTOL, atol=1e-12)
+    if q.need_sdf:  # fp32 network: the SURVEY §8(d) bar
+        np.testing.assert_allclose(got["h"][..., 2], ref["h"][..., 2], rtol=0, atol=1e-5 * max(1.0, np.abs(ref["h"][..., 2]).max()))
+        np.testing.assert_allclose(got["Jh"][..., 2], ref["Jh"][..., 2], rtol=0, atol=1e-4 * max(1.0, np.abs(ref["Jh"][..., 2]).max()))
+    else:  # the SDF kernels did not run: the sdf column stays as it was (NaN here)
+        assert np.isnan(got["h"][..., 2]).all()
+    if q.rec_feas or q.stability:
+        for k in ("hE", "JhE"):
+            cols = slice(0, 6) if q.rec_feas else slice(3, 6)
+            np.testing.assert_allclose(got[k][..., cols], ref[k][..., cols], rtol=LIN_RTOL, atol=1e-11, err_msg=k)
+
+
+@pytest.mark.parametrize("name", list(F.FLAG_SETS))
+def test_qp_per_flag_set_vs_c_ipm_and_exact(gpu_ctx, oracle_lib, name):
+    """The QP kernel on the GPU linearisation of each flag set: the same iterations as the C restatement
+    (oracle/qp_ipm.c), du / dx within 5e-6 of it, and the exact solution's objective / convexity-ball bounds."""
+    import qp_oracle
+    B, N = 8, 20
+    cfg, q, prob, x0, t = _setup(gpu_ctx, name, B, N, seed=12)
+    _lib.linearize(gpu_ctx, _net(gpu_ctx, q), _lib.quad_model(cfg, q), B, N, q.np, t, nyN=q.nyN, no_sdf=not q.need_sdf)
+    _lib.qp_solve(gpu_ctx, _lib.qp_opts(q, tol=QP_TOL), B, N, t)
+    gpu_ctx.synchronize()
+    got = _np(t, OUT)
+    assert (got["status"] == 0).all(), got["iters"]
+    lin = {k: got[k] for k in LIN}
+    c = oracle_lib.qp_ipm_batch(lin, prob, x0, q, tol=QP_TOL)
+    assert (c["status"] == 0).all()
+    assert np.abs(got["iters"] - c["iters"]).max() <= 1, (got["iters"], c["iters"])
+    err = np.maximum(np.abs(got["du"] - c["du"]).max(axis=(1, 2)), np.abs(got["dx"] - c["dx"]).max(axis=(1, 2)))
+    assert (err <= ORC_ATOL).mean() >= 0.75, (err, got["iters"], c["iters"])
+    for b in range(B):
+        qq = qp_oracle.stage_qp({k: v[b] for k, v in lin.items()}, prob["x"][b], prob["u"][b], x0[b], prob["yref"][b],
+                                prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], q, 10.0)
+        H, g, E, e, G, d = qp_oracle.dense_problem(qq)
+        ex = qp_oracle.polish_active_set(qq, qp_oracle.solve_dense(qq))
+        sol = dict(dx=got["dx"][b], du=got["du"][b], sl=got["slack"][b][..., 0], su=got["slack"][b][..., 1])
+        z, zs = qp_oracle.z_of(qq, sol), qp_oracle.z_of(qq, ex)
+        Fz, Fs = 0.5 * z @ H @ z + g @ z, 0.5 * zs @ H @ zs + g @ zs
+        assert (G @ z + d).min() > -1e-7 and np.abs(E @ z - e).max() < 1e-8
+        assert Fz - Fs <= G.shape[0] * QP_TOL, (b, Fz - Fs)
+        n_xu = 10 * (N + 1) + 4 * N
+        mu = np.linalg.eigvalsh(H[:n_xu, :n_xu]).min()
+        assert np.linalg.norm(z[:n_xu] - zs[:n_xu]) <= np.sqrt(2 * max(Fz - Fs, 0.0) / mu) + 1e-6
+    # unused slack entries are zero: stage rows past nh, terminal rows past nsN
+    assert (got["slack"][:, :N, q.nh:] == 0).all() and (got["slack"][:, N, q.nsN:] == 0).all()
+
+
+@pytest.mark.parametrize("name", ["no_vfov", "lidar_sdf_only", "sdf_cost_only", "no_sdf", "rec_feas", "stability"])
+def test_phase_split_bitwise_per_flag_set(gpu_ctx, name):
+    """rti_prepare (records packed beside the SDF kernel; the sdf row of C^T -- row 1 with no_vfov, row 0 with
+    lidar_sdf_only -- patched by the QP kernel) + qp_feedback == linearize + qp_solve, bit for bit."""
+    B, N = 24, 20
+    cfg, q, prob, x0, ta = _setup(gpu_ctx, name, B, N, seed=13)
+    _, _, _, _, tb = _setup(gpu_ctx, name, B, N, seed=13)
+    net, qm, opts = _net(gpu_ctx, q), _lib.quad_model(cfg, q), _lib.qp_opts(q)
+    _lib.linearize(gpu_ctx, net, qm, B, N, q.np, ta, nyN=q.nyN, no_sdf=not q.need_sdf)
+    _lib.qp_solve(gpu_ctx, opts, B, N, ta)
+    _lib.rti_prepare(gpu_ctx, net, qm, opts, B, N, q.np, tb, no_sdf=not q.need_sdf)
+    _lib.qp_feedback(gpu_ctx, opts, B, N, tb)
+    gpu_ctx.synchronize()
+    a, b = _np(ta, OUT), _np(tb, OUT)
+    assert (a["status"] == 0).all()
+    for k in OUT:
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+
+
+def test_capacity_and_refusals(gpu_ctx):
+    """The occupancy gate per constraint set (LDS per instance follows the rows), and the ABI's refusals."""
+    base = gpu_ctx.qp_capacity(40)
+    assert gpu_ctx.qp_capacity(40, _lib.qp_opts(F.quad("default"))) == base
+    assert gpu_ctx.qp_capacity(40, _lib.qp_opts(F.quad("no_sdf"))) >= base
+    assert gpu_ctx.qp_capacity(40, _lib.qp_opts(F.quad("stability"))) >= 256
+    bad = _lib.qp_opts(F.quad("default"))
+    bad.h_col[1] = 0  # not increasing
+    with pytest.raises(_lib.SdfnmpcError):
+        gpu_ctx.qp_capacity(40, bad)
+    B, N = 2, 20
+    cfg, q, prob, x0, t = _setup(gpu_ctx, "stability", B, N, seed=1)
+    with pytest.raises(_lib.SdfnmpcError, match="nyN"):  # stability needs the 5-row terminal residual
+        _lib.linearize(gpu_ctx, _net(gpu_ctx, q), _lib.quad_model(cfg, q), B, N, q.np, t, nyN=4)
+    cfg, q, prob, x0, t = _setup(gpu_ctx, "default", B, N, seed=1)
+    with pytest.raises(_lib.SdfnmpcError, match="NULL network"):
+        _lib.linearize(gpu_ctx, None, _lib.quad_model(cfg, q), B, N, q.np, t)
+
+
+def _nmpc(name, B, N, seed):
+    from sdf_nmpc_amd.controller import Nmpc
+    from sdf_nmpc_amd.reference import Ref, yaw2quat
+    cfg = _config(name, N)
+    q = F.quad(name, cfg)
+    n = Nmpc(cfg, batch=B, braking_coeffs=q.poly if q.rec_feas else None)
+    rng = np.random.default_rng(seed)
+    x0 = np.zeros((B, 10))
+    x0[:, :3] = rng.uniform(-1, 1, (B, 3))
+    x0[:, 3:7] = np.stack([yaw2quat(y) for y in rng.uniform(-0.5, 0.5, B)])
+    x0[:, 7] = rng.uniform(0, 1.5, B)  # moving forward: the braking point ahead of the camera
+    n.set_sdf_flag(1.0)
+    n.set_latent(rng.normal(size=(B, 128)), x0[:, :3], np.stack([np.eye(3)] * B))
+    r = Ref(cfg)
+    r.p, r.q = np.array([4.0, 0.5, 1.0]), yaw2quat(0.1)
+    r.use_weights(r.W_on)
+    for k in range(N + 1):
+        n.set_ref(r, k)
+    n.set_x0(x0)
+    return n, q, x0
+
+
+@pytest.mark.parametrize("name", ["no_sdf", "no_sdf_constraint", "lidar", "rec_feas_soft_brake", "stability"])
+def test_controller_rti_step_per_flag_set(oracle_lib, name):
+    """Nmpc.solve (host setters, solver object) for a flag set: one SQP-RTI step against the oracle pipeline
+    (oracle linearisation + the C IPM) on the same iterate; u0 within 2e-5."""
+    B, N = 6, 20
+    n, q, x0 = _nmpc(name, B, N, seed=21)
+    xbar, ubar = n.ocp.download("x").copy(), n.ocp.download("u").copy()
+    xbar[:, 0] = x0
+    assert n.solve() == 0
+    u0 = n.get_u()
+    # the step's preparation phase (solver fields) against the oracle linearisation of the same iterate
+    glin = {k: n.ocp.download(k).reshape(B, *s) for k, s in dict(
+        xn=(N, 10), AB=(N, 14, 10), y=(N, 11), Jy=(N, 14, 11), yN=(q.nyN,), JyN=(10, q.nyN), h=(N + 1, 3),
+        Jh=(N + 1, 10, 3), hE=(6,), JhE=(10, 6)).items()}
+    onet = oracle_lib.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
+    lin = oracle_lib.linearize_batch(oracle_lib.quad_model(n.cfg), onet, xbar, ubar, n.p, n.ocp.dt, model=q)
+    for k in ("xn", "AB", "y", "Jy", "yN", "JyN"):
+        np.testing.assert_allclose(glin[k], lin[k], rtol=LIN_RTOL, atol=1e-12 * max(1.0, np.abs(lin[k]).max()), err_msg=k)
+    # the QP of that step against the C restatement on the step's own linearisation
+    prob = dict(x=xbar, u=ubar, yref=n.y, W=n.W, yN=n.yN, WN=n.WN, dt=n.ocp.dt)
+    r = oracle_lib.qp_ipm_batch(glin, prob, x0, q, tol=QP_TOL)
+    assert (r["status"] == 0).all()
+    np.testing.assert_allclose(u0, ubar[:, 0] + r["du"][:, 0], rtol=0, atol=2e-5)
+    if q.enable_sdf:  # Nmpc.eval: [sdf] (+ [poly(v), sdf - poly(v)] with rec_feas), flag = 1
+        ev = n.eval(N)
+        assert ev.shape == (B, 3 if q.rec_feas else 1)
+    else:
+        assert (n.eval(0) == 0).all()
+    n.ocp.close()

@@ -119,3 +119,53 @@ def test_variant_full_jacobian_host_path(gpu_ctx, golden, name):
     _check(df, gr, g, name, cols=D)  # the whole 1 x (3 + L) row: position and latent columns
     np.testing.assert_array_equal(df1[0], df[5])  # one row per call: the same as row 5 of the batch
     np.testing.assert_array_equal(gr1[0], gr[5])
+
+
+@pytest.mark.parametrize("name", ["sin_oct_full_L64", "softplus_cube_latent_L200", "relu_pos_none"])
+def test_l4c_shim_any_latent_size(golden, tmp_path, name):
+    """libsdf_l4c.so for a network with size_latent != 128: L4CasADi then emits sdf_l4c with
+    3 + L inputs (gen_model.py:39,60; neural_df.py:16).  The CasADi sparsity queries report the loaded
+    network's width, and sdf_l4c / jac_sdf_l4c / adj1_sdf_l4c, called one row at a time as acados calls
+    them, return the reference's own df and 1 x (3 + L) Jacobian (variants_golden.npz) to the variant bar."""
+    import ctypes
+    g, spec = golden["variants"], NET_VARIANTS[name]
+    D = 3 + spec.size_latent
+    wpath = tmp_path / f"{name}.sdfw"
+    W.save(str(wpath), spec, W.siren_weights(spec, SEED, bias_gain=BIAS_GAIN))
+    lib = ctypes.CDLL(_lib.L4C_PATH)
+    lib.sdf_l4c_configure.argtypes = [ctypes.c_char_p, ctypes.c_int]
+    lib.sdf_l4c_last_error.restype = ctypes.c_char_p
+    assert lib.sdf_l4c_configure(str(wpath).encode(), 0) == 0, lib.sdf_l4c_last_error()
+    LL = ctypes.POINTER(ctypes.c_longlong)
+    for f in ("sdf_l4c", "jac_sdf_l4c", "adj1_sdf_l4c"):
+        getattr(lib, f + "_sparsity_in").restype = LL
+        getattr(lib, f + "_sparsity_out").restype = LL
+        getattr(lib, f + "_sparsity_in").argtypes = [ctypes.c_longlong]
+        getattr(lib, f + "_sparsity_out").argtypes = [ctypes.c_longlong]
+    sin, sout, jout = lib.sdf_l4c_sparsity_in(0), lib.sdf_l4c_sparsity_out(0), lib.jac_sdf_l4c_sparsity_out(0)
+    assert (sin[0], sin[1], sin[2], sin[3]) == (D, 1, 0, D) and [sin[4 + i] for i in range(D)] == list(range(D))
+    assert (sout[0], sout[1]) == (1, 1)
+    assert (jout[0], jout[1]) == (1, D) and [jout[2 + j] for j in range(D + 1)] == list(range(D + 1))
+    assert lib.jac_sdf_l4c_sparsity_in(0)[0] == D and lib.adj1_sdf_l4c_sparsity_out(0)[0] == D
+    P = ctypes.POINTER(ctypes.c_double)
+    for fn in (lib.sdf_l4c, lib.jac_sdf_l4c, lib.adj1_sdf_l4c):
+        fn.argtypes = [ctypes.POINTER(P), ctypes.POINTER(P), ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    inp = variant_input(g, name).astype(np.float64)
+    n = 24
+    df, gr = np.zeros(n), np.zeros((n, D))
+    for i in range(n):
+        x = np.ascontiguousarray(inp[i])
+        out, jac, adj, seed = np.zeros(1), np.zeros(D), np.zeros(D), np.array([-2.0])
+        args = (P * 3)(x.ctypes.data_as(P), out.ctypes.data_as(P), seed.ctypes.data_as(P))
+        assert lib.sdf_l4c(args, (P * 1)(out.ctypes.data_as(P)), None, None, 0) == 0
+        assert lib.jac_sdf_l4c(args, (P * 1)(jac.ctypes.data_as(P)), None, None, 0) == 0
+        assert lib.adj1_sdf_l4c(args, (P * 1)(adj.ctypes.data_as(P)), None, None, 0) == 0
+        np.testing.assert_array_equal(adj, -2.0 * jac)
+        df[i], gr[i] = out[0], jac
+    sub = {k: (g[k][:n] if k.startswith(name + "/") else g[k]) for k in g.files if k.startswith(name + "/")}
+    _check(df, gr, sub, name, cols=D)
+    # back to the deployed net: the width follows the configured network
+    wdef = tmp_path / "sdf_l4c.sdfw"
+    W.save(str(wdef), W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
+    assert lib.sdf_l4c_configure(str(wdef).encode(), 0) == 0
+    assert lib.sdf_l4c_sparsity_in(0)[0] == 131

@@ -41,7 +41,7 @@ timeout -k 10 200 python3 $R/tools/qp_stamps.py > $O/qp_stamps.txt 2>&1
 # the segmented kernel: per-phase stamps (P = 4, B = 64 and 1024) and the serial / segmented sweep over B and N
 (cd $R && timeout -k 10 300 hipcc --offload-arch=gfx950 -O3 -std=c++17 -w -mllvm -amdgpu-mfma-vgpr-form -DSEG_STAMPS -I sdf-nmpc_amd/csrc \
     tools/seg_stamps_drv.hip sdf-nmpc_amd/csrc/rti_qp_seg.hip sdf-nmpc_amd/csrc/rti_qp.hip -o tools/_qp_stamps_drv_seg)
-(cd $R && P=4 timeout -k 10 250 bash tools/_segrun.sh && cp gpurun_out/seg_stamps_b64.log $O/seg_stamps_b64.txt && cp gpurun_out/seg_stamps.log $O/seg_stamps_b1024.txt)
+(cd $R && P=4 timeout -k 10 250 bash tools/seg_stamps.sh && cp gpurun_out/seg_stamps_b64.log $O/seg_stamps_b64.txt && cp gpurun_out/seg_stamps.log $O/seg_stamps_b1024.txt)
 (cd $R && for n in 40 60; do N=$n timeout -k 10 120 python3 tools/seg_sweep_b.py 1 8 64 256 512 1024 || exit 1; done) > $O/qp_kernel_sweep.txt 2>&1
 fi
 echo done
