@@ -33,7 +33,7 @@ path = os.path.join(os.environ.get("TMPDIR", "/tmp"), "qp_in.bin")
 os.makedirs(os.path.dirname(path), exist_ok=True)
 with open(path, "wb") as f:
     f.write(np.array([B, N], np.int32).tobytes())
-    for k in _lib.QP_IN:
+    for k in ("xn", "AB", "y", "Jy", "yN", "JyN", "h", "Jh", "x", "u", "x0", "yref", "W", "yNref", "WN", "dt"):  # the driver's order
         f.write(np.ascontiguousarray(t[k].double().cpu().numpy()).tobytes())
     f.write(np.concatenate([model.lbu, model.ubu, model.lh, model.uh, model.zl, model.Zl, [10.0, 1e-8]]).astype(np.float64).tobytes())
 del t; torch.cuda.synchronize()
