@@ -9,6 +9,8 @@
 #include <dlfcn.h>
 
 #include <atomic>
+#include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -44,13 +46,33 @@ std::string lib_dir() {
     return ".";
 }
 
-int init_locked(const char* path, int device) {
-    if (g_net) return 0;
+std::string weights_path(const char* path) {
     std::string wpath = path ? path : "";
     if (wpath.empty()) {
         const char* env = getenv("SDFNMPC_WEIGHTS");
         wpath = env && *env ? env : lib_dir() + "/sdf_l4c.sdfw";
     }
+    return wpath;
+}
+
+// 3 + size_latent from the .sdfw header (magic, version, nb_states, L, ...), without touching a device:
+// CasADi asks for the sparsity patterns when it builds the OCP, possibly on a host without the GPU
+int header_width(const std::string& wpath) {
+    FILE* f = fopen(wpath.c_str(), "rb");
+    if (!f) return 0;
+    unsigned char h[20];
+    const size_t n = fread(h, 1, sizeof h, f);
+    fclose(f);
+    uint32_t ver = 0, L = 0;
+    if (n != sizeof h || memcmp(h, "SDFNMPCW", 8) != 0) return 0;
+    memcpy(&ver, h + 8, 4);
+    memcpy(&L, h + 16, 4);
+    return (ver == 1 || ver == 2) && L <= 4096 ? 3 + (int)L : 0;
+}
+
+int init_locked(const char* path, int device) {
+    if (g_net) return 0;
+    const std::string wpath = weights_path(path);
     if (device < 0) {
         const char* env = getenv("SDFNMPC_DEVICE");
         device = env && *env ? atoi(env) : 0;
@@ -69,13 +91,21 @@ int init_locked(const char* path, int device) {
     return 0;
 }
 
-// the input width, loading the network on first use (CasADi asks for the sparsity before any call);
-// 0 when no network could be loaded (the error is in sdf_l4c_last_error)
+std::string g_cfg_path;  // the weights path of the last sdf_l4c_configure (guarded by g_mu)
+
+constexpr int DEPLOYED_WIDTH = 3 + 128;  // the deployed network's input (default.yaml nn.size_latent)
+std::atomic<int> g_handed{0};            // the width of the last sparsity pattern handed to CasADi
+
+// the input width: the loaded network's, else the header of the file the first call will load
+// (CasADi asks for the sparsity before any call, possibly on a host without the GPU), else the
+// deployed network's
 int width() {
     const int d = g_D.load();
     if (d) return d;
     std::lock_guard<std::mutex> lk(g_mu);
-    return init_locked(nullptr, -1) ? 0 : g_D.load();
+    if (g_D.load()) return g_D.load();
+    const int w = header_width(weights_path(g_cfg_path.empty() ? nullptr : g_cfg_path.c_str()));
+    return w ? w : DEPLOYED_WIDTH;
 }
 
 // value + gradient for one input, cached per thread
@@ -88,6 +118,13 @@ int eval(const double* in) {
     if (init_locked(nullptr, -1)) return 1;
     const unsigned long long gen = g_gen.load();
     const int d = g_D.load();  // the network may have changed since width() (sdf_l4c_configure)
+    const int hw = g_handed.load();
+    if (hw && hw != d) {  // CasADi sized its buffers from a pattern of another width
+        g_err = "sdf_l4c: the loaded network takes " + std::to_string(d) + " inputs, the sparsity pattern handed out " +
+                std::to_string(hw);
+        t_gen = 0;
+        return 1;
+    }
     t_grad.resize(d);
     if (sdfnmpc_sdf_eval_host(g_ctx, g_net, 1, in, &t_df, t_grad.data()) != SDFNMPC_OK) {
         g_err = std::string("sdf_l4c: ") + sdfnmpc_last_error();
@@ -117,6 +154,7 @@ const Sp* sp() {
     static std::vector<Sp*> all;  // never freed: pointers handed out stay valid
     const int D = width();
     if (!D) return nullptr;
+    g_handed.store(D);
     std::lock_guard<std::mutex> lk(mu);
     for (Sp* s : all)
         if ((int)s->in[0] == D) return s;
@@ -143,6 +181,8 @@ int sdf_l4c_configure(const char* weights_path, int device) {
         g_ctx = nullptr;
     }
     g_D.store(0);
+    g_handed.store(0);  // an explicit reconfiguration: the caller sizes its buffers anew
+    g_cfg_path = weights_path ? weights_path : "";
     return init_locked(weights_path, device) ? 1 : 0;
 }
 const char* sdf_l4c_last_error(void) {  // a per-thread copy taken under the lock
