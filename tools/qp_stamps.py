@@ -23,7 +23,7 @@ t = {k: torch.from_numpy(np.ascontiguousarray(v)).to(dev) for k, v in
      dict(x=prob["x"], u=prob["u"], p=prob["p"], dt=prob["dt"], x0=x0, yref=prob["yref"], W=prob["W"],
           yNref=prob["yN"], WN=prob["WN"]).items()}
 sh = dict(xn=(B, N, 10), AB=(B, N, 14, 10), y=(B, N, 11), Jy=(B, N, 14, 11), yN=(B, 4), JyN=(B, 10, 4),
-          h=(B, N + 1, 3), Jh=(B, N + 1, 10, 3))
+          h=(B, N + 1, 3), Jh=(B, N + 1, 10, 3), hE=(B, 6), JhE=(B, 10, 6))
 for k, s in sh.items():
     t[k] = torch.zeros(s, dtype=torch.float64, device=dev)
 torch.cuda.synchronize()
