@@ -94,3 +94,51 @@ def test_scene_closed_loop_sdf_rows_activate_and_release(oracle_lib, warm):
     assert not active[-5:].any()
     assert (xg[:, 0] > 3.6).all()
     ocp.close()
+
+
+def test_scene_c3_full_size_active_rows_vs_oracle(oracle_lib):
+    """C3's size (1024 instances x N = 40) on the scene net, where the SDF rows are active in a large share
+    of the instances (the setup of bench.py's scene leg: starts spread over x in [0, 2.5] m and lateral
+    offsets in [-1, 1.5] m, the loop closed with a perfect-model plant).  After six warm steps, at two
+    steps, 24 instances with an active SDF soft row and 8 without are pinned to the oracle pipeline (the C
+    linearisation and the structured C IPM at the iterate the GPU step linearised at): u_0 of the step."""
+    O = oracle_lib
+    B, N = 1024, 40
+    cfg = Config(mpc__N=N)
+    ocp = Ocp(Quad(cfg), batch=B, weights=S.SCENE)
+    n = Nmpc(cfg, batch=B, ocp=ocp)
+    rng = np.random.default_rng(77)
+    x = S.setup(n, y0=rng.uniform(-1.0, 1.5, B))
+    x[:, 0] = rng.uniform(0.0, 2.5, B)
+    with open(S.SCENE, "rb") as f:
+        onet = O.Net(*W.unpack(f.read()))
+    try:
+        for _ in range(6):
+            n.set_x0(x)
+            assert n.solve() == 0
+            x = n.get_matrices()[0][:, 1].copy()
+        for step in range(2):
+            n.set_x0(x)
+            xs, us = (a.copy() for a in n.get_matrices())  # the iterate this step linearises at (mpc.shift = 0)
+            assert n.solve() == 0 and (ocp.status == 0).all()
+            u0 = n.get_u().copy()
+            act = (ocp.download("slack").reshape(B, N + 1, 3, 2)[:, :, 2, 0] > 1e-6).any(axis=1)
+            pick = np.concatenate([np.flatnonzero(act)[:24], np.flatnonzero(~act)[:8]])
+            xi, ui = xs[pick], us[pick]
+            xi[:, 0] = x[pick]
+            lin = O.linearize_batch(O.quad_model(cfg), onet, xi, ui, n.p[pick], ocp.dt)
+            prob = {"yref": n.y[pick], "W": n.W[pick], "yN": n.yN[pick], "WN": n.WN[pick], "dt": ocp.dt, "x": xi,
+                    "u": ui}
+            r = O.qp_ipm_batch(lin, prob, x[pick], n.model, nthreads=8)
+            assert (r["status"] == 0).all()
+            d = np.abs(u0[pick] - (ui[:, 0] + r["du"][:, 0])).max(axis=1)
+            oact = (r["slack"][:, :, 2, 0] > 1e-6).any(axis=1)
+            print(f"\nstep {step}: SDF row active in {act.mean():.0%} of {B}; sample max |u0 - u0_oracle| "
+                  f"{d.max():.2e}; oracle agrees on activity in {np.mean(oact == act[pick]):.0%}; GPU iterations "
+                  f"max {ocp.iters.max()}")
+            assert act.mean() >= 0.25 and len(pick) == 32
+            assert d.max() <= U0_ATOL, d
+            assert (oact == act[pick]).mean() >= 0.9
+            x = n.get_matrices()[0][:, 1].copy()
+    finally:
+        ocp.close()
