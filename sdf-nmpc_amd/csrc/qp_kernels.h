@@ -52,17 +52,12 @@ inline void qp_default_rows(QpArgs& q) {
 }
 
 constexpr int QP_REC = 304;   // stage record: [A B | c | g | C^T | H upper | 0 ..] (128-B rows) (rti_qp.hip)
-constexpr int QP_FREC = 192;  // factor record: 16 x 12 column-major [A~ 0 b~; chol(R^), P c pairs; K 0 k_ff] (rti_qp.hip)
+constexpr int QP_FREC = 192;  // factor record: [A~|b~ | K|k_ff (rows of 12) | chol(R^) (1/diag) | P_{k+1} c_k | 4 junk]
 #ifndef QP_RING_DEPTH
 #define QP_RING_DEPTH 3
 #endif
-#ifndef QP_FRING_DEPTH
-#define QP_FRING_DEPTH 8
-#endif
 constexpr int QP_RING = QP_RING_DEPTH;  // stream positions in flight per wavefront
-constexpr int QP_FRING = QP_FRING_DEPTH;  // forward-sweep nodes in flight (its own register ring)
-constexpr int QP_SLOT = 5;    // 64-double loads per stream position
-constexpr int QP_WIN = 344;   // committed LDS window (the corrector's remapped factor record + R[96, 224))
+constexpr int QP_SLOT = 5;    // 64-double loads per stream position (committed LDS window = 320 doubles)
 // segmented kernel (rti_qp_seg.hip): four wavefronts per instance, each a segment of the horizon
 constexpr int QP_NSEG = 4;  // at most
 constexpr int QP_FRECS = 368;  // its factor record: rows (+ chol(R^), kf_pred) | J c | Z | c, g, B, C^T copies | G | junk
@@ -92,9 +87,9 @@ __host__ __device__ inline size_t qp_lds_doubles(int N, QpRows q) {
            + 2 * qp_even(N1 * 10)           // dx, dxc
            + 3 * qp_even((size_t)N * 4)     // du, dua, duc
            + 2 * qp_even(G)                 // cxa, cxc
-           + QP_WIN                         // committed stream window
-           + QP_RING * QP_FREC              // factor records of nodes 0..RING-1 (written late in a backward sweep)
-           + 24 + 2                         // zero rows; junk
+           + QP_SLOT * 64                   // committed stream window
+           + QP_RING * 168                  // [A~|b~ K|k_ff] of nodes 0..RING-1 (written late in a backward sweep)
+           + 48 + 2                         // zero rows; junk
            + qp_even((size_t)N * 4) + qp_even(G) + qp_even(N1)  // u, h per group, s_k
            + 2 * qp_even(G)                 // folds (w, gamma) per group
            + 2 * qp_even((size_t)N * 4)     // box terms (diag, v)

@@ -48,40 +48,32 @@ namespace {
 
 using namespace qpd;
 
-// factor record: the 16 x 12 matrix M, column-major (element (a, x) at 16 x + a), which is the A operand
-// layout of the f64 16x16x4 MFMA: k-step s of lane (g, c) is M[c][4 s + g] = F[64 s + lane], one
-// coalesced load per k-step.  Rows 0..9: [A~ | 0 | b~], rows 12..15: [K | 0 | k_ff] (column 10 is zero,
-// column 11 multiplies a constant 1), so that one chained MFMA triple per node is the forward step
-// [x_{k+1}; u_k] = M [x_k; 0; 1].  Rows 10, 11 (whose products the forward stage discards) hold the
-// corrector's uniform pairs: chol(R^) (lower packed, diagonal 1/L_ii) at columns 0..4, P_{k+1} c_k at
-// columns 5..9; (10, 10) is a junk slot.
-constexpr int F_B = 16 * 11, F_KF = F_B + 12, F_J = 16 * 10 + 10, FREC = QP_FREC;  // b~ | k_ff (column 11); junk
-__host__ __device__ constexpr int f_at(int a, int x) { return 16 * x + a; }
-__host__ __device__ constexpr int f_pair(int x) { return 16 * x + 10; }  // (row 10, row 11) of column x
-constexpr int F_FW = FREC;  // the LDS copy of nodes < PD (fsave) mirrors the whole record
-constexpr int SLOT = QP_SLOT, PD = QP_RING, DF = QP_FRING;
+// factor record: [A~|b~ 10 x 12 | K|k_ff 4 x 12 | L 10 (lower packed, diagonal 1/L_ii) | P c 10 | junk 2]; rows are
+// 12 doubles (11 used) so that a forward stage reads its row with five 16-byte LDS reads
+constexpr int F_AB = 0, F_K = 10 * FR, F_L = 14 * FR, F_PC = F_L + 10, F_J = F_PC + 10, FREC = QP_FREC;
+constexpr int F_FW = 14 * FR;  // forward sweeps read [0, F_FW)
+constexpr int SLOT = QP_SLOT, PD = QP_RING;
 // Window of one stream position per sweep kind: n_loads(K) loads of 64 consecutive doubles (lanes
-// clamped to the record), load j landing at window offset 64 j (kind 3: the factor part remapped):
+// clamped to the record), load j landing at window offset 64 j:
 //   0 initial forward     R[0, 256)                    AB, c, C^T in place
 //   1 backward factor     R[0, 320)                    the stage record in place; [R_Z, 320) reads 0
-//   3 backward corrector  F[0, 192) | R[96, 224)       F[e] at e + 2 (e / 16) (columns of M 18 doubles apart:
-//                                                      the per-lane column reads hit distinct banks);
-//                                                      R[i] at WB_R + i (i >= 96; loads start on a 128-byte line)
-// The forward sweeps (2, 4) use no window: the shared ring carries only their C operand (one gather)
-// for nodes < PD (M from fsave), and the forward loop streams its other nodes through its own ring.
-constexpr int WF_END = FREC + 2 * (FREC / 16), WB_R = WF_END - 96, WIN = QP_WIN;
-__host__ __device__ constexpr int wf_at(int e) { return e + 2 * (e >> 4); }
-static_assert((WB_R + R_G + NX) % 2 == 0 && (WB_R + R_AB + 100) % 2 == 0, "16-byte blocks of the corrector window");
-__host__ __device__ constexpr int n_loads(int K) { return (K == 1 || K == 3) ? 5 : (K == 0) ? 4 : 1; }
-__host__ __device__ constexpr bool load_f(int K, int j) { return K == 3 && j < 3; }
-__host__ __device__ constexpr int load_at(int K, int j) { return (K == 0 || K == 1 || j < 3) ? 64 * j : 96 + 64 * (j - 3); }
+//   2, 4 forward          F[0, 192) | R[164, 228)      factor rows at 0, C^T at WF_CT
+//   3 backward corrector  F[0, 192) | R[96, 224)       factor record at 0, R[i] at WB_R + i (i >= 96; loads
+//                                                      start on a 128-byte line)
+constexpr int WF_CT = 192, WB_R = 192 - 96;
+static_assert((WB_R + R_G + NX) % 2 == 0, "g~_u block of the corrector window is 16-byte aligned");
+__host__ __device__ constexpr int n_loads(int K) { return (K == 1 || K == 3) ? 5 : 4; }
+__host__ __device__ constexpr bool load_f(int K, int j) { return (K == 2 || K == 3 || K == 4) ? j < 3 : false; }
+__host__ __device__ constexpr int load_at(int K, int j) {
+    return (K == 0 || K == 1) ? 64 * j : (K == 2 || K == 4) ? (j < 3 ? 64 * j : R_CT) : (j < 3 ? 64 * j : 96 + 64 * (j - 3));
+}
 // extent of each record a sweep kind reads (lanes past it load the last needed element again, so a
 // 64-lane load touches only the cache lines the stage uses)
-__host__ __device__ constexpr int f_end(int K) { return FREC; }
+__host__ __device__ constexpr int f_end(int K) { return (K == 2 || K == 4) ? F_FW : F_J; }
 __host__ __device__ constexpr int r_end(int K) { return K == 1 ? REC : R_CT + 30; }
-static_assert((REC * 8) % 128 == 0 && FREC == 192 && PD >= 2 && SLOT == 5 && DF >= 2, "record layout");
-static_assert(WIN >= 64 * SLOT && WIN >= WB_R + 96 + 128 && WB_R + R_G + 14 <= WIN && (96 * 8) % 128 == 0 && R_Z < 64 * SLOT &&
-              wf_at(FREC - 1) < WF_END, "window layout");
+static_assert(FREC == F_J + 4 && (REC * 8) % 128 == 0 && (FREC * 8) % 128 == 0 && F_FW <= WF_CT && FREC <= 192 && PD >= 2 && SLOT == 5, "record layout");
+static_assert(WB_R + R_G + 14 <= 64 * SLOT && WF_CT + 30 <= 64 * SLOT && WB_R + 96 + 128 <= 64 * SLOT && (96 * 8) % 128 == 0 && R_Z < 64 * SLOT,
+              "window layout");
 
 template <typename Fn, int... S>
 __device__ __forceinline__ void for_each_ic(Fn& fn, std::integer_sequence<int, S...>) {
@@ -94,8 +86,8 @@ struct Smem {
     ldsd *du, *dua, *duc;          // iterate du; affine / corrector du
     ldsd *cxa, *cxc;               // C dx of the affine / corrector solution, per group
     ldsd* win;                     // committed stream window
-    ldsd* fsave;                   // factor records (M) of nodes < PD
-    ldsd *zero, *junk;             // 24 doubles that stay 0 (zero rows for strided reads); a store sink
+    ldsd* fsave;                   // [A~|b~ K|k_ff] of nodes < PD
+    ldsd *zero, *junk;             // 48 doubles that stay 0 (zero rows for strided reads); a store sink
     ldsd *uu, *hv, *skv;           // u (box constants), h per group, cost scaling per node
     ldsd *fw, *fg, *bd, *bv;       // folds per group (w, gamma), box terms [N][4] (diag, v)
     ldsd* cst;                     // lbu 4 | ubu 4 | (lh, uh, zl, Zl) of stage rows 0..2 | of terminal rows 0..7
@@ -115,8 +107,8 @@ __device__ __forceinline__ Smem carve(ldsd* q, int N, QpRows rw) {  // mirrors q
     s.dx = take(N1 * NX); s.dxc = take(N1 * NX);
     s.du = take(N * NU); s.dua = take(N * NU); s.duc = take(N * NU);
     s.cxa = take(G); s.cxc = take(G);
-    s.win = take(WIN); s.fsave = take(PD * F_FW);
-    s.zero = take(24); s.junk = take(2);
+    s.win = take(SLOT * 64); s.fsave = take(PD * F_FW);
+    s.zero = take(48); s.junk = take(2);
     s.uu = take(N * NU); s.hv = take(G); s.skv = take(N1);
     s.fw = take(G); s.fg = take(G); s.bd = take(N * NU); s.bv = take(N * NU);
     s.cst = take(8 + 4 * (3 + QP_NHN));
@@ -154,7 +146,7 @@ __device__ __forceinline__ FConst fconst(int lane) {
     f.gj = g < NSS ? g : 0;
     // closed loop: [A | c][a][c] at ab01 + 4 r (r = 0, 1), ab2; A operand B[a = c][g] at bmi
     const bool xcol = c < NX || c == 14;  // columns of [P | p], [A | c], [K | k_ff]
-    const int xo = c < NX ? c : 11;       // their column of M
+    const int xo = c < NX ? c : 10;       // their column in the 11-wide factor-record rows
     f.ab01 = opaque(xcol ? (c < NX ? c : 14) * 10 + g : R_Z);
     f.ab2 = opaque((xcol && g < 2) ? (c < NX ? c : 14) * 10 + g + 8 : R_Z);
     f.bmi = opaque(c < NX ? (NX + g) * 10 + c : R_Z);
@@ -162,10 +154,10 @@ __device__ __forceinline__ FConst fconst(int lane) {
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const int a = g + 4 * r;
-        f.spc[r] = (unsigned)opaque((c == 14 && a < NX) ? 8 * (f_pair(5 + a / 2) + (a & 1)) : FJB);
-        f.sab[r] = (unsigned)opaque((xcol && a < NX) ? 8 * f_at(a, xo) : FJB);
+        f.spc[r] = (unsigned)opaque((c == 14 && a < NX) ? 8 * (F_PC + a) : FJB);
+        f.sab[r] = (unsigned)opaque((xcol && a < NX) ? 8 * (F_AB + a * FR + xo) : FJB);
     }
-    f.sk_ = (unsigned)opaque(xcol ? 8 * f_at(12 + g, xo) : FJB);
+    f.sk_ = (unsigned)opaque(xcol ? 8 * (F_K + g * FR + xo) : FJB);
     // Joseph form operands (window indices; R_Z reads 0):  A operand H^_xu[c][g] (c < 10);
     // A operand R^0[c][g] = H_uu[c][g] (+ box diagonal, c < 4); C init H^[10 + g][c] of V's row g
     f.hxu_i = opaque(c < NX ? R_H + tri14(c, NX + g) : R_Z);
@@ -438,11 +430,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         __threadfence_block();  // stored before any lane of the wave streams the records
     }
     if (lane < NX) s.dx[lane] = A.x0[(size_t)b * 10 + lane] - A.x[(size_t)b * N1 * 10 + lane];
-    if (lane < 24) s.zero[lane] = 0.0;
-    // column 10 of M multiplies a don't-care entry of the forward operand: keep it 0 (finite) in the
-    // records and in their LDS copies, which the sweeps never write there (except the junk slot)
-    for (int e = lane; e < N1 * 16; e += 64) F[(size_t)(e >> 4) * FREC + f_at(e & 15, 10)] = 0.0;
-    for (int e = lane; e < PD * F_FW; e += 64) s.fsave[e] = 0.0;
+    if (lane < 48) s.zero[lane] = 0.0;
     __syncthreads();
     STAMP(0);
 
@@ -456,36 +444,23 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     double ring[PD][SLOT];
     // fn(IC<S>) for the ring slots S = 0 .. PD - 1 in order (static slots: the loops are unrolled by PD)
     auto each_slot = [](auto&& fn) { for_each_ic(fn, std::make_integer_sequence<int, PD>{}); };
-    // C operand of the forward stage's 4x4x4 product C x_k (block b = c >> 2 covers x[4 b .. 4 b + 3]):
-    // lane (g, c) holds C[c & 3][4 (c >> 2) + g], gathered from the C^T field (0 outside C)
-    const int fc3 = lane & 3, fcb = (lane >> 2) & 3, fg = lane >> 4;
-    const bool cq_live = fc3 < NS && fcb < 3 && 4 * fcb + fg < NX;
-    const int cq_i = R_CT + 10 * (fc3 < NS ? fc3 : 0) + (4 * fcb + fg < NX ? 4 * fcb + fg : 0);
     auto issue = [&](auto KIc, double* rs, int q) {
         constexpr int KI = decltype(KIc)::value;
         const int qq = q < N ? q : N;
         const int k = (KI == 1 || KI == 3) ? N - qq : qq;
         const double* rb = R + (size_t)k * REC;
         const double* fb = F + (size_t)k * FREC;
-        if constexpr (KI == 2 || KI == 4) {
-            rs[0] = rb[cq_i];
-        } else {
 #pragma unroll
-            for (int j = 0; j < n_loads(KI); ++j) {
-                const int e = load_at(KI, j) + lane;
-                if (load_f(KI, j)) rs[j] = fb[e < f_end(KI) ? e : f_end(KI) - 1];
-                else rs[j] = rb[e < r_end(KI) ? e : r_end(KI) - 1];
-            }
+        for (int j = 0; j < n_loads(KI); ++j) {
+            const int e = load_at(KI, j) + lane;
+            if (load_f(KI, j)) rs[j] = fb[e < f_end(KI) ? e : f_end(KI) - 1];
+            else rs[j] = rb[e < r_end(KI) ? e : r_end(KI) - 1];
         }
     };
-    const int wfl = lane + 2 * (lane >> 4);  // wf_at(64 j + lane) = 72 j + wfl
     auto commit = [&](auto Kc, const double* rs) {
         constexpr int K = decltype(Kc)::value;
 #pragma unroll
-        for (int j = 0; j < n_loads(K); ++j) {
-            if constexpr (K == 3) win[j < 3 ? 72 * j + wfl : WB_R + 96 + 64 * (j - 3) + lane] = rs[j];
-            else win[lane + 64 * j] = rs[j];
-        }
+        for (int j = 0; j < n_loads(K); ++j) win[lane + 64 * j] = rs[j];
     };
 
     // box rows (k, i, up): t = +-du + d, d = (u - lbu) | (ubu - u)
@@ -494,25 +469,42 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         return up ? s.cst[4 + i] - u : u - s.cst[0 + i];
     };
 
-    // ------------------------------------------------------------ initial forward stage (kind 0)
-    // lane r < 10: row r of A x + c + B du (x_{k+1} of the start iterate); r = 14..16: (C x)_{r-14}
+    // ------------------------------------------------------------ forward stage
+    // lane r < 10: row r of A~ x + b~ (x_{k+1}); r = 10..13: row of K x + k_ff (u_k); r = 14..16:
+    // (C x)_{r-14}; kind 0 (initial iterate, u = 0): rows r < 10 of A x + c from the stage record.
+    // Factor rows of nodes < PD come from fsave (written late in the backward sweeps).
     double chain = 0.0;  // p_{k+1} of the corrector sweep in lanes 0..9
     auto fw_stage = [&](auto Kc, int k, const int lane) {
-        const bool fx = lane < NX, fc = lane >= 14 && lane < 14 + NS;
+        const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 14 + NS;
         const int fcj = fc ? lane - 14 : 0;
-        ldsd* const dxo = s.dx;
-        ldsd* const cxo = s.cxa;
-        double row[NX];
-        const ldsd* rp = fx ? win + R_AB + lane : fc ? win + R_CT + fcj * 10 : win;
-        const int str = fx ? 10 : 1;
+        constexpr int K = decltype(Kc)::value;
+        ldsd* const dxo = K == 0 ? s.dx : s.dxc;
+        ldsd* const duo = K == 4 ? s.duc : s.dua;
+        ldsd* const cxo = K == 4 ? s.cxc : s.cxa;
+        double row[NX], off;
+        if constexpr (K == 0) {
+            const ldsd* rp = fx ? win + R_AB + lane : fc ? win + R_CT + fcj * 10 : win;
+            const int str = fx ? 10 : 1;
 #pragma unroll
-        for (int l = 0; l < NX; ++l) row[l] = rp[l * str];
-        double off = *(fx ? win + R_C + lane : s.zero);
-        // + B du_k of the start iterate (0 on a cold start): B[r][j] at R_AB + 10 (NX + j) + r
-        const int bx = fx ? lane : 0, ku = k < N ? k : N - 1;
-        const double bdu = win[R_AB + 100 + bx] * s.du[ku * NU] + win[R_AB + 110 + bx] * s.du[ku * NU + 1] +
-                           win[R_AB + 120 + bx] * s.du[ku * NU + 2] + win[R_AB + 130 + bx] * s.du[ku * NU + 3];
-        off += (fx ? 1.0 : 0.0) * bdu;
+            for (int l = 0; l < NX; ++l) row[l] = rp[l * str];
+            off = *(fx ? win + R_C + lane : s.zero);
+            // + B du_k of the start iterate (0 on a cold start): B[r][j] at R_AB + 10 (NX + j) + r
+            const int bx = fx ? lane : 0, ku = k < N ? k : N - 1;
+            const double bdu = win[R_AB + 100 + bx] * s.du[ku * NU] + win[R_AB + 110 + bx] * s.du[ku * NU + 1] +
+                               win[R_AB + 120 + bx] * s.du[ku * NU + 2] + win[R_AB + 130 + bx] * s.du[ku * NU + 3];
+            off += (fx ? 1.0 : 0.0) * bdu;
+        } else {
+            const ldsd* fk = k < PD ? s.fsave + k * F_FW : win;
+            // 16-byte aligned rows: [A~ | b~] / [K | k_ff] row `lane`, C^T row lane - 14, zeros
+            const ldsd2* rp = (const ldsd2*)(lane < 14 ? fk + lane * FR : fc ? win + WF_CT + fcj * 10 : s.zero);
+#pragma unroll
+            for (int l = 0; l < NX / 2; ++l) {
+                const d2 v = rp[l];
+                row[2 * l] = v.x;
+                row[2 * l + 1] = v.y;
+            }
+            off = *(lane < 14 ? fk + lane * FR + 10 : s.zero);
+        }
         const ldsd2* xp = (const ldsd2*)(dxo + k * NX);
         d2 xv[NX / 2];  // the chain input x_k, read after everything else
 #pragma unroll
@@ -526,85 +518,10 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         }
         const double z = a0 + a1;
         // the terminal node's rows are formed after the sweep (term_cx): any row set, C rows from LDS
-        ldsd* dst = (fc && k < N) ? cxo + k * NS + fcj : (k < N && fx) ? dxo + (k + 1) * NX + lane : s.junk;
+        ldsd* dst = (fc && k < N) ? cxo + k * NS + fcj
+                  : (k < N && fx) ? dxo + (k + 1) * NX + lane
+                  : (K != 0 && k < N && fu) ? duo + k * NU + lane - NX : s.junk;
         *dst = z;
-    };
-
-    // ------------------------------------------------------------ forward sweeps (kinds 2, 4)
-    // [x_{k+1}; *; u_k] = M_k [x_k; 0; 1] as three chained f64 16x16x4 MFMAs: the accumulator of one
-    // node is the B operand of the next with no lane movement (k-step s of lane (g, c) is register s of
-    // the accumulator, row g + 4 s; all 16 columns are equal), except rows 10, 11 of k-step 2, which are
-    // set to (0, 1).  C x_k runs off the chain on one 4x4x4 MFMA (its three blocks are the three k-steps,
-    // summed over the blocks by two DPP row rotations).  Nodes < PD read M from fsave and their C operand
-    // from the shared ring (loaded during the preceding backward sweep); the other nodes stream M (three
-    // coalesced loads) and the C operand through a DF-deep register ring of their own, which the stage
-    // time (three dependent MFMAs) needs to cover the memory latency.  Lanes with c = 0 store
-    // x_{k+1}, u_k and C x_k into LDS for the row phases.
-    auto fw_sweep = [&](auto Kc) {
-        constexpr int K = decltype(Kc)::value, KN = K == 4 ? 1 : 3;
-        const int ln = opaque(lane);
-        const int g = ln >> 4, c = ln & 15, cb = (c >> 2) & 3;
-        const bool xs = g < 2, fst = c == 0, cst_ = fst && g < NS, ust = fst, x2st = fst && g < 2;
-        const double xk = g == 3 ? 1.0 : 0.0;
-        const bool cb0 = cb == 0, cb1 = cb == 1;
-        ldsd* const dxo = s.dxc;
-        ldsd* const duo = K == 4 ? s.duc : s.dua;
-        ldsd* const cxo = K == 4 ? s.cxc : s.cxa;
-        double xb0 = dxo[g], xb1 = dxo[4 + g], xb2 = xs ? dxo[8 + (xs ? g : 0)] : xk;
-        const d4 z4 = {0.0, 0.0, 0.0, 0.0};
-        auto fstage = [&](int k, double m0, double m1, double m2, double cq) {
-            d4 D = mfma(m0, xb0, z4);
-            D = mfma(m1, xb1, D);
-            D = mfma(m2, xb2, D);
-            // off the chain: C x_k (the block of lane c covers x[4 (c >> 2) ..])
-            const double xbc = cb0 ? xb0 : cb1 ? xb1 : xb2;
-            double P = mfma4(cq_live ? cq : 0.0, xbc, 0.0);
-            P += dpp64<0x124, 0xF>(P, 0.0);  // row_ror:4
-            P += dpp64<0x128, 0xF>(P, 0.0);  // row_ror:8
-            xb0 = D[0];
-            xb1 = D[1];
-            xb2 = xs ? D[2] : xk;
-            ldsd* xo = dxo + (k + 1) * NX;
-            if (fst) {
-                xo[g] = D[0];
-                xo[4 + g] = D[1];
-            }
-            if (x2st) xo[8 + g] = D[2];
-            if (ust) duo[k * NU + g] = D[3];
-            if (cst_) cxo[k * NS + g] = P;
-        };
-        double fr[DF][4];
-        auto fissue = [&](double* rs, int k) {
-            const int kk = k < N ? k : N - 1;
-            const double* fb = F + (size_t)kk * FREC + ln;
-#pragma unroll
-            for (int j = 0; j < 3; ++j) rs[j] = fb[64 * j];
-            rs[3] = R[(size_t)kk * REC + cq_i];
-        };
-        // the forward ring first (its loads overlap the fsave nodes), then the fsave nodes (their C
-        // operands in the shared ring), then the next sweep's first positions into the shared ring
-#pragma unroll
-        for (int j = 0; j < DF; ++j) fissue(fr[j], PD + j);
-        each_slot([&](auto Sc) {
-            constexpr int S = decltype(Sc)::value;
-            if (S < N) {
-                const ldsd* fs = s.fsave + S * F_FW + ln;
-                fstage(S, fs[0], fs[64], fs[128], ring[S][0]);
-            }
-        });
-        each_slot([&](auto Sc) { issue(IC<KN>{}, ring[decltype(Sc)::value], decltype(Sc)::value); });
-        for (int q0 = PD; q0 < N; q0 += DF) {
-#pragma unroll
-            for (int j = 0; j < DF; ++j) {
-                const int q = q0 + j;
-                if (q < N) {
-                    const double m0 = fr[j][0], m1 = fr[j][1], m2 = fr[j][2], cq = fr[j][3];
-                    fissue(fr[j], q + DF);
-                    fstage(q, m0, m1, m2, cq);
-                }
-            }
-        }
-        wave_sync();
     };
 
     // C dx_N of the terminal rows into cxo[NGS + j] (after a forward sweep): lane j < nhN, the fw_stage's
@@ -628,7 +545,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     // Lane maps (fixed for the solve): accumulator rows a_r = g + 4 r of column c; operand k-step st
     // covers k = 4 st + g.  Every lane-dependent read is a precomputed window index (R_Z: a zero) and
     // every store of an inactive lane goes to a junk slot.
-    auto fs_at = [&](int k, int e) -> ldsd* { return s.fsave + k * F_FW + e; };  // e < FREC
+    auto fs_at = [&](int k, int e) -> ldsd* { return e < F_FW ? s.fsave + k * F_FW + e : s.junk; };
 
 #define FBST(v, off) bst(v, rsF, off, sko)
     d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
@@ -766,12 +683,8 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         // ---- factor record (and its LDS copy for the first forward stages)
         FBST(kg, sk_);
         {  // the (uniform) Cholesky factor: every lane stores the same 16 bytes, no lane selection
-            double* Fk = F + (size_t)k * FREC;
-            *(d2*)(Fk + f_pair(0)) = d2{i0, l10};
-            *(d2*)(Fk + f_pair(1)) = d2{i1, l20};
-            *(d2*)(Fk + f_pair(2)) = d2{l21, i2};
-            *(d2*)(Fk + f_pair(3)) = d2{l30, l31};
-            *(d2*)(Fk + f_pair(4)) = d2{l32, i3};
+            d2* Lp = (d2*)(F + (size_t)k * FREC + F_L);
+            Lp[0] = d2{i0, l10}; Lp[1] = d2{i1, l20}; Lp[2] = d2{l21, i2}; Lp[3] = d2{l30, l31}; Lp[4] = d2{l32, i3};
         }
 #pragma unroll
         for (int r = 0; r < 3; ++r) FBST(Ab[r], sab[r]);
@@ -790,17 +703,17 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     auto bc_stage = [&](auto Fc, int q, const int lane) {
         constexpr bool FIRST = decltype(Fc)::value;
         const bool fx = lane < NX, fu = lane >= NX && lane < 14;
-        // column `lane` of A~ (the window holds column x of M at 18 x) | column lane - 10 of B
-        const ldsd2* bc_row = (const ldsd2*)(fx ? win + wf_at(f_at(0, lane)) : fu ? win + WB_R + lane * 10 : win);
-        const ldsd* bc_ct = fx ? win + WB_R + R_CT + lane : s.zero;          // C^T[j][r] at + 10 j
-        const ldsd2* bc_k = (const ldsd2*)(fx ? win + wf_at(f_at(12, lane)) : s.zero);  // K[i][r] at + i
+        const ldsd* bc_row = fx ? win + F_AB + lane : fu ? win + WB_R + lane * 10 : win;
+        const int bc_str = fx ? FR : 1;
+        const ldsd* bc_ct = fx ? win + WB_R + R_CT + lane : s.zero;  // C^T[j][r] at + 10 j
+        const ldsd* bc_k = fx ? win + F_K + lane : s.zero;           // K[i][r] at + FR i
         const ldsd* bc_g = lane < 14 ? win + WB_R + R_G + lane : s.zero;
         const double mfx = fx ? 1.0 : 0.0;
         double mu_[NU];
     #pragma unroll
         for (int i = 0; i < NU; ++i) mu_[i] = lane == NX + i ? 1.0 : 0.0;
         const int bx = fx ? lane : 0;
-        const unsigned bc_st = fx ? F_B + lane : fu ? F_KF + lane - NX : F_J;  // b~ rows (lanes < 10), k_ff rows (10..13)
+        const unsigned bc_st = lane < 14 ? lane * FR + 10 : F_J;  // b~ rows (lanes < 10), k_ff rows (lanes 10..13)
         const int k = N - q;
         FSTAMP(7, mfx);
         double off = *bc_g;
@@ -821,21 +734,17 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             bvv[0] = b0.x; bvv[1] = b0.y; bvv[2] = b1.x; bvv[3] = b1.y;
             guw[0] = g0.x; guw[1] = g0.y; guw[2] = g1.x; guw[3] = g1.y;
         }
-        {
-            const d2 k01 = bc_k[0], k23 = bc_k[1];
-            kk[0] = k01.x; kk[1] = k01.y; kk[2] = k23.x; kk[3] = k23.y;
-        }
+#pragma unroll
+        for (int i = 0; i < NU; ++i) kk[i] = bc_k[FR * i];
+#pragma unroll
+        for (int l = 0; l < NX; ++l) row[l] = bc_row[l * bc_str];
+        const ldsd2* pc = (const ldsd2*)(win + F_PC);
+        const ldsd2* Lq = (const ldsd2*)(win + F_L);
+        d2 pcv[NX / 2], Lv[5];
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) {
-            const d2 v = bc_row[l];
-            row[2 * l] = v.x;
-            row[2 * l + 1] = v.y;
-        }
-        d2 pcv[NX / 2], Lv[5];  // uniform pairs (rows 10, 11 of M)
-#pragma unroll
-        for (int l = 0; l < NX / 2; ++l) {
-            pcv[l] = *(const ldsd2*)(win + wf_at(f_pair(5 + l)));
-            Lv[l] = *(const ldsd2*)(win + wf_at(f_pair(l)));
+            pcv[l] = pc[l];
+            Lv[l] = Lq[l];
         }
         const double cb = win[WB_R + R_C + bx], B0 = win[WB_R + 100 + bx], B1 = win[WB_R + 110 + bx];
         const double B2 = win[WB_R + 120 + bx], B3 = win[WB_R + 130 + bx];
@@ -1349,7 +1258,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         STAMP(2);
         if (lane < NX) s.dxc[lane] = s.dx[lane];
         wave_sync();
-        fw_sweep(IC<2>{});
+        sweep(IC<2>{});
         term_cx(s.cxa, s.dxc);
         STAMP(3);
         const double sigmu = rows_pred();
@@ -1360,7 +1269,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         STAMP(5);
         if (lane < NX) s.dxc[lane] = s.dx[lane];
         wave_sync();
-        fw_sweep(IC<4>{});
+        sweep(IC<4>{});
         term_cx(s.cxc, s.dxc);
         STAMP(3);
         rows_update(sigmu);
