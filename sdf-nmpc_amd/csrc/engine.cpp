@@ -1656,7 +1656,7 @@ struct sdfnmpc_vae {
     void* dmem = nullptr;
     VaeLayer stem, conv[11], head;  // conv: b0a b0s b0b b1a b1s b1b b2a b2s b2b b3a b3b
     const unsigned short* stem_wpl = nullptr;  // the stem weights split into bf16 planes (VaeStemArgs::wpl)
-    const float* zero16 = nullptr;              // 16 zero floats (VaeConvArgs::zero16)
+    const float* zero16 = nullptr;              // 16 zero floats (VaeConvArgs::zero: a tap outside the map)
     DevBuf ws;
     int ws_B = 0;
 };
@@ -1706,7 +1706,7 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
     }
     // + the stem weights split exactly into three bf16 planes [3][64 n][64 k] (vae_enc.hip's split3), in
     // the kernel's K order (vae_stem_slot_tap), appended after the layers (16-byte aligned), then every
-    // ResBlock convolution's weights split the same way into planes [3][Cout][K] (16-byte aligned each)
+    // ResBlock convolution's weights split the same way into planes of K-tile slabs (16-byte aligned each)
     auto split3 = [](float x, unsigned short* hi, unsigned short* mid, unsigned short* lo) {
         uint32_t u, hb, mb, lb;
         memcpy(&u, &x, 4);
@@ -1752,7 +1752,18 @@ extern "C" int sdfnmpc_vae_load(sdfnmpc_ctx* ctx, const void* blob, size_t bytes
         } else {
             memcpy(&dev[off], src + off, nw * 4);
             unsigned short* pl = (unsigned short*)&dev[cpl_off[li]];
-            for (size_t e = 0; e < nw; ++e) split3(src[off + e], &pl[e], &pl[nw + e], &pl[2 * nw + e]);
+            // K-tile slabs in vae_conv_kernel's K order (channel block, ky, kx): weight (n, ky, kx, ci) goes
+            // to K-tile t = (ci / 16) KS KS + ky KS + kx, plane element ((n / 128 KT + t) 128 + n % 128) 16
+            // + ci % 16 with the two 8-element halves of rows with bit 3 set swapped -- the LDS image of the
+            // kernel's B tile, so its LDS-DMA reads 1 KB contiguous per wave (one slab: 4 KB per plane)
+            const int KK = s.ks * s.ks, K = KK * s.cin, KT = K / 16;
+            for (int n = 0; n < s.cout; ++n)
+                for (int k = 0; k < K; ++k) {
+                    const int tp = k / s.cin, ci = k % s.cin, t = (ci / 16) * KK + tp, c = ci % 16;
+                    const int r = n % 128, h = (c / 8) ^ ((r >> 3) & 1);
+                    const size_t e = (((size_t)(n / 128) * KT + t) * 128 + r) * 16 + 8 * h + c % 8;
+                    split3(src[off + (size_t)n * K + k], &pl[e], &pl[nw + e], &pl[2 * nw + e]);
+                }
         }
         memcpy(&dev[off + nw], src + off + nw, (size_t)s.cout * 4);
         off += nw + s.cout;
@@ -1800,7 +1811,8 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
     const int B = o->B;
     if (B == 0) return SDFNMPC_OK;
     ScopedDevice sd(ctx->device);
-    // workspace: pre [B][H][W] | X | Y (block in/out ping-pong) | T (conv_a) | S (shortcut) | F (head features)
+    // workspace: pre [B][H][W] | X | Y (block in/out ping-pong, bf16 planes) | T (conv_a, planes) | S (shortcut,
+    // fp32) | F (head features).  A planes tensor of n values per image: [3][B][n] bf16, plane stride B n.
     const size_t n_pre = (size_t)v->H * v->W;
     size_t n_x = (size_t)v->Hp * v->Wp * 64, n_t = 0;
     for (int k = 0; k < 4; ++k) {
@@ -1808,40 +1820,55 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
         n_x = std::max(n_x, nb);
         n_t = std::max(n_t, nb);
     }
-    const size_t per = n_pre + 2 * n_x + 2 * n_t + 2048;
+    // in floats per image: planes take 1.5 floats a value (n_x, n_t are multiples of 64: every plane 16-byte aligned)
+    const size_t per = n_pre + 2 * (3 * n_x / 2) + 3 * n_t / 2 + n_t + 2048;
     HIPCHK(v->ws.ensure(per * B * sizeof(float)));
     float* P = (float*)v->ws.p;
-    float* X = P + n_pre * B;
-    float* Y = X + n_x * B;
-    float* T = Y + n_x * B;
-    float* S = T + n_t * B;
+    unsigned short* X = (unsigned short*)(P + n_pre * B);
+    unsigned short* Y = X + 3 * n_x * B;
+    unsigned short* T = Y + 3 * n_x * B;
+    float* S = (float*)(T + 3 * n_t * B);
     float* F = S + n_t * B;  // [B][2048] pooled head features
+    const unsigned short* zero = (const unsigned short*)v->zero16;
     hipStream_t st = ctx->stream;
     VaePreArgs pa{img, o->dtype, B, o->in_h, o->in_w, v->H, v->W, o->clip, o->yz, P};
     HIPCHK(timed(ctx, "vae_pre", [&] { return launch_vae_pre(pa, st); }));
-    VaeStemArgs sa{P, v->stem_wpl, v->stem.b, X, B, v->H, v->W, v->Hc, v->Wc, v->Hp, v->Wp};
+    size_t xps = (size_t)B * v->Hp * v->Wp * 64;  // the plane stride of the tensor in X
+    // a map read by a stride-2 convolution is stored in parity-phase column order (vae_col)
+    auto phased = [](int k) { return k < 4 && kVaeBlockStride[k] == 2 ? 1 : 0; };
+    VaeStemArgs sa{P, v->stem_wpl, v->stem.b, X, xps, B, v->H, v->W, v->Hc, v->Wc, v->Hp, v->Wp, phased(0)};
     HIPCHK(timed(ctx, "vae_stem", [&] { return launch_vae_stem(sa, ctx->n_cu, st); }));
     int h = v->Hp, w = v->Wp, li = 0;
     for (int k = 0; k < 4; ++k) {
         const int s = kVaeBlockStride[k], ho = v->bh[k], wo = v->bw[k];
         const VaeLayer& ca = v->conv[li++];
-        VaeConvArgs a1{X, ca.w, ca.wpl, ca.b, v->zero16, nullptr, T, B, h, w, ca.cin, ho, wo, ca.cout, 1};
+        const size_t ops = (size_t)B * ho * wo * ca.cout;  // plane stride of this block's outputs
+        const int in_ph = phased(k), out_ph = phased(k + 1);
+        VaeConvArgs a1{X, xps, ca.w, ca.wpl, ca.b, zero, nullptr, nullptr, 0, nullptr, T, ops,
+                       B, h, w, ca.cin, ho, wo, ca.cout, 1, in_ph, 0, 0};
         HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a1, 3, s, st); }));
-        const float* resid = X;
+        const float* resid = nullptr;
+        const unsigned short* resid_pl = X;  // identity shortcut: the block input, as planes
+        int res_ph = in_ph;
         if (s != 1) {
             const VaeLayer& cs = v->conv[li++];
-            VaeConvArgs a2{X, cs.w, cs.wpl, cs.b, v->zero16, nullptr, S, B, h, w, cs.cin, ho, wo, cs.cout, 0};
+            VaeConvArgs a2{X, xps, cs.w, cs.wpl, cs.b, zero, nullptr, nullptr, 0, S, nullptr, 0,
+                           B, h, w, cs.cin, ho, wo, cs.cout, 0, in_ph, out_ph, 0};
             HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a2, 1, s, st); }));
             resid = S;
+            resid_pl = nullptr;
+            res_ph = out_ph;
         }
         const VaeLayer& cb = v->conv[li++];
-        VaeConvArgs a3{T, cb.w, cb.wpl, cb.b, v->zero16, resid, Y, B, ho, wo, cb.cin, ho, wo, cb.cout, 1};
+        VaeConvArgs a3{T, ops, cb.w, cb.wpl, cb.b, zero, resid, resid_pl, xps, nullptr, Y, ops,
+                       B, ho, wo, cb.cin, ho, wo, cb.cout, 1, 0, out_ph, res_ph};
         HIPCHK(timed(ctx, "vae_conv", [&] { return launch_vae_conv(a3, 3, 1, st); }));
         std::swap(X, Y);
+        xps = ops;
         h = ho;
         w = wo;
     }
-    VaeHeadArgs ha{X, F, v->head.w, v->head.b, latent, latent64, B, h, w, v->L};
+    VaeHeadArgs ha{X, xps, F, v->head.w, v->head.b, latent, latent64, B, h, w, v->L};
     HIPCHK(timed(ctx, "vae_head", [&] { return launch_vae_head(ha, st); }));
     return SDFNMPC_OK;
 }

@@ -10,9 +10,10 @@
 // Model: quad_rollpitchyawrate.py:19-55 ('att'), utils/math.py:7-54,169-192; constraints
 // cost_const_helpers.py:48-75 (add_fov_const_trigo) and gen_model.py:46-70 (sdf with flag).
 //
-// Derivatives are forward-mode dual numbers with ONE tangent per lane: a node is served by 16
-// lanes, lane t < 14 carrying d/d(x,u)_t, so every lane writes one Jacobian column (column-major
-// blocks, 80-112 contiguous bytes per lane).  The sdf row of h / J_h is written by sdf_mlp_kernel's
+// Derivatives are forward-mode dual numbers with ONE tangent per lane: a node is served by 8 lanes,
+// each carrying one of the eight directions whose Jacobian columns are not constants of the model
+// (linearize_kernel), so every lane writes one or two Jacobian columns (column-major blocks, 80-112
+// contiguous bytes per column).  The sdf row of h / J_h is written by sdf_mlp_kernel's
 // epilogue, so this kernel is independent of the network and runs concurrently with it.
 #include <hip/hip_runtime.h>
 
@@ -42,9 +43,16 @@ __device__ __forceinline__ dd datan2(dd y, dd x) {
     return {atan2(y.v, x.v), (x.v * y.t - y.v * x.t) / den};
 }
 
-// 1 / sqrt(a) as a dual number: one fp64 sqrt + one division
+// 1 / sqrt(a) as a dual number (a > 0): the hardware estimate and two Newton steps y += y (1 - a y^2) / 2
+// (each squares the relative error: within an ulp or two of the rounded 1 / sqrt(a), 8 instructions in
+// place of a correctly rounded sqrt and division)
 __device__ __forceinline__ dd drsqrt(dd a) {
-    const double r = 1.0 / sqrt(a.v);
+    double r = __builtin_amdgcn_rsq(a.v);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+        const double e = __builtin_fma(-(a.v * r), r, 1.0);
+        r = __builtin_fma(0.5 * r, e, r);
+    }
     return {r, -0.5 * a.t * r * r * r};
 }
 
@@ -90,22 +98,31 @@ __device__ __forceinline__ dd qerr3(const dd* x, const double* qd) {
 #ifndef LIN_WAVES
 #define LIN_WAVES 1
 #endif
+// Eight lanes per node.  f_expl does not depend on the position and only f[0:3] = v depends on the
+// velocity, so the columns of [A|B], J_y for d/dp and d/dv are constants (the dual evaluation would give
+// exactly these: d x+/dp_j = e_j; d x+/dv_j = ((h b1 + h b2) + h b3) + h b4 e_j + e_{7+j}, summed in the
+// RK4 accumulation's order; J_y: unit columns) and the lanes carry the eight others: slot s -> direction
+// q_{s} (s < 4) or u_{s-4}.  The fov rows of J_h depend on the position only: slots 0..2 seed p_s there.
+// The terminal node (all ten directions of x) takes two passes.
 __global__ __launch_bounds__(256, LIN_WAVES) void linearize_kernel(LinArgs A) {
     const int tid = threadIdx.x;
-    const int t = tid & 15;                           // tangent direction of this lane
-    const long long r = (long long)blockIdx.x * 16 + (tid >> 4);  // node row = b * (N+1) + k
+    const int sl = tid & 7;                           // lane slot within the node
+    const long long r = (long long)blockIdx.x * 32 + (tid >> 3);  // node row = b * (N+1) + k
     const int N = A.N, N1 = A.N + 1;
     if (r >= (long long)A.B * N1) return;
     const long long b = r / N1;
     const int k = (int)(r - b * N1);
     const QuadModel& m = A.m;
-
     const double* xr = A.x + r * 10;
-    dd X[10];
+    double xv[10];
 #pragma unroll
-    for (int i = 0; i < 10; ++i) X[i] = {xr[i], (i == t) ? 1.0 : 0.0};
+    for (int i = 0; i < 10; ++i) xv[i] = xr[i];
 
     if (k < N) {
+        const int t = sl < 4 ? 3 + sl : 6 + sl;  // the tangent direction of this lane: q0..q3, u0..u3
+        dd X[10];
+#pragma unroll
+        for (int i = 0; i < 10; ++i) X[i] = {xv[i], (i == t) ? 1.0 : 0.0};
         const long long s = b * N + k;
         const double* ur = A.u + s * 4;
         dd U[4];
@@ -134,114 +151,134 @@ __global__ __launch_bounds__(256, LIN_WAVES) void linearize_kernel(LinArgs A) {
 #pragma unroll
             for (int i = 0; i < 10; ++i) xo[i] = xo[i] + kk[i] * hb[st];
         }
-        double* ABc = A.AB + (s * 14 + t) * 10;
+        double* AB = A.AB + s * 140;
 #pragma unroll
-        for (int i = 0; i < 10; ++i) {
-            if (t < 14) ABc[i] = xo[i].t;
-            if (t == i) A.xn[s * 10 + i] = xo[i].v;
+        for (int i = 0; i < 10; ++i) AB[t * 10 + i] = xo[i].t;
+        if (sl < 6) {  // the constant columns p_j (sl = j) and v_j (sl = 3 + j)
+            const int j = sl < 3 ? sl : sl - 3, col = sl < 3 ? j : 7 + j;
+            const double hs = ((hb[0] + hb[1]) + hb[2]) + hb[3];
+#pragma unroll
+            for (int i = 0; i < 10; ++i) AB[col * 10 + i] = (i == col) ? 1.0 : (sl >= 3 && i == j) ? hs : 0.0;
         }
+#pragma unroll
+        for (int i = 0; i < 10; ++i)
+            if (i == sl || i == sl + 8) A.xn[s * 10 + i] = xo[i].v;
         // ---- NONLINEAR_LS residual (quad_rollpitchyawrate.py:48-55)
         const double* pr = A.p + r * A.np;
         const dd qe3 = qerr3(X, pr + 13);  // p_idx.q_d
         dd Y[11] = {X[0], X[1], X[2], qe3, X[7], X[8], X[9], roll, pitch, wz, W_a2};
-        double* Jyc = A.Jy + (s * 14 + t) * 11;
+        double* Jy = A.Jy + s * 154;
 #pragma unroll
-        for (int i = 0; i < 11; ++i) {
-            if (t < 14) Jyc[i] = Y[i].t;
-            if (t == i) A.y[s * 11 + i] = Y[i].v;
+        for (int i = 0; i < 11; ++i) Jy[t * 11 + i] = Y[i].t;
+        if (sl < 6) {  // y = [p, qe3, v, ...]: unit columns for p_j -> row j, v_j -> row 4 + j
+            const int col = sl < 3 ? sl : 4 + sl, row = sl < 3 ? sl : 1 + sl;
+#pragma unroll
+            for (int i = 0; i < 11; ++i) Jy[col * 11 + i] = (i == row) ? 1.0 : 0.0;
         }
+#pragma unroll
+        for (int i = 0; i < 11; ++i)
+            if (i == sl || i == sl + 8) A.y[s * 11 + i] = Y[i].v;
     } else {
         // ---- terminal residual y_N = [p, q_e[3]]; with flags.stability scaled by the flag, plus the
-        //      stability cost row flag |v|^2 (quad_rollpitchyawrate.py:52-55, gen_model.py:142-149)
+        //      stability cost row flag |v|^2 (quad_rollpitchyawrate.py:52-55, gen_model.py:142-149);
+        //      directions sl and sl + 8
         const double* pr = A.p + r * A.np;
-        const dd qe3 = qerr3(X, pr + 13);
         const int nyN = A.nyN;
         const double fl = m.stability ? pr[0] : 1.0;
-        const dd Y[5] = {X[0] * fl, X[1] * fl, X[2] * fl, qe3 * fl, ((X[7] * X[7] + X[8] * X[8]) + X[9] * X[9]) * pr[0]};
-        if (t < 10) {
+        for (int t = sl; t < 10; t += 8) {
+            dd X[10];
+#pragma unroll
+            for (int i = 0; i < 10; ++i) X[i] = {xv[i], (i == t) ? 1.0 : 0.0};
+            const dd qe3 = qerr3(X, pr + 13);
+            const dd Y[5] = {X[0] * fl, X[1] * fl, X[2] * fl, qe3 * fl, ((X[7] * X[7] + X[8] * X[8]) + X[9] * X[9]) * pr[0]};
             double* J = A.JyN + (b * 10 + t) * nyN;
 #pragma unroll
             for (int i = 0; i < 5; ++i)
                 if (i < nyN) J[i] = Y[i].t;
-        }
 #pragma unroll
-        for (int i = 0; i < 5; ++i)
-            if (t == i && i < nyN) A.yN[b * nyN + i] = Y[i].v;
-        if (m.rec_feas | m.stability) {
-            // ---- terminal extras (gen_model.py:81-121): -flag poly(v), the fov functions at
-            //      Co_p_E = W_R_Co^T (p + poly(v) v / sqrt(|v|^2 + 1e-4) - W_p_Co) + B_R_C^T B_p_C + [off, 0, 0]
-            //      (braking_dist_flag with the flag forced to 1, gen_model.py:86-87,110), and v
-            dd H[6] = {C(0.0), C(0.0), C(0.0), X[7], X[8], X[9]};
-            if (m.rec_feas) {
-                const int deg = m.poly_deg;
-                dd pw[3][7];  // v_i^a, a <= 6
+            for (int i = 0; i < 5; ++i)
+                if (t == i && i < nyN) A.yN[b * nyN + i] = Y[i].v;
+            if (m.rec_feas | m.stability) {
+                // ---- terminal extras (gen_model.py:81-121): -flag poly(v), the fov functions at
+                //      Co_p_E = W_R_Co^T (p + poly(v) v / sqrt(|v|^2 + 1e-4) - W_p_Co) + B_R_C^T B_p_C + [off, 0, 0]
+                //      (braking_dist_flag with the flag forced to 1, gen_model.py:86-87,110), and v
+                dd H[6] = {C(0.0), C(0.0), C(0.0), X[7], X[8], X[9]};
+                if (m.rec_feas) {
+                    const int deg = m.poly_deg;
+                    dd pw[3][7];  // v_i^a, a <= 6
 #pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    pw[i][0] = C(1.0);
+                    for (int i = 0; i < 3; ++i) {
+                        pw[i][0] = C(1.0);
 #pragma unroll
-                    for (int a = 1; a < 7; ++a) pw[i][a] = pw[i][a - 1] * X[7 + i];
-                }
-                dd poly = C(0.0);
-                int q = 0;  // polynomial_3variate's order (utils/math.py:307-314)
-                for (int d = 0; d <= deg; ++d)
-                    for (int a = 0; a <= d; ++a)
-                        for (int bb = 0; bb <= d - a; ++bb, ++q) {
-                            dd pa = C(1.0), pb = C(1.0), pc = C(1.0);
+                        for (int a = 1; a < 7; ++a) pw[i][a] = pw[i][a - 1] * X[7 + i];
+                    }
+                    dd poly = C(0.0);
+                    int q = 0;  // polynomial_3variate's order (utils/math.py:307-314)
+                    for (int d = 0; d <= deg; ++d)
+                        for (int a = 0; a <= d; ++a)
+                            for (int bb = 0; bb <= d - a; ++bb, ++q) {
+                                dd pa = C(1.0), pb = C(1.0), pc = C(1.0);
 #pragma unroll
-                            for (int e = 0; e < 7; ++e) {
-                                if (e == a) pa = pw[0][e];
-                                if (e == bb) pb = pw[1][e];
-                                if (e == d - a - bb) pc = pw[2][e];
+                                for (int e = 0; e < 7; ++e) {
+                                    if (e == a) pa = pw[0][e];
+                                    if (e == bb) pb = pw[1][e];
+                                    if (e == d - a - bb) pc = pw[2][e];
+                                }
+                                poly = poly + ((pa * pb) * pc) * m.poly[q];
                             }
-                            poly = poly + ((pa * pb) * pc) * m.poly[q];
-                        }
-                H[0] = -(poly * pr[0]);
-                const dd nrm = dsqrt(((X[7] * X[7] + X[8] * X[8]) + X[9] * X[9]) + C(1e-4));
-                const dd sc = poly / nrm;
-                const double* R = pr + 4;
-                const dd e0 = (X[0] + X[7] * sc) - C(pr[1]), e1 = (X[1] + X[8] * sc) - C(pr[2]),
-                         e2 = (X[2] + X[9] * sc) - C(pr[3]);
-                const dd cx = (e0 * R[0] + e1 * R[3]) + e2 * R[6] + C(m.fov_off[0]);
-                const dd cy = (e0 * R[1] + e1 * R[4]) + e2 * R[7] + C(m.fov_off[1]);
-                const dd cz = (e0 * R[2] + e1 * R[5]) + e2 * R[8] + C(m.fov_off[2]);
-                H[1] = datan2(cy, cx) * pr[0];
-                H[2] = datan2(cz, dsqrt(cx * cx + cy * cy)) * pr[0];
-            }
-            if (t < 10) {
-                double* J = A.JhE + (b * 10 + t) * 6;
+                    H[0] = -(poly * pr[0]);
+                    const dd nrm = dsqrt(((X[7] * X[7] + X[8] * X[8]) + X[9] * X[9]) + C(1e-4));
+                    const dd sc = poly / nrm;
+                    const double* R = pr + 4;
+                    const dd e0 = (X[0] + X[7] * sc) - C(pr[1]), e1 = (X[1] + X[8] * sc) - C(pr[2]),
+                             e2 = (X[2] + X[9] * sc) - C(pr[3]);
+                    const dd cx = (e0 * R[0] + e1 * R[3]) + e2 * R[6] + C(m.fov_off[0]);
+                    const dd cy = (e0 * R[1] + e1 * R[4]) + e2 * R[7] + C(m.fov_off[1]);
+                    const dd cz = (e0 * R[2] + e1 * R[5]) + e2 * R[8] + C(m.fov_off[2]);
+                    H[1] = datan2(cy, cx) * pr[0];
+                    H[2] = datan2(cz, dsqrt(cx * cx + cy * cy)) * pr[0];
+                }
+                double* JE = A.JhE + (b * 10 + t) * 6;
 #pragma unroll
-                for (int i = 0; i < 6; ++i) J[i] = H[i].t;
-            }
+                for (int i = 0; i < 6; ++i) JE[i] = H[i].t;
 #pragma unroll
-            for (int i = 0; i < 6; ++i)
-                if (t == i) A.hE[b * 6 + i] = H[i].v;
+                for (int i = 0; i < 6; ++i)
+                    if (t == i) A.hE[b * 6 + i] = H[i].v;
+            }
         }
     }
 
-    // ---- constraints h = [hfov, vfov, sdf] (cost_const_helpers.py:48-75, gen_model.py:46-61)
+    // ---- constraints h = [hfov, vfov, sdf] (cost_const_helpers.py:48-75, gen_model.py:46-61): functions
+    //      of the position only; slot sl < 3 carries d/dp_sl
     const double* pr = A.p + r * A.np;
     const double flag = pr[0];
     const double Wp0 = pr[1], Wp1 = pr[2], Wp2 = pr[3];
     const double* R = pr + 4;  // W_R_Co row-major (== casadi reshape((3,3)).T)
-    const dd e0 = X[0] - C(Wp0), e1 = X[1] - C(Wp1), e2 = X[2] - C(Wp2);
+    const dd e0 = {xv[0] - Wp0, sl == 0 ? 1.0 : 0.0}, e1 = {xv[1] - Wp1, sl == 1 ? 1.0 : 0.0},
+             e2 = {xv[2] - Wp2, sl == 2 ? 1.0 : 0.0};
     const dd cx = (e0 * R[0] + e1 * R[3]) + e2 * R[6] + C(m.fov_off[0]);
     const dd cy = (e0 * R[1] + e1 * R[4]) + e2 * R[7] + C(m.fov_off[1]);
     const dd cz = (e0 * R[2] + e1 * R[5]) + e2 * R[8] + C(m.fov_off[2]);
     const dd hf = datan2(cy, cx) * flag;
     const dd vf = datan2(cz, dsqrt(cx * cx + cy * cy)) * flag;
-    if (t < 10) {  // rows 0, 1; row 2 (sdf) is written by the SDF kernel's epilogue
-        double* J = A.Jh + (r * 10 + t) * 3;
-        J[0] = hf.t;
-        J[1] = vf.t;
+    // rows 0, 1 of columns sl (< 3: d/dp_sl) and 3 + sl (zero); row 2 (sdf) is the SDF kernel's epilogue
+    double* J = A.Jh + r * 30;
+    if (sl < 3) {
+        J[sl * 3 + 0] = hf.t;
+        J[sl * 3 + 1] = vf.t;
     }
-    if (t == 0) A.h[r * 3 + 0] = hf.v;
-    if (t == 1) A.h[r * 3 + 1] = vf.v;
+    if (sl < 7) {
+        J[(3 + sl) * 3 + 0] = 0.0;
+        J[(3 + sl) * 3 + 1] = 0.0;
+    }
+    if (sl == 0) A.h[r * 3 + 0] = hf.v;
+    if (sl == 1) A.h[r * 3 + 1] = vf.v;
 }
 
 hipError_t launch_linearize(const LinArgs& a, hipStream_t s) {
     const long long rows = (long long)a.B * (a.N + 1);
     if (rows <= 0) return hipSuccess;
-    hipLaunchKernelGGL(linearize_kernel, dim3((unsigned)((rows + 15) / 16)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(linearize_kernel, dim3((unsigned)((rows + 31) / 32)), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 

@@ -16,6 +16,9 @@
 //   vae_head_kernel  AdaptiveAvgPool2d((2,2)) + Flatten + mean Linear, 4 images per workgroup
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
+#include <type_traits>
+
 #include <math.h>
 
 #include "vae_kernels.h"
@@ -97,13 +100,33 @@ constexpr int ST_CONV = ST_CY * ST_CX * ST_CS;             // floats
 constexpr int ST_LDS = (3 * ST_PATCH * 2 > ST_CONV * 4 ? 3 * ST_PATCH * 2 : ST_CONV * 4);
 static_assert(ST_IXP % 2 == 0 && ST_PATCH % 2 == 0, "32-bit tap-pair reads need even rows and planes");
 
-// x = hi + mid + lo exactly, each a bf16 truncation of the remainder (the split of split3_store)
+// x = hi + mid + lo exactly, each a bf16 truncation of the remainder
 __device__ __forceinline__ void split3(float x, unsigned& h, unsigned& m, unsigned& l) {
     h = __float_as_uint(x) & 0xffff0000u;
     const float r1 = x - __uint_as_float(h);
     m = __float_as_uint(r1) & 0xffff0000u;
     const float r2 = r1 - __uint_as_float(m);
     l = __float_as_uint(r2) & 0xffff0000u;
+}
+
+// four consecutive channels of one pixel into the three planes (8-byte stores), and back: (hi + mid) + lo is
+// the fp32 value exactly (hi + mid drops only the low 8 bits, representable)
+__device__ __forceinline__ void store_planes4(unsigned short* pl, size_t ps, size_t o, float4 v) {
+    unsigned h[4], m[4], l[4];
+    split3(v.x, h[0], m[0], l[0]);
+    split3(v.y, h[1], m[1], l[1]);
+    split3(v.z, h[2], m[2], l[2]);
+    split3(v.w, h[3], m[3], l[3]);
+    *(uint2*)&pl[o] = make_uint2((h[0] >> 16) | h[1], (h[2] >> 16) | h[3]);
+    *(uint2*)&pl[ps + o] = make_uint2((m[0] >> 16) | m[1], (m[2] >> 16) | m[3]);
+    *(uint2*)&pl[2 * ps + o] = make_uint2((l[0] >> 16) | l[1], (l[2] >> 16) | l[3]);
+}
+__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+__device__ __forceinline__ float4 load_planes4(const unsigned short* pl, size_t ps, size_t o) {
+    const uint2 h = *(const uint2*)&pl[o], m = *(const uint2*)&pl[ps + o], l = *(const uint2*)&pl[2 * ps + o];
+    return make_float4((bf_lo(h.x) + bf_lo(m.x)) + bf_lo(l.x), (bf_hi(h.x) + bf_hi(m.x)) + bf_hi(l.x),
+                       (bf_lo(h.y) + bf_lo(m.y)) + bf_lo(l.y), (bf_hi(h.y) + bf_hi(m.y)) + bf_hi(l.y));
 }
 
 // ELU(alpha = 1) = x for x > 0, expm1(x) otherwise (torch elu).  expm1 on x <= 0: the Taylor series to
@@ -316,8 +339,9 @@ __global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a, int til
             const int pyl = q >> 3, pxl = q & 7;
             const int py = py0 + pyl, px = px0 + pxl;
             if (py >= a.Hp || px >= a.Wp) continue;
+            const size_t oo = ((size_t)img * 64 + (c4 & ~15)) * a.Hp * a.Wp + (py * a.Wp + vae_col(px, a.Wp, a.out_ph)) * 16 + (c4 & 15);
 #ifdef STEM_DIAG_NOPOOL  // diagnostic builds only (tools/build_variant.sh)
-            *(float4*)&a.out[((size_t)img * 64 + (c4 & ~15)) * a.Hp * a.Wp + (py * a.Wp + px) * 16 + (c4 & 15)] = *(const float4*)&conv[((2 * pyl + 1) * ST_CX + 2 * pxl + 1) * ST_CS + c4];
+            store_planes4(a.out, a.ops, oo, *(const float4*)&conv[((2 * pyl + 1) * ST_CX + 2 * pxl + 1) * ST_CS + c4]);
 #else
             float4 v[9];
 #pragma unroll
@@ -326,13 +350,11 @@ __global__ __launch_bounds__(256, 2) void vae_stem_kernel(VaeStemArgs a, int til
                 for (int dx = 0; dx < 3; ++dx)
                     v[3 * dy + dx] = *(const float4*)&conv[((2 * pyl + dy) * ST_CX + 2 * pxl + dx) * ST_CS + c4];
 #ifdef STEM_DIAG_NOELU
-            *(float4*)&a.out[((size_t)img * 64 + (c4 & ~15)) * a.Hp * a.Wp + (py * a.Wp + px) * 16 + (c4 & 15)] =
-                make_float4(max9(v, 0), max9(v, 1), max9(v, 2), max9(v, 3));
+            store_planes4(a.out, a.ops, oo, make_float4(max9(v, 0), max9(v, 1), max9(v, 2), max9(v, 3)));
 #else
             const float2v e0 = elu2(float2v{max9(v, 0), max9(v, 1)}), e1 = elu2(float2v{max9(v, 2), max9(v, 3)});
-            // channel-blocked output [B][4][Hp][Wp][16] (the convolutions' layout)
-            *(float4*)&a.out[((size_t)img * 64 + (c4 & ~15)) * a.Hp * a.Wp + (py * a.Wp + px) * 16 + (c4 & 15)] =
-                make_float4(e0.x, e0.y, e1.x, e1.y);
+            // channel-blocked output [B][4][Hp][Wp][16] (the convolutions' layout), as planes
+            store_planes4(a.out, a.ops, oo, make_float4(e0.x, e0.y, e1.x, e1.y));
 #endif
 #endif
         }
@@ -358,270 +380,301 @@ hipError_t launch_vae_stem(const VaeStemArgs& a, int n_cu, hipStream_t s) {
 
 // ------------------------------------------------------------------------------------------------
 // implicit-GEMM convolution: out[m][n] = sum_k A[m][k] W[n][k], m = (image, oy, ox), n = channel,
-// k = (ky, kx, ci).  Tile 128 x 128 x 16, 4 waves as 2 x 2 of 64 x 64 (four 32x32 MFMA blocks each).
-// LDS rows are 16 k-values padded to 20 floats: the ds_read_b128 lane groups then hit 16 distinct
-// 16-byte slots (conflict-free).  Within a K-tile, MFMA step s feeds lane half h with k = 8h + s
-// (the same permutation for A and B), so each lane reads its 8 k-values with two ds_read_b128.
-constexpr int CV_BM = 128, CV_BN = 128, CV_BK = 16;
-#ifndef VAE_CONV_WGS
-#define VAE_CONV_WGS 3
-#endif
-// bf16 plane rows of 16 k-values, 32 bytes, unpadded; the two 16-byte halves of rows 8..15 of every 16
-// swapped (row bit 3), so the lane groups of the fragments' ds_read_b128 hit 16 distinct 16-byte slots
-// and the staging stores stay contiguous.  Two stages x 3 planes x 256 rows = 48 KB: three workgroups
-// per CU (the 48-byte padded rows took 72 KB, two per CU).
-#if VAE_CONV_WGS == 3
-constexpr int CV_SLD = 16;
+// k = (ci / 16, ky, kx, ci % 16).  Tile 128 x 128 x 16, 4 waves as 2 x 2 of 64 x 64 (four 32x32 MFMA blocks each).
+// Both operands arrive split into bf16 planes -- the activations by the layer that produced them, the
+// weights at load -- so a K-tile is staged from memory straight into LDS by LDS-DMA (global_load_lds, 16
+// bytes per lane): three A and three B loads per thread, no vector-ALU work and no register staging.  Three
+// LDS buffers: tiles kt + 1 and kt + 2 are in flight under the products of tile kt; one barrier per tile.
+// LDS plane rows are 16 bf16 (32 B) with the two 16-byte halves of rows 8..15 of every 16 swapped (row bit
+// 3), so the lane groups of the fragments' ds_read_b128 hit 16 distinct 16-byte slots.  LDS-DMA writes a
+// wave's loads lane-linearly (base + 16 lane), so the swap is made on the SOURCE side: for A, lane 2 r + h
+// of the wave's 32 rows loads half h ^ bit3(row) of its row; B is stored at load as the LDS image of each
+// K-tile (4 KB slabs), so a wave's B load is 1 KB contiguous (8 cache lines, not 32 rows K apart: the
+// texture-address unit's work per tile, which bounds this kernel, drops by half).  The reads apply the
+// same involution (cv_off).
+// Within a K-tile, MFMA step s feeds lane half h with k = 8h + s (the same permutation for A and B).
+// The weight fragment is the MFMA's first operand, so the accumulator is C^T: a lane ends with four
+// consecutive channels of one pixel per register quad (8-byte plane stores, 16-byte fp32 stores).
+constexpr int CV_BK = 16;
 __device__ __forceinline__ int cv_off(int row, int half) { return row * 16 + 8 * (half ^ ((row >> 3) & 1)); }
-#else  // diagnostic build: the round-3 layout (48-byte rows, two workgroups per CU)
-constexpr int CV_SLD = 24;
-__device__ __forceinline__ int cv_off(int row, int half) { return row * 24 + 8 * half; }
-#endif
+template <class T>
+__device__ __forceinline__ void cv_tie(T& x) { asm volatile("" : "+v"(x)); }
 
-// fp32 -> three bf16 by truncation: x = hi + mid + lo EXACTLY (each takes the next 8 significant bits of
-// the 24; the remainders are exact fp32 differences).  A float4 of one row -> its 4-bf16 pieces of the
-// hi / mid / lo planes (8-byte stores).
-__device__ __forceinline__ void split3_store(float4 v, unsigned short* planes, int pstride, int off) {
-#ifdef VAE_DIAG_NOSPLIT  // diagnostic build (tools/build_variant.sh): the time without the split's VALU work
-    const uint2 q = make_uint2((__float_as_uint(v.x) >> 16) | (__float_as_uint(v.y) & 0xffff0000u),
-                               (__float_as_uint(v.z) >> 16) | (__float_as_uint(v.w) & 0xffff0000u));
-    *(uint2*)&planes[off] = q;
-    *(uint2*)&planes[pstride + off] = q;
-    *(uint2*)&planes[2 * pstride + off] = q;
-    return;
-#endif
-    const float x[4] = {v.x, v.y, v.z, v.w};
-    unsigned hb[4], mb[4], lb[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-        hb[q] = __float_as_uint(x[q]) & 0xffff0000u;
-        const float r1 = x[q] - __uint_as_float(hb[q]);
-        mb[q] = __float_as_uint(r1) & 0xffff0000u;
-        const float r2 = r1 - __uint_as_float(mb[q]);
-        lb[q] = __float_as_uint(r2) & 0xffff0000u;
-    }
-    *(uint2*)&planes[off] = make_uint2((hb[0] >> 16) | hb[1], (hb[2] >> 16) | hb[3]);
-    *(uint2*)&planes[pstride + off] = make_uint2((mb[0] >> 16) | mb[1], (mb[2] >> 16) | mb[3]);
-    *(uint2*)&planes[2 * pstride + off] = make_uint2((lb[0] >> 16) | lb[1], (lb[2] >> 16) | lb[3]);
-}
-
-// component-wise select (a ?: on the float4 struct goes through a stack slot)
-__device__ __forceinline__ float4 sel4(bool ok, float4 v) {
-    return make_float4(ok ? v.x : 0.f, ok ? v.y : 0.f, ok ? v.z : 0.f, ok ? v.w : 0.f);
-}
-
-#ifndef VAE_LOAD_DEPTH
-#define VAE_LOAD_DEPTH 1
-#endif
-constexpr int CV_D = VAE_LOAD_DEPTH;  // K-tiles whose global loads are in flight in registers
-
-template <int KS, int S>
-__global__ __launch_bounds__(256, VAE_CONV_WGS) void vae_conv_kernel(VaeConvArgs a) {
-    constexpr int P = KS / 2;
-    // the K-tile split ONCE, by the thread that loads it, into bf16 hi / mid / lo planes: rows of 16 bf16
-    // at a 24-bf16 (48-byte) stride, so the lane groups of a ds_read_b128 hit distinct 16-byte slots
-    __shared__ __align__(16) unsigned short As3[2][3][CV_BM * CV_SLD];
-    __shared__ __align__(16) unsigned short Bs3[2][3][CV_BN * CV_SLD];
+// WM x WN 32x32 blocks per wave, 2 x 2 waves: a (64 WM) x (64 WN) workgroup tile; NB LDS buffers.
+template <int KS, int S, int WM, int WN, int NB>
+__global__ __launch_bounds__(256, 2) void vae_conv_kernel(VaeConvArgs a) {
+    constexpr int P = KS / 2, BM = 64 * WM, BN = 64 * WN, RA = BM / 128, RB = BN / 128;
+    constexpr int NV = 3 * (RA + RB);  // LDS-DMA loads per thread and K-tile
+    typedef __attribute__((address_space(3))) void ldsv;
+    // one LDS object per buffer and operand, each addressed with a compile-time buffer index: the compiler
+    // then tells a buffer's fragment reads from the LDS-DMA into the other buffers (one shared object
+    // indexed at run time makes every ds_read wait for all DMA in flight, vmcnt(0))
+    __shared__ __align__(16) unsigned short A0[3][BM * 16], A1[3][BM * 16], A2[NB > 2 ? 3 : 1][BM * 16];
+    __shared__ __align__(16) unsigned short B0[3][BN * 16], B1[3][BN * 16], B2[NB > 2 ? 3 : 1][BN * 16];
+    auto As = [&](auto bc) -> unsigned short(*)[BM * 16] {
+        constexpr int b = decltype(bc)::value;
+        if constexpr (b == 0) return A0;
+        else if constexpr (b == 1) return A1;
+        else return A2;
+    };
+    auto Bs = [&](auto bc) -> unsigned short(*)[BN * 16] {
+        constexpr int b = decltype(bc)::value;
+        if constexpr (b == 0) return B0;
+        else if constexpr (b == 1) return B1;
+        else return B2;
+    };
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int wm = wave >> 1, wn = wave & 1, lr = lane & 31, lh = lane >> 5;
-    const int M = a.B * a.Ho * a.Wo, MT = (M + CV_BM - 1) / CV_BM;
+    const int M = a.B * a.Ho * a.Wo, MT = (M + BM - 1) / BM;
     const int nt = blockIdx.x / MT, mt = blockIdx.x - nt * MT;
     const int Cin = a.Cin, K = KS * KS * Cin, KT = K / CV_BK;
-    const int kq = tid & 3;
 
-    // loader rows (A) and columns (B) of this thread (scalars, so nothing is indexed dynamically)
+    // the A rows this thread stages (pixels 128 r + 32 wave + lane / 2) and which half of them
+    const int srow = 32 * wave + (lane >> 1), shalf = (lane & 1) ^ ((srow >> 3) & 1);
     const int HW = a.Ho * a.Wo;
-    const int m0 = mt * CV_BM + (tid >> 2), m1 = m0 + 64;
-    const bool v0 = m0 < M, v1 = m1 < M;
-    const int q0 = v0 ? m0 : 0, q1 = v1 ? m1 : 0;
-    const int im0 = q0 / HW, r0 = q0 - im0 * HW, oy0 = r0 / a.Wo, ox0 = r0 - oy0 * a.Wo;
-    const int im1 = q1 / HW, r1 = q1 - im1 * HW, oy1 = r1 / a.Wo, ox1 = r1 - oy1 * a.Wo;
-    const int iyA = oy0 * S - P, ixA = ox0 * S - P, iyB = oy1 * S - P, ixB = ox1 * S - P;
-    // activations channel-blocked, [B][C / 16][H][W][16] (VaeConvArgs): a K-tile's 16 channels of
-    // consecutive pixels are consecutive 64-byte pieces, so a load instruction's 16 rows x 4 quarters
-    // read 1 KB of whole cache lines (NHWC spread them over 16 lines, half of each used)
     const size_t HWi = (size_t)a.Hi * a.Wi;
-    const float* pa0 = a.in + (size_t)im0 * HWi * Cin + 4 * kq;
-    const float* pa1 = a.in + (size_t)im1 * HWi * Cin + 4 * kq;
-    // B from the weight planes split at load: column tid / 2, k-values 8 (tid % 2) .. + 7 (16 bytes) of
-    // each plane
+    int iy0[RA], ix0[RA];
+    bool vm[RA];
+    const unsigned short* pa[RA];
+#pragma unroll
+    for (int r = 0; r < RA; ++r) {
+        const int m0 = mt * BM + 128 * r + srow;
+        vm[r] = m0 < M;
+        const int q0 = vm[r] ? m0 : 0;
+        const int im = q0 / HW, r0 = q0 - im * HW, oy = r0 / a.Wo, ox = r0 - oy * a.Wo;
+        iy0[r] = oy * S - P;
+        ix0[r] = ox * S - P;
+        pa[r] = a.in + (size_t)im * HWi * Cin + 8 * shalf;  // channel-blocked planes
+    }
     const size_t wps = (size_t)a.Cout * K;
-    const unsigned short* pb = a.wpl + (size_t)(nt * CV_BN + (tid >> 1)) * K + 8 * (tid & 1);
-    const int brow = cv_off(tid >> 1, tid & 1);
-    const int hrow0 = cv_off(tid >> 2, kq >> 1) + 4 * (kq & 1), hrow1 = cv_off((tid >> 2) + 64, kq >> 1) + 4 * (kq & 1);
-
-    // a ring of CV_D register sets (A rows m0, m1; B columns n0, n1 of one K-tile): the loads of K-tile
-    // kt + 1 + CV_D are issued when tile kt + 1 has been stashed.  Depth 2, 3 and 4 measure the same
-    // (15.5 / 15.6 / 15.6 ms of convolutions per 512 images): the loop is not load-latency bound.
-    struct Stage {
-        float4 a0, a1;  // A rows m0, m1 (fp32, split at the stash)
-        uint4 b[3];     // B: hi / mid / lo (split at load)
-    };
-    Stage ring[CV_D];
-    int ky = 0, kx = 0, c0 = 0, kl = 0;  // the next K-tile to load: tap (ky, kx), channel block c0, index kl
-    // the rows' pixel pointers for the current tap, recomputed only when the tap changes (every Cin / 16
-    // K-tiles); a K-tile then adds c0 (H W) of the row's channel stride.  A pixel outside the map reads a
-    // zeroed 64-byte block with stride 0 (a.zero16): the loaded value is the operand, no select.
-    const float *ap0 = pa0, *ap1 = pa1;
-    unsigned st0 = 0, st1 = 0;
+    // B: the weights' K-tile slabs (the LDS image of 128 channels x 16 k), loaded lane-linearly
+    const unsigned short* pb = a.wpl + (size_t)nt * RB * KT * (128 * CV_BK) + 8 * tid;
+    // a row's pixel for the current tap, recomputed every K-tile; the K-tile then adds c0 (H W) elements
+    // (its channel block).  A pixel outside the map reads the zero block with stride 0.
+    int ky = 0, kx = 0, c0 = 0, kl = 0;
+    const unsigned short* ap[RA];
+    size_t st[RA], pst[RA];  // channel-block and plane strides of a row's source (0 on the zero block)
     auto tap = [&]() {
-        const int iy0 = iyA + ky, ix0 = ixA + kx, iy1 = iyB + ky, ix1 = ixB + kx;
-        const bool ok0 = v0 && (unsigned)iy0 < (unsigned)a.Hi && (unsigned)ix0 < (unsigned)a.Wi;
-        const bool ok1 = v1 && (unsigned)iy1 < (unsigned)a.Hi && (unsigned)ix1 < (unsigned)a.Wi;
-        ap0 = ok0 ? pa0 + ((size_t)iy0 * a.Wi + ix0) * 16 : a.zero16 + 4 * kq;
-        ap1 = ok1 ? pa1 + ((size_t)iy1 * a.Wi + ix1) * 16 : a.zero16 + 4 * kq;
-        st0 = ok0 ? (unsigned)HWi : 0u;
-        st1 = ok1 ? (unsigned)HWi : 0u;
+#pragma unroll
+        for (int r = 0; r < RA; ++r) {
+            const int iy = iy0[r] + ky, ix = ix0[r] + kx;
+            const bool ok = vm[r] && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
+            ap[r] = ok ? pa[r] + ((size_t)iy * a.Wi + vae_col(ix, a.Wi, a.in_ph)) * 16 : a.zero + 8 * shalf;
+            st[r] = ok ? HWi : 0;
+            pst[r] = ok ? a.ips : 0;
+        }
     };
     tap();
-    // Loads are unconditional and their values untouched until the stash (past the last K-tile they
-    // re-read valid addresses: the last weight tile; A's channel offset stays inside the map, Cin (H W)
-    // at most): a select or a branch next to a load makes the compiler wait for it at once (vmcnt),
-    // which serialised every K-tile on its A loads.
-    auto load = [&](Stage& r) {
-#ifdef VAE_DIAG_NOALOAD  // diagnostic build: A from registers, not memory (results invalid)
-        r.a0 = make_float4(1.f + c0, 2.f, 3.f, 4.f);
-        r.a1 = make_float4(5.f, 6.f + kx, 7.f, 8.f);
-#else
-        r.a0 = *(const float4*)(ap0 + (size_t)c0 * st0);
-        r.a1 = *(const float4*)(ap1 + (size_t)c0 * st1);
-#endif
-        const int klc = kl < KT ? kl : KT - 1;
+    // K-tile kl into LDS buffer bc (per load, a wave's 32 rows of a plane: 1 KB), then advance
+    auto issue = [&](auto bc) {
+        auto* LA = As(bc);
+        auto* LB = Bs(bc);
 #pragma unroll
-        for (int p = 0; p < 3; ++p) r.b[p] = *(const uint4*)(pb + p * wps + (size_t)klc * CV_BK);
-        c0 += CV_BK;
-        if (c0 == Cin) {
-            c0 = 0;
+        for (int p = 0; p < 3; ++p) {
+#pragma unroll
+            for (int r = 0; r < RA; ++r)
+                __builtin_amdgcn_global_load_lds((const void*)(ap[r] + (size_t)c0 * st[r] + p * pst[r]),
+                                                 (ldsv*)&LA[p][2048 * r + 512 * wave], 16, 0, 0);
+#pragma unroll
+            for (int r = 0; r < RB; ++r)
+                __builtin_amdgcn_global_load_lds((const void*)(pb + ((size_t)r * KT + kl) * (128 * CV_BK) + p * wps),
+                                                 (ldsv*)&LB[p][2048 * r + 512 * wave], 16, 0, 0);
+        }
+        // K order (channel block, ky, kx): the nine taps of a channel block are consecutive K-tiles, so
+        // the rows' input pixels are re-read while they are still in L2
+        if constexpr (KS > 1) {
             if (++kx == KS) {
                 kx = 0;
-                ++ky;
+                if (++ky == KS) {
+                    ky = 0;
+                    c0 += CV_BK;
+                }
             }
             tap();
+        } else {
+            c0 += CV_BK;
         }
         ++kl;
     };
-    auto stash = [&](int buf, const Stage& r) {
-        split3_store(r.a0, As3[buf][0], CV_BM * CV_SLD, hrow0);
-        split3_store(r.a1, As3[buf][0], CV_BM * CV_SLD, hrow1);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) *(uint4*)&Bs3[buf][p][brow] = r.b[p];
-    };
 
-    floatx16 acc[2][2];
+    floatx16 acc[WM][WN];
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < WM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
+        for (int j = 0; j < WN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-    auto products = [&](int buf) {
+    auto products = [&](auto bc) {
+        const auto* LA = As(bc);
+        const auto* LB = Bs(bc);
         // fp32 products on the bf16 matrix pipe: a = ah + am + al, b = bh + bm + bl exactly, and the six
         // products down to 2^-16 relative (al.bh, ah.bl, am.bm, am.bh, ah.bm, ah.bh; smallest first)
         // are accumulated in fp32 -- the dropped ones (am.bl, al.bm, al.bl) are <= 2^-24 relative, the
-        // fp32 rounding level.  One 32x32x16 K-step covers the K-tile (lane half h: k = 8h .. 8h + 7,
-        // the same permutation for A and B).  6 x 32 cycles of the matrix pipe per block and K-tile.
-        bf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
+        // fp32 rounding level.  One 32x32x16 K-step covers the K-tile.  6 x 32 cycles of the matrix pipe
+        // per block and K-tile.
+        // Fragment reads are inline ds_read_b128: the compiler cannot see their LDS access, so it adds no
+        // wait for the LDS-DMA in flight (it would wait for all of it after every loop merge); the vmcnt +
+        // barrier of the step order them after this tile's DMA.  Each lgkmcnt wait is followed by empty
+        // asm "redefining" the fragments it covers, so no MFMA is scheduled above it.
+        bf16x8 ah[WM], am[WM], al[WM], bh[WN], bm[WN], bl[WN];
+        const unsigned la = (unsigned)(uintptr_t)(const ldsv*)&LA[0][0];
+        const unsigned lb = (unsigned)(uintptr_t)(const ldsv*)&LB[0][0];
+#define VAE_DSR(R, ADDR, OFF) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(R) : "v"(ADDR), "i"(OFF))
+        unsigned ao[WM], bo[WN];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            const int ao = cv_off(wm * 64 + 32 * i + lr, lh), bo = cv_off(wn * 64 + 32 * i + lr, lh);
-            ah[i] = *(const bf16x8*)&As3[buf][0][ao];
-            am[i] = *(const bf16x8*)&As3[buf][1][ao];
-            al[i] = *(const bf16x8*)&As3[buf][2][ao];
-            bh[i] = *(const bf16x8*)&Bs3[buf][0][bo];
-            bm[i] = *(const bf16x8*)&Bs3[buf][1][bo];
-            bl[i] = *(const bf16x8*)&Bs3[buf][2][bo];
+        for (int i = 0; i < WM; ++i) {
+            ao[i] = la + 2 * cv_off(wm * 32 * WM + 32 * i + lr, lh);
+            VAE_DSR(ah[i], ao[i], 0);
+            VAE_DSR(al[i], ao[i], 2 * BM * 16 * 2);
+        }
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+            bo[j] = lb + 2 * cv_off(wn * 32 * WN + 32 * j + lr, lh);
+            VAE_DSR(bh[j], bo[j], 0);
+            VAE_DSR(bl[j], bo[j], 2 * BN * 16 * 2);
+        }
+#pragma unroll
+        for (int i = 0; i < WM; ++i) VAE_DSR(am[i], ao[i], BM * 16 * 2);
+#pragma unroll
+        for (int j = 0; j < WN; ++j) VAE_DSR(bm[j], bo[j], BN * 16 * 2);
+#undef VAE_DSR
+        // the mid planes arrive under the first 2 WM WN MFMAs
+        asm volatile("s_waitcnt lgkmcnt(%0)" ::"i"(WM + WN));
+#pragma unroll
+        for (int i = 0; i < WM; ++i) {
+            cv_tie(ah[i]);
+            cv_tie(al[i]);
+        }
+#pragma unroll
+        for (int j = 0; j < WN; ++j) {
+            cv_tie(bh[j]);
+            cv_tie(bl[j]);
         }
 #define VAE_MM(X, Y)                                                                                   \
-    _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)         \
-        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[i], Y[j], acc[i][j], 0, 0, 0);
-#ifndef VAE_DIAG_ONEMM  // diagnostic build: one product per block and K-tile instead of six (results invalid)
+    _Pragma("unroll") for (int i = 0; i < WM; ++i) _Pragma("unroll") for (int j = 0; j < WN; ++j)       \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(Y[j], X[i], acc[i][j], 0, 0, 0);
         VAE_MM(al, bh)
         VAE_MM(ah, bl)
+#pragma unroll
+        for (int i = 0; i < WM; ++i)
+#pragma unroll
+            for (int j = 0; j < WN; ++j) cv_tie(acc[i][j]);  // those MFMAs stay above the second wait
+        asm volatile("s_waitcnt lgkmcnt(0)");
+#pragma unroll
+        for (int i = 0; i < WM; ++i) cv_tie(am[i]);
+#pragma unroll
+        for (int j = 0; j < WN; ++j) cv_tie(bm[j]);
         VAE_MM(am, bm)
         VAE_MM(am, bh)
         VAE_MM(ah, bm)
-#else
-        (void)al; (void)bl; (void)am; (void)bm;
-#endif
         VAE_MM(ah, bh)
 #undef VAE_MM
     };
 
-    // prologue: K-tiles 0 .. CV_D - 1 in flight, tile 0 stashed, slot 0 refilled with tile CV_D
-#pragma unroll
-    for (int d = 0; d < CV_D; ++d) load(ring[d]);
-    stash(0, ring[0]);
-    load(ring[0]);
-    __syncthreads();
-    // K-tile kt: products from LDS buffer kt & 1; then tile kt + 1 (ring slot (kt + 1) % CV_D) is split
-    // into the other buffer and its slot refilled with tile kt + 1 + CV_D.  Unrolled by CV_D so that the
-    // ring slots are static registers.
-#ifdef VAE_DIAG_NOSYNC  // diagnostic build: no barrier per K-tile (results invalid)
-#define CV_SYNC() __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup")
-#else
-#define CV_SYNC() __syncthreads()
-#endif
-    // main trips: CV_D K-tiles each, every one followed by a stash and a load (no conditions)
-    int kt0 = 0;
-    for (; kt0 + CV_D < KT; kt0 += CV_D) {
-#pragma unroll
-        for (int d = 0; d < CV_D; ++d) {
-            products((kt0 + d) & 1);
-            stash((kt0 + d + 1) & 1, ring[(d + 1) % CV_D]);
-            load(ring[(d + 1) % CV_D]);
-            CV_SYNC();
+    // K-tile kt (buffer kt % NB): wait for this thread's DMA of it (VMEM operations of a wave complete in
+    // order, so the NV loads of the tile after it may stay in flight), then a barrier (every thread's DMA
+    // of tile kt has landed; every wave's reads of the buffer about to be refilled are done), stage tile
+    // kt + NB - 1, and the products of tile kt under the tiles in flight.
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
+    int kt = 0;
+    if constexpr (NB == 3) {
+        auto step = [&](int kt, auto bc, auto bnext) {
+            if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(NV) : "memory");
+            else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (kt + 2 < KT) issue(bnext);
+            products(bc);
+        };
+        issue(I0{});
+        if (KT > 1) issue(I1{});
+        for (; kt + 3 <= KT; kt += 3) {
+            step(kt, I0{}, I2{});
+            step(kt + 1, I1{}, I0{});
+            step(kt + 2, I2{}, I1{});
         }
-    }
-    // the last 1 .. CV_D K-tiles
-#pragma unroll
-    for (int d = 0; d < CV_D; ++d) {
-        const int kt = kt0 + d;
-        if (kt < KT) {
-            products(kt & 1);
-            if (kt + 1 < KT) stash((kt + 1) & 1, ring[(d + 1) % CV_D]);
-            CV_SYNC();
+        if (kt < KT) step(kt, I0{}, I2{});
+        if (kt + 1 < KT) step(kt + 1, I1{}, I0{});
+    } else {
+        auto step = [&](int kt, auto bc, auto bnext) {
+            asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (kt + 1 < KT) issue(bnext);
+            products(bc);
+        };
+        issue(I0{});
+        for (; kt + 2 <= KT; kt += 2) {
+            step(kt, I0{}, I1{});
+            step(kt + 1, I1{}, I0{});
         }
+        if (kt < KT) step(kt, I0{}, I1{});
     }
-#undef CV_SYNC
 
-    // epilogue: lane (lr, lh), register r holds row 8(r/4) + 4 lh + r%4, column lr of each block
+    // epilogue (C^T): lane (lr, lh) holds pixel 32 i + lr of the wave's rows and, in register quad g,
+    // channels 32 j + 8 g + 4 lh .. + 3
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-        const int n = nt * CV_BN + wn * 64 + 32 * j + lr;
-        const float bias = a.b[n];
+    for (int i = 0; i < WM; ++i) {
+        const int m = mt * BM + wm * 32 * WM + 32 * i + lr;
+        if (m >= M) continue;
+        const int img = m / HW, pix = m - img * HW, oy = pix / a.Wo, ox = pix - oy * a.Wo;
+        const int po = oy * a.Wo + vae_col(ox, a.Wo, a.out_ph), pr = oy * a.Wo + vae_col(ox, a.Wo, a.res_ph);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int j = 0; j < WN; ++j)
 #pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int m = mt * CV_BM + wm * 64 + 32 * i + 8 * (r >> 2) + 4 * lh + (r & 3);
-                if (m < M) {
-                    const int img = m / HW, pix = m - img * HW;  // channel-blocked output
-                    const size_t o = ((size_t)img * a.Cout + (n & ~15)) * HW + pix * 16 + (n & 15);
-                    float v = acc[i][j][r] + bias;
-                    if (a.resid) v += a.resid[o];
-                    if (a.relu) v = v < 0.f ? 0.f : v;  // torch.relu keeps a NaN (fmaxf would drop it)
-                    a.out[o] = v;
+            for (int g = 0; g < 4; ++g) {
+                const int n = nt * BN + wn * 32 * WN + 32 * j + 8 * g + 4 * lh;
+                const size_t cb = ((size_t)img * a.Cout + (n & ~15)) * HW + (n & 15);
+                const size_t o = cb + po * 16, orr = cb + pr * 16;
+                const float4 bias = make_float4(a.b[n], a.b[n + 1], a.b[n + 2], a.b[n + 3]);
+                float4 v = make_float4(acc[i][j][4 * g] + bias.x, acc[i][j][4 * g + 1] + bias.y,
+                                       acc[i][j][4 * g + 2] + bias.z, acc[i][j][4 * g + 3] + bias.w);
+                if (a.resid || a.resid_pl) {
+                    const float4 rv = a.resid ? *(const float4*)&a.resid[orr] : load_planes4(a.resid_pl, a.rps, orr);
+                    v = make_float4(v.x + rv.x, v.y + rv.y, v.z + rv.z, v.w + rv.w);
                 }
+                if (a.relu)  // torch.relu keeps a NaN (fmaxf would drop it)
+                    v = make_float4(v.x < 0.f ? 0.f : v.x, v.y < 0.f ? 0.f : v.y, v.z < 0.f ? 0.f : v.z, v.w < 0.f ? 0.f : v.w);
+                if (a.out_pl) store_planes4(a.out_pl, a.ops, o, v);
+                else *(float4*)&a.out[o] = v;
             }
+    }
+}
+
+// tile shape per layer: VAE_CV_SHAPE 0 = 128 x 128 (three LDS buffers), 1 = wide (128 x 256 when Cout is a
+// multiple of 256, else 256 x 128; two buffers).  Both measured within 1 % of each other;
+// the product is the 128 x 128 tile.
+#ifndef VAE_CV_SHAPE
+#define VAE_CV_SHAPE 0
+#endif
+template <int KS, int S>
+static void cv_launch(const VaeConvArgs& a, long long M, hipStream_t s) {
+    if (VAE_CV_SHAPE == 0) {
+        const long long g = ((M + 127) / 128) * (a.Cout / 128);
+        hipLaunchKernelGGL((vae_conv_kernel<KS, S, 2, 2, 3>), dim3((unsigned)g), dim3(256), 0, s, a);
+    } else if (a.Cout % 256 == 0) {
+        const long long g = ((M + 127) / 128) * (a.Cout / 256);
+        hipLaunchKernelGGL((vae_conv_kernel<KS, S, 2, 4, 2>), dim3((unsigned)g), dim3(256), 0, s, a);
+    } else {
+        const long long g = ((M + 255) / 256) * (a.Cout / 128);
+        hipLaunchKernelGGL((vae_conv_kernel<KS, S, 4, 2, 2>), dim3((unsigned)g), dim3(256), 0, s, a);
     }
 }
 
 hipError_t launch_vae_conv(const VaeConvArgs& a, int ks, int stride, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     const int p = ks / 2;
-    if (a.Cin % CV_BK || a.Cout % CV_BN || a.Ho != (a.Hi + 2 * p - ks) / stride + 1 ||
-        a.Wo != (a.Wi + 2 * p - ks) / stride + 1)
+    if (a.Cin % CV_BK || a.Cout % 128 || a.Ho != (a.Hi + 2 * p - ks) / stride + 1 ||
+        a.Wo != (a.Wi + 2 * p - ks) / stride + 1 || !a.in || !a.wpl || !a.zero || (!a.out && !a.out_pl) ||
+        ((uintptr_t)a.in & 15) || (a.ips & 7) || ((uintptr_t)a.zero & 15))
         return hipErrorInvalidValue;
     const long long M = (long long)a.B * a.Ho * a.Wo;
-    const long long grid = ((M + CV_BM - 1) / CV_BM) * (a.Cout / CV_BN);
-    if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
+    if ((M + 127) / 128 * (a.Cout / 128) > 0x7fffffffLL) return hipErrorInvalidValue;
     if (ks == 3 && stride == 1)
-        hipLaunchKernelGGL((vae_conv_kernel<3, 1>), dim3((unsigned)grid), dim3(256), 0, s, a);
+        cv_launch<3, 1>(a, M, s);
     else if (ks == 3 && stride == 2)
-        hipLaunchKernelGGL((vae_conv_kernel<3, 2>), dim3((unsigned)grid), dim3(256), 0, s, a);
+        cv_launch<3, 2>(a, M, s);
     else if (ks == 1 && stride == 2)
-        hipLaunchKernelGGL((vae_conv_kernel<1, 2>), dim3((unsigned)grid), dim3(256), 0, s, a);
+        cv_launch<1, 2>(a, M, s);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -639,7 +692,8 @@ hipError_t launch_vae_conv(const VaeConvArgs& a, int ks, int stride, hipStream_t
 // per 512 images.)
 __global__ __launch_bounds__(256) void vae_pool_kernel(VaeHeadArgs a) {
     const int b = blockIdx.x, c = blockIdx.y * 256 + threadIdx.x;
-    const float* in = a.in + ((size_t)b * 512 + (c & ~15)) * a.h * a.w + (c & 15);  // channel-blocked
+    const size_t ci = ((size_t)b * 512 + (c & ~15)) * a.h * a.w + (c & 15);  // channel-blocked planes
+    const unsigned short *in = a.in + ci, *in1 = in + a.ips, *in2 = in + 2 * a.ips;
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -648,7 +702,11 @@ __global__ __launch_bounds__(256) void vae_pool_kernel(VaeHeadArgs a) {
             const int x0 = (j * a.w) / 2, x1 = ((j + 1) * a.w + 1) / 2;
             float s = 0.f;
             for (int y = y0; y < y1; ++y)
-                for (int x = x0; x < x1; ++x) s += in[((size_t)y * a.w + x) * 16];
+                for (int x = x0; x < x1; ++x) {
+                    const size_t e = ((size_t)y * a.w + x) * 16;  // (hi + mid) + lo: the fp32 value
+                    s += (__uint_as_float((unsigned)in[e] << 16) + __uint_as_float((unsigned)in1[e] << 16)) +
+                         __uint_as_float((unsigned)in2[e] << 16);
+                }
             a.feat[(size_t)b * 2048 + c * 4 + i * 2 + j] = s / (float)((y1 - y0) * (x1 - x0));
         }
 }

@@ -13,16 +13,28 @@ struct VaePreArgs {
     float* out;        // [B][H][W]
 };
 
-// conv7x7/2 (+bias) + ELU + maxpool3/2 (vae.py:19-21), channel-blocked output [B][64/16][Hp][Wp][16]
+// Activations between the stem and the head are stored pre-split: three bf16 planes (hi, mid, lo; x = hi + mid
+// + lo exactly, each the bf16 truncation of the remainder), plane p at p * ps elements, each in the
+// channel-blocked order [B][C/16][H][W][16].  A convolution then stages its operand tiles from memory
+// straight into LDS (global_load_lds), with no split on the vector ALU.
+// conv7x7/2 (+bias) + ELU + maxpool3/2 (vae.py:19-21), output as planes [3][B][64/16][Hp][Wp][16]
 struct VaeStemArgs {
     const float* in;   // [B][H][W]
     const unsigned short* wpl;  // [3][64 n][64 k] bf16 bits: the weights split hi / mid / lo, slot k holding
                                 // tap vae_stem_slot_tap(k)
     const float* b;    // [64]
-    float* out;        // [B][4][Hp][Wp][16]
+    unsigned short* out;  // planes, plane stride ops
+    size_t ops;
     int B, H, W, Hc, Wc, Hp, Wp;
+    int out_ph;  // output columns in parity-phase order (vae_col): the next layer is a stride-2 convolution
 };
-constexpr int VAE_STEM_PLANE = 64 * 64;  // bf16 per plane of VaeStemArgs::wpl
+constexpr int VAE_STEM_PLANE = 64 * 64;
+
+// Parity-phase column order of a map of width W: the even columns first, then the odd ones.  A stride-2
+// convolution's taps then read consecutive output columns from consecutive stored columns (32 B apart in
+// a channel-blocked plane instead of 64), halving the cache lines its activation loads touch.  Maps read by
+// a stride-2 convolution are stored in this order; the others in natural order.
+__host__ __device__ inline int vae_col(int x, int W, int ph) { return ph ? ((x & 1) ? ((W + 1) >> 1) : 0) + (x >> 1) : x; }  // bf16 per plane of VaeStemArgs::wpl
 
 // The stem's K order: slot k of a plane row holds tap vae_stem_slot_tap(k) = ky * 7 + kx (-1: zero).
 // Slots pair up (2p, 2p + 1).  Pairs 0..17, 20, 21 are horizontal neighbours (ky, kx), (ky, kx + 1) with kx
@@ -61,19 +73,27 @@ static_assert(vae_stem_order_ok(), "stem K order");
 // implicit-GEMM convolution (BatchNorm folded) + bias (+ residual) (+ ReLU); activations channel-blocked,
 // [B][C/16][H][W][16]
 struct VaeConvArgs {
-    const float* in;     // [B][Cin/16][Hi][Wi][16]
+    const unsigned short* in;  // planes [3][B][Cin/16][Hi][Wi][16], plane stride ips
+    size_t ips;
     const float* w;      // [Cout][KS][KS][Cin]
-    const unsigned short* wpl;  // the same weights split into bf16 planes [3 hi/mid/lo][Cout][KS KS Cin] (at load)
+    const unsigned short* wpl;  // the same weights split into bf16 planes [3 hi/mid/lo][Cout/128][K/16][128][16]
+                                // (K-tile slabs, row halves swapped on row bit 3; at load)
     const float* b;      // [Cout]
-    const float* zero16; // 16 zero floats (64 B, 16-byte aligned): what a tap outside the map reads
-    const float* resid;  // [B][Cout/16][Ho][Wo][16] or nullptr
-    float* out;          // [B][Cout/16][Ho][Wo][16]
+    const unsigned short* zero;  // 32 zero bytes (16-byte aligned): what a tap outside the map reads
+    const float* resid;  // fp32 [B][Cout/16][Ho][Wo][16], or nullptr
+    const unsigned short* resid_pl;  // or the residual as planes (plane stride rps), or nullptr
+    size_t rps;
+    float* out;          // fp32 [B][Cout/16][Ho][Wo][16], or nullptr
+    unsigned short* out_pl;  // or the output as planes (plane stride ops), or nullptr
+    size_t ops;
     int B, Hi, Wi, Cin, Ho, Wo, Cout, relu;
+    int in_ph, out_ph, res_ph;  // which of in / out / resid keep their columns in parity-phase order (vae_col)
 };
 
 // AdaptiveAvgPool2d((2,2)) + Flatten + mean Linear (vae.py:26-30, 42-43)
 struct VaeHeadArgs {
-    const float* in;     // [B][512/16][h][w][16]
+    const unsigned short* in;  // planes [3][B][512/16][h][w][16], plane stride ips
+    size_t ips;
     float* feat;         // [B][2048] workspace: the pooled, flattened features
     const float* wt;     // [2048][L]  (transposed mean.weight)
     const float* b;      // [L]
