@@ -469,6 +469,7 @@ __global__ __launch_bounds__(256, 2) void vae_conv_kernel(VaeConvArgs a) {
     auto issue = [&](auto bc) {
         auto* LA = As(bc);
         auto* LB = Bs(bc);
+#ifndef VAE_DIAG_NOISSUE  // diagnostic build: no staging loads at all (results invalid)
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
 #pragma unroll
@@ -480,6 +481,9 @@ __global__ __launch_bounds__(256, 2) void vae_conv_kernel(VaeConvArgs a) {
                 __builtin_amdgcn_global_load_lds((const void*)(pb + ((size_t)r * KT + kl) * (128 * CV_BK) + p * wps),
                                                  (ldsv*)&LB[p][2048 * r + 512 * wave], 16, 0, 0);
         }
+#else
+        (void)LA; (void)LB;
+#endif
         // K order (channel block, ky, kx): the nine taps of a channel block are consecutive K-tiles, so
         // the rows' input pixels are re-read while they are still in L2
         if constexpr (KS > 1) {
@@ -582,7 +586,11 @@ __global__ __launch_bounds__(256, 2) void vae_conv_kernel(VaeConvArgs a) {
     int kt = 0;
     if constexpr (NB == 3) {
         auto step = [&](int kt, auto bc, auto bnext) {
+#ifdef VAE_DIAG_NOWAIT  // diagnostic build: the products do not wait for the DMA (results invalid)
+            if (kt + 1 < KT) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
             if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(NV) : "memory");
+#endif
             else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             if (kt + 2 < KT) issue(bnext);
             products(bc);
