@@ -17,7 +17,9 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <numeric>
 #include <type_traits>
+#include <utility>
 
 #include <math.h>
 
@@ -399,6 +401,11 @@ constexpr int CV_BK = 16;
 __device__ __forceinline__ int cv_off(int row, int half) { return row * 16 + 8 * (half ^ ((row >> 3) & 1)); }
 template <class T>
 __device__ __forceinline__ void cv_tie(T& x) { asm volatile("" : "+v"(x)); }
+// f(integral_constant<int, I>) for I = 0, 1, ... in order
+template <class F, int... I>
+__device__ __forceinline__ void cv_static_for(F&& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
 
 // WM x WN 32x32 blocks per wave, 2 x 2 waves: a (64 WM) x (64 WN) workgroup tile; NB LDS buffers.
 template <int KS, int S, int WM, int WN, int NB>
@@ -449,55 +456,55 @@ __global__ __launch_bounds__(256, 2) void vae_conv_kernel(VaeConvArgs a) {
     const size_t wps = (size_t)a.Cout * K;
     // B: the weights' K-tile slabs (the LDS image of 128 channels x 16 k), loaded lane-linearly
     const unsigned short* pb = a.wpl + (size_t)nt * RB * KT * (128 * CV_BK) + 8 * tid;
-    // a row's pixel for the current tap, recomputed every K-tile; the K-tile then adds c0 (H W) elements
-    // (its channel block).  A pixel outside the map reads the zero block with stride 0.
-    int ky = 0, kx = 0, c0 = 0, kl = 0;
-    const unsigned short* ap[RA];
-    size_t st[RA], pst[RA];  // channel-block and plane strides of a row's source (0 on the zero block)
-    auto tap = [&]() {
+    // the rows' nine tap pixels, once: element offset of tap t = ky KS + kx within the row's image plane
+    // (channel block 0), or ~0u outside the map (the tile then reads the zero block with strides 0).  The
+    // K loop is unrolled over a channel block's KS KS taps, so the tap index is a compile-time constant.
+    constexpr int NT = KS * KS;
+    unsigned toff[RA][NT];
 #pragma unroll
-        for (int r = 0; r < RA; ++r) {
-            const int iy = iy0[r] + ky, ix = ix0[r] + kx;
+    for (int r = 0; r < RA; ++r)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            const int iy = iy0[r] + t / KS, ix = ix0[r] + t % KS;
             const bool ok = vm[r] && (unsigned)iy < (unsigned)a.Hi && (unsigned)ix < (unsigned)a.Wi;
-            ap[r] = ok ? pa[r] + ((size_t)iy * a.Wi + vae_col(ix, a.Wi, a.in_ph)) * 16 : a.zero + 8 * shalf;
-            st[r] = ok ? HWi : 0;
-            pst[r] = ok ? a.ips : 0;
+            toff[r][t] = ok ? (unsigned)((iy * a.Wi + vae_col(ix, a.Wi, a.in_ph)) * 16) : ~0u;
         }
-    };
-    tap();
-    // K-tile kl into LDS buffer bc (per load, a wave's 32 rows of a plane: 1 KB), then advance
-    auto issue = [&](auto bc) {
+    int kl = 0;                // next K-tile to stage
+    size_t cofs = 0;           // its channel block's element offset (c0 H W)
+    // K-tile kl (tap tc, K order (channel block, ky, kx)) into LDS buffer bc (per load, a wave's 32 rows of
+    // a plane: 1 KB), then advance
+    auto issue = [&](auto bc, auto tc) {
+        constexpr int t = decltype(tc)::value;
         auto* LA = As(bc);
         auto* LB = Bs(bc);
+        if (t == 0 && kl > 0) cofs += (size_t)CV_BK * HWi;  // the next channel block
 #ifndef VAE_DIAG_NOISSUE  // diagnostic build: no staging loads at all (results invalid)
+        const unsigned short* ap[RA];
+        size_t pst[RA];
+#pragma unroll
+        for (int r = 0; r < RA; ++r) {
+            const bool ok = toff[r][t] != ~0u;
+            ap[r] = ok ? pa[r] + cofs + toff[r][t] : a.zero + 8 * shalf;
+            pst[r] = ok ? a.ips : 0;
+        }
 #pragma unroll
         for (int p = 0; p < 3; ++p) {
+#ifndef VAE_DIAG_NOA  // diagnostic build: no A staging loads (results invalid)
 #pragma unroll
             for (int r = 0; r < RA; ++r)
-                __builtin_amdgcn_global_load_lds((const void*)(ap[r] + (size_t)c0 * st[r] + p * pst[r]),
+                __builtin_amdgcn_global_load_lds((const void*)(ap[r] + p * pst[r]),
                                                  (ldsv*)&LA[p][2048 * r + 512 * wave], 16, 0, 0);
+#endif
+#ifndef VAE_DIAG_NOB  // diagnostic build: no B staging loads (results invalid)
 #pragma unroll
             for (int r = 0; r < RB; ++r)
                 __builtin_amdgcn_global_load_lds((const void*)(pb + ((size_t)r * KT + kl) * (128 * CV_BK) + p * wps),
                                                  (ldsv*)&LB[p][2048 * r + 512 * wave], 16, 0, 0);
+#endif
         }
 #else
         (void)LA; (void)LB;
 #endif
-        // K order (channel block, ky, kx): the nine taps of a channel block are consecutive K-tiles, so
-        // the rows' input pixels are re-read while they are still in L2
-        if constexpr (KS > 1) {
-            if (++kx == KS) {
-                kx = 0;
-                if (++ky == KS) {
-                    ky = 0;
-                    c0 += CV_BK;
-                }
-            }
-            tap();
-        } else {
-            c0 += CV_BK;
-        }
         ++kl;
     };
 
@@ -580,43 +587,37 @@ __global__ __launch_bounds__(256, 2) void vae_conv_kernel(VaeConvArgs a) {
     // order, so the NV loads of the tile after it may stay in flight), then a barrier (every thread's DMA
     // of tile kt has landed; every wave's reads of the buffer about to be refilled are done), stage tile
     // kt + NB - 1, and the products of tile kt under the tiles in flight.
-    using I0 = std::integral_constant<int, 0>;
-    using I1 = std::integral_constant<int, 1>;
-    using I2 = std::integral_constant<int, 2>;
-    int kt = 0;
-    if constexpr (NB == 3) {
-        auto step = [&](int kt, auto bc, auto bnext) {
+    // Steps are unrolled over L = lcm(NB, KS KS) K-tiles (9 for 3x3: a channel block; NB for 1x1), so
+    // buffer and tap are compile-time constants; 3x3 layers have KT = 9 Cin / 16, a multiple of 9.
+    constexpr int L = std::lcm(NB, KS > 1 ? NT : 1);
+    auto stepc = [&](int kt, auto sc) {
+        constexpr int s = decltype(sc)::value;
+        using BC = std::integral_constant<int, s % NB>;
+        using BN = std::integral_constant<int, (s + NB - 1) % NB>;
+        using TN = std::integral_constant<int, (s + NB - 1) % (KS > 1 ? NT : 1)>;
+        if constexpr (NB == 3) {
 #ifdef VAE_DIAG_NOWAIT  // diagnostic build: the products do not wait for the DMA (results invalid)
             if (kt + 1 < KT) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 #else
             if (kt + 1 < KT) asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"i"(NV) : "memory");
 #endif
             else asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (kt + 2 < KT) issue(bnext);
-            products(bc);
-        };
-        issue(I0{});
-        if (KT > 1) issue(I1{});
-        for (; kt + 3 <= KT; kt += 3) {
-            step(kt, I0{}, I2{});
-            step(kt + 1, I1{}, I0{});
-            step(kt + 2, I2{}, I1{});
-        }
-        if (kt < KT) step(kt, I0{}, I2{});
-        if (kt + 1 < KT) step(kt + 1, I1{}, I0{});
-    } else {
-        auto step = [&](int kt, auto bc, auto bnext) {
+        } else {
             asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (kt + 1 < KT) issue(bnext);
-            products(bc);
-        };
-        issue(I0{});
-        for (; kt + 2 <= KT; kt += 2) {
-            step(kt, I0{}, I1{});
-            step(kt + 1, I1{}, I0{});
         }
-        if (kt < KT) step(kt, I0{}, I1{});
-    }
+        if (kt + NB - 1 < KT) issue(BN{}, TN{});
+        products(BC{});
+    };
+    // prologue: tiles 0 .. NB - 2
+    issue(std::integral_constant<int, 0>{}, std::integral_constant<int, 0>{});
+    if constexpr (NB == 3)
+        if (KT > 1) issue(std::integral_constant<int, 1>{}, std::integral_constant<int, (KS > 1 ? 1 : 0)>{});
+    int kt = 0;
+    for (; kt + L <= KT; kt += L)
+        cv_static_for([&](auto sc) { stepc(kt + decltype(sc)::value, sc); }, std::make_integer_sequence<int, L>{});
+    // the last KT % L tiles (none for the encoder's 3x3 layers)
+    cv_static_for([&](auto sc) { if (kt + decltype(sc)::value < KT) stepc(kt + decltype(sc)::value, sc); },
+                  std::make_integer_sequence<int, L - 1>{});
 
     // epilogue (C^T): lane (lr, lh) holds pixel 32 i + lr of the wave's rows and, in register quad g,
     // channels 32 j + 8 g + 4 lh .. + 3
@@ -648,24 +649,13 @@ __global__ __launch_bounds__(256, 2) void vae_conv_kernel(VaeConvArgs a) {
     }
 }
 
-// tile shape per layer: VAE_CV_SHAPE 0 = 128 x 128 (three LDS buffers), 1 = wide (128 x 256 when Cout is a
-// multiple of 256, else 256 x 128; two buffers).  Both measured within 1 % of each other;
-// the product is the 128 x 128 tile.
-#ifndef VAE_CV_SHAPE
-#define VAE_CV_SHAPE 0
-#endif
+// The product tile is 128 x 128 with three LDS buffers.  (Round 5 measured a 128 x 256 / 256 x 128 tile
+// with two buffers -- 48 MFMAs per wave and barrier -- at 11.39-11.5 vs 11.26-11.31 ms per 512 images;
+// the template keeps WM, WN, NB as parameters.)
 template <int KS, int S>
 static void cv_launch(const VaeConvArgs& a, long long M, hipStream_t s) {
-    if (VAE_CV_SHAPE == 0) {
-        const long long g = ((M + 127) / 128) * (a.Cout / 128);
-        hipLaunchKernelGGL((vae_conv_kernel<KS, S, 2, 2, 3>), dim3((unsigned)g), dim3(256), 0, s, a);
-    } else if (a.Cout % 256 == 0) {
-        const long long g = ((M + 127) / 128) * (a.Cout / 256);
-        hipLaunchKernelGGL((vae_conv_kernel<KS, S, 2, 4, 2>), dim3((unsigned)g), dim3(256), 0, s, a);
-    } else {
-        const long long g = ((M + 255) / 256) * (a.Cout / 128);
-        hipLaunchKernelGGL((vae_conv_kernel<KS, S, 4, 2, 2>), dim3((unsigned)g), dim3(256), 0, s, a);
-    }
+    const long long g = ((M + 127) / 128) * (a.Cout / 128);
+    hipLaunchKernelGGL((vae_conv_kernel<KS, S, 2, 2, 3>), dim3((unsigned)g), dim3(256), 0, s, a);
 }
 
 hipError_t launch_vae_conv(const VaeConvArgs& a, int ks, int stride, hipStream_t s) {
