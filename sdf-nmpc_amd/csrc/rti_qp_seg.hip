@@ -104,23 +104,27 @@ __device__ __forceinline__ double rsqrt2(double v) {
 // In-register Cholesky, one column per lane: lane c < 10 holds column c of an SPD 10 x 10 matrix in
 // col[0..9]; on return column c of L (col[i] = L[i][c], 0 above the diagonal) and inv[j] = 1 / L[j][j]
 // (uniform).  Lanes >= 10 compute garbage that is never read.
+// The elimination runs on the unscaled columns (the Schur complements A'); lane c scales its column by
+// 1 / L[c][c] once at the end, and the rank-1 update is masked through its multiplier (0 in lanes <= j:
+// fma(-a, 0, x) = x exactly), so a pivot costs its broadcasts, its 1/sqrt and one fma per row instead of
+// a branch, ten multiplies and two selects per row -- the same operations on the same values as the
+// column-at-a-time form, so the same bits.
 __device__ __forceinline__ void chol_cols(double (&col)[NX], double (&inv)[NX], int lane) {
+    double myinv = 0.0;
 #pragma unroll
     for (int j = 0; j < NX; ++j) {
         const double d = rdlane(col[j], j);
         const double iv = rsqrt_nr(d);
         inv[j] = iv;
-        // A[i][c] -= L[i][j] L[c][j] = A[i][j] A[c][j] / d  (A symmetric: A[j][c] = A[c][j])
-        const double tcj = col[j] * (iv * iv);
+        myinv = lane == j ? iv : myinv;
+        // A'[i][c] -= A'[i][j] A'[c][j] / d for c > j, i > j  (A' symmetric: A'[c][j] = col[j] in lane c)
+        const double tcj = lane > j ? col[j] * (iv * iv) : 0.0;
 #pragma unroll
-        for (int i = j + 1; i < NX; ++i) col[i] = lane > j ? fma(-rdlane(col[i], j), tcj, col[i]) : col[i];
-        // column j itself: L[i][j] = A[i][j] / L[j][j] for i >= j (a branch: as selects, 20 v_cndmask per
-        // column made the factorisation 20 % slower)
-        if (lane == j) {
-#pragma unroll
-            for (int i = 0; i < NX; ++i) col[i] = i < j ? 0.0 : col[i] * iv;
-        }
+        for (int i = j + 1; i < NX; ++i) col[i] = fma(-rdlane(col[i], j), tcj, col[i]);
     }
+    // L[i][c] = A'[i][c] / L[c][c] for i >= c
+#pragma unroll
+    for (int i = 0; i < NX; ++i) col[i] = i < lane ? 0.0 : col[i] * myinv;
 }
 
 struct SegSmem {
