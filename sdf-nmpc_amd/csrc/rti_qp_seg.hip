@@ -450,11 +450,13 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
                 off -= (fx ? 1.0 : 0.0) * bdv + (fu ? 1.0 : 0.0) * dv;  // bdv used by every lane: its reads stay unconditional
             }
         }
-        refill();
+        // x_k (the chain's LDS hand-off) is read before the refill, so the refill's lgkmcnt(0) covers it
+        // together with the window reads: one LDS round trip on the chain instead of two
         const ldsd2* xp = (const ldsd2*)(s.dxc + k * NX);
         d2 xv[NX / 2];
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) xv[l] = xp[l];
+        refill();
         double a0 = off, a1 = 0.0;
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) {
