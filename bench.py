@@ -257,12 +257,12 @@ def main():
         x1, u1_, u01 = b1["x"].clone(), b1["u"].clone(), torch.empty((1, 4), dtype=torch.float64, device=dev)
         x1[:, 0].copy_(b1["x0"])  # ocp.py:161, as above
 
+        rti1 = _lib.RtiStep(ctx, net, model, qopts, 1, N, np_, b1, u0=u01)  # argument blocks bound once
+
         def step1():
             b1["x"].copy_(x1)
             b1["u"].copy_(u1_)
-            _lib.rti_prepare(ctx, net, model, qopts, 1, N, np_, b1)
-            _lib.qp_feedback(ctx, qopts, 1, N, b1)
-            _lib.rti_apply(ctx, 1, N, b1["x"], b1["u"], b1["dx"], b1["du"], u01)
+            rti1()
         for _ in range(5):
             step1()
         l1 = []

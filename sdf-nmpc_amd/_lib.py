@@ -438,6 +438,30 @@ def qp_feedback(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
     _check(load().sdfnmpc_qp_feedback(ctx.h, C.byref(opts), C.byref(a)))
 
 
+class RtiStep:
+    """One SQP-RTI control step (rti_prepare + qp_feedback + rti_apply) over buffers bound once: the ctypes
+    argument blocks are built here, not per call, so a step costs three foreign calls of host time (the
+    per-call form spends ~15 us of Python per phase building them, on the B = 1 latency path).  The bound
+    tensors must stay alive and at the same addresses."""
+
+    def __init__(self, ctx: Context, net, model: QuadModelC, opts: QpOptsC, B: int, N: int, np_: int, bufs: dict,
+                 u0=None, latent_mode=0, no_sdf=False):
+        self._lib = load()
+        self._ctx, self._net = ctx.h, None if net is None else net.h
+        self._model, self._opts, self._B, self._N = model, opts, B, N
+        self._la = lin_args(B, N, np_, bufs, latent_mode, opts.nyN, no_sdf)
+        self._qa = QpArgsC(B, N, *[_ptr(bufs.get(k)) for k in QP_IN + QP_OUT])
+        self._apply = (_ptr(bufs["x"]), _ptr(bufs["u"]), _ptr(bufs["dx"]), _ptr(bufs["du"]), _ptr(u0),
+                       _ptr(bufs.get("status")))
+        self._keep = (bufs, u0)
+
+    def __call__(self):
+        lib, r = self._lib, C.byref
+        _check(lib.sdfnmpc_rti_prepare(self._ctx, self._net, r(self._model), r(self._la), r(self._opts), r(self._qa)))
+        _check(lib.sdfnmpc_qp_feedback(self._ctx, r(self._opts), r(self._qa)))
+        _check(lib.sdfnmpc_rti_apply(self._ctx, self._B, self._N, *self._apply))
+
+
 def rti_apply(ctx: Context, B: int, N: int, x, u, dx, du, u0=None, status=None):
     """x += dx, u += du, u0 = u[:, 0]; instances whose QP status is >= 2 (numerical failure) keep x, u."""
     _check(load().sdfnmpc_rti_apply(ctx.h, B, N, _ptr(x), _ptr(u), _ptr(dx), _ptr(du), _ptr(u0), _ptr(status)))

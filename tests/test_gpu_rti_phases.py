@@ -79,3 +79,29 @@ def test_feedback_needs_a_matching_preparation(gpu_ctx, cfg):
     with pytest.raises(_lib.SdfnmpcError, match="rti_prepare"):
         _lib.qp_feedback(gpu_ctx, opts, B - 1, N, t)       # another batch than the one prepared
     gpu_ctx.synchronize()
+
+
+@pytest.mark.parametrize("B,N", [(1, 40), (8, 20)])
+def test_bound_rti_step_bitwise_equals_per_call_phases(gpu_ctx, cfg, B, N):
+    """_lib.RtiStep (argument blocks bound once, the B = 1 latency leg of bench.py) runs the same three
+    entry points as the per-call wrappers: two closed-loop steps, bitwise the same iterates and outputs."""
+    import torch
+    net = _lib.Net.siren(gpu_ctx, 0)
+    model = _model(cfg, False)
+    opts = _lib.qp_opts(model)
+    qm = _lib.quad_model(cfg)
+    prob, ta = _bufs(gpu_ctx, cfg, B, N, 11, False)
+    _, tb = _bufs(gpu_ctx, cfg, B, N, 11, False)
+    np_ = prob["p"].shape[-1]
+    ua = torch.empty((B, 4), dtype=torch.float64, device=ta["x"].device)
+    ub = torch.empty_like(ua)
+    step = _lib.RtiStep(gpu_ctx, net, qm, opts, B, N, np_, tb, u0=ub)
+    for _ in range(2):
+        _lib.rti_prepare(gpu_ctx, net, qm, opts, B, N, np_, ta)
+        _lib.qp_feedback(gpu_ctx, opts, B, N, ta)
+        _lib.rti_apply(gpu_ctx, B, N, ta["x"], ta["u"], ta["dx"], ta["du"], ua, ta["status"])
+        step()
+    gpu_ctx.synchronize()
+    for k in OUT + ("x", "u"):
+        np.testing.assert_array_equal(ta[k].cpu().numpy(), tb[k].cpu().numpy(), err_msg=k)
+    np.testing.assert_array_equal(ua.cpu().numpy(), ub.cpu().numpy())

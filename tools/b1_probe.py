@@ -29,9 +29,15 @@ x1, u1, u0 = b1["x"].clone(), b1["u"].clone(), torch.empty((1, 4), dtype=torch.f
 np_ = prob["p"].shape[-1]
 print("QP kernel:", ctx.qp_kernel(N, 1))
 
+rti1 = _lib.RtiStep(ctx, net, cmodel, qopts, 1, N, np_, b1, u0=u0) if hasattr(_lib, "RtiStep") else None
+
+
 def step():
     b1["x"].copy_(x1)
     b1["u"].copy_(u1)
+    if rti1 is not None and not os.environ.get("B1_PERCALL"):
+        rti1()
+        return
     _lib.rti_prepare(ctx, net, cmodel, qopts, 1, N, np_, b1)
     _lib.qp_feedback(ctx, qopts, 1, N, b1)
     _lib.rti_apply(ctx, 1, N, b1["x"], b1["u"], b1["dx"], b1["du"], u0)
