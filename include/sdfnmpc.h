@@ -48,7 +48,7 @@
 extern "C" {
 #endif
 
-#define SDFNMPC_ABI_VERSION 5
+#define SDFNMPC_ABI_VERSION 6
 
 enum {
     SDFNMPC_OK = 0,
@@ -315,6 +315,20 @@ int sdfnmpc_qp_feedback(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* opts, const sdf
  * instances with status >= 2 (QP failure) keep x and u; their u0 is the unchanged u[:, 0]. */
 int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, const double* dx, const double* du,
                       double* u0, const int* status);
+
+/* One whole SQP-RTI control step -- sdfnmpc_rti_prepare + sdfnmpc_qp_feedback + sdfnmpc_rti_apply on
+ * fixed buffers -- captured once into a HIP graph and replayed by sdfnmpc_step_launch with one host call
+ * (the latency path: the per-call form spends its host time in ≈10 runtime calls per step).  create runs the
+ * step once eagerly (workspaces allocated, arguments checked), then captures it on a private stream; launch
+ * enqueues the graph on the context stream.  The buffers named in the arguments must stay allocated at the
+ * same addresses; results are bitwise those of the three calls.  Timing (sdfnmpc_ctx_enable_timing) does not
+ * see graph launches.  (Not a reference interface: the acados solver object's solve() is one call too.) */
+typedef struct sdfnmpc_step sdfnmpc_step;
+int sdfnmpc_step_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* model,
+                        const sdfnmpc_lin_args* lin_args, const sdfnmpc_qp_opts* opts, const sdfnmpc_qp_args* qp_args,
+                        double* u0, const int* status, sdfnmpc_step** out);
+int sdfnmpc_step_launch(sdfnmpc_ctx* ctx, sdfnmpc_step* step);
+void sdfnmpc_step_destroy(sdfnmpc_step* step);
 
 /* ---- batched reference / parameter packing into the OCP device buffers (sdfnmpc_ref_args) ---- */
 int sdfnmpc_pack_refs(sdfnmpc_ctx* ctx, const sdfnmpc_ref_opts* opts, const sdfnmpc_ref_args* args);

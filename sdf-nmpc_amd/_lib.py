@@ -28,7 +28,7 @@ SYMBOLS = [
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
     "sdfnmpc_linearize", "sdfnmpc_shooting_grid", "sdfnmpc_qp_solve", "sdfnmpc_rti_prepare", "sdfnmpc_qp_feedback",
-    "sdfnmpc_rti_apply", "sdfnmpc_pack_refs",
+    "sdfnmpc_rti_apply", "sdfnmpc_step_create", "sdfnmpc_step_launch", "sdfnmpc_step_destroy", "sdfnmpc_pack_refs",
     "sdfnmpc_vae_load", "sdfnmpc_vae_free", "sdfnmpc_vae_size_latent", "sdfnmpc_vae_encode",
     "sdfnmpc_ctx_device", "sdfnmpc_dev_alloc", "sdfnmpc_dev_free", "sdfnmpc_memcpy",
     "sdfnmpc_solver_create", "sdfnmpc_solver_destroy", "sdfnmpc_solver_field", "sdfnmpc_solver_upload",
@@ -157,6 +157,9 @@ def load():
         "sdfnmpc_rti_prepare": (i, [vp, vp, P(QuadModelC), P(LinArgsC), P(QpOptsC), P(QpArgsC)]),
         "sdfnmpc_qp_feedback": (i, [vp, P(QpOptsC), P(QpArgsC)]),
         "sdfnmpc_rti_apply": (i, [vp, i, i, vp, vp, vp, vp, vp, vp]),
+        "sdfnmpc_step_create": (i, [vp, vp, P(QuadModelC), P(LinArgsC), P(QpOptsC), P(QpArgsC), vp, vp, P(vp)]),
+        "sdfnmpc_step_launch": (i, [vp, vp]),
+        "sdfnmpc_step_destroy": (None, [vp]),
         "sdfnmpc_pack_refs": (i, [vp, P(RefOptsC), P(RefArgsC)]),
         "sdfnmpc_vae_load": (i, [vp, vp, sz, P(vp)]),
         "sdfnmpc_vae_free": (None, [vp]),
@@ -179,7 +182,7 @@ def load():
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
         fn.restype, fn.argtypes = res, args
-    if lib.sdfnmpc_abi_version() != 5:
+    if lib.sdfnmpc_abi_version() != 6:
         raise SdfnmpcError("libsdfnmpc.so ABI version mismatch")
     _lib = lib
     return lib
@@ -440,12 +443,13 @@ def qp_feedback(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):
 
 class RtiStep:
     """One SQP-RTI control step (rti_prepare + qp_feedback + rti_apply) over buffers bound once: the ctypes
-    argument blocks are built here, not per call, so a step costs three foreign calls of host time (the
-    per-call form spends ~15 us of Python per phase building them, on the B = 1 latency path).  The bound
-    tensors must stay alive and at the same addresses."""
+    argument blocks are built here, not per call (the per-call form spends ~15 us of Python per phase
+    building them, on the B = 1 latency path).  graph=True: the step is captured into a HIP graph
+    (sdfnmpc_step_create, which runs it once eagerly) and a call is one graph launch.  The bound tensors
+    must stay alive and at the same addresses."""
 
     def __init__(self, ctx: Context, net, model: QuadModelC, opts: QpOptsC, B: int, N: int, np_: int, bufs: dict,
-                 u0=None, latent_mode=0, no_sdf=False):
+                 u0=None, latent_mode=0, no_sdf=False, graph=False):
         self._lib = load()
         self._ctx, self._net = ctx.h, None if net is None else net.h
         self._model, self._opts, self._B, self._N = model, opts, B, N
@@ -453,13 +457,30 @@ class RtiStep:
         self._qa = QpArgsC(B, N, *[_ptr(bufs.get(k)) for k in QP_IN + QP_OUT])
         self._apply = (_ptr(bufs["x"]), _ptr(bufs["u"]), _ptr(bufs["dx"]), _ptr(bufs["du"]), _ptr(u0),
                        _ptr(bufs.get("status")))
-        self._keep = (bufs, u0)
+        self._keep = (bufs, u0, ctx, net)
+        self._step = None
+        if graph:
+            for t in list(bufs.values()) + [u0]:
+                sync_producer(t)
+            h = C.c_void_p()
+            _check(self._lib.sdfnmpc_step_create(self._ctx, self._net, C.byref(model), C.byref(self._la),
+                                                 C.byref(opts), C.byref(self._qa), self._apply[4], self._apply[5],
+                                                 C.byref(h)))
+            self._step = h
 
     def __call__(self):
         lib, r = self._lib, C.byref
+        if self._step is not None:
+            _check(lib.sdfnmpc_step_launch(self._ctx, self._step))
+            return
         _check(lib.sdfnmpc_rti_prepare(self._ctx, self._net, r(self._model), r(self._la), r(self._opts), r(self._qa)))
         _check(lib.sdfnmpc_qp_feedback(self._ctx, r(self._opts), r(self._qa)))
         _check(lib.sdfnmpc_rti_apply(self._ctx, self._B, self._N, *self._apply))
+
+    def __del__(self):
+        if getattr(self, "_step", None) is not None:
+            self._lib.sdfnmpc_step_destroy(self._step)
+            self._step = None
 
 
 def rti_apply(ctx: Context, B: int, N: int, x, u, dx, du, u0=None, status=None):

@@ -1587,6 +1587,90 @@ extern "C" int sdfnmpc_qp_feedback(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, c
     return SDFNMPC_OK;
 }
 
+// ------------------------------------------------------------------------------------------------
+// the control step as a HIP graph (include/sdfnmpc.h sdfnmpc_step_create)
+struct sdfnmpc_step {
+    hipGraph_t graph = nullptr;
+    hipGraphExec_t exec = nullptr;
+    int device = 0;
+};
+
+static int step_eager(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl, const sdfnmpc_lin_args* la,
+                      const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* qa, double* u0, const int* status) {
+    if (int rc = sdfnmpc_rti_prepare(ctx, net, mdl, la, o, qa)) return rc;
+    if (int rc = sdfnmpc_qp_feedback(ctx, o, qa)) return rc;
+    // the step applies to the iterate the QP linearised about (qp_args.x, .u: the caller's writable buffers)
+    return sdfnmpc_rti_apply(ctx, qa->B, qa->N, const_cast<double*>(qa->x), const_cast<double*>(qa->u), qa->dx, qa->du, u0,
+                             status);
+}
+
+extern "C" int sdfnmpc_step_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
+                                   const sdfnmpc_lin_args* la, const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* qa,
+                                   double* u0, const int* status, sdfnmpc_step** out) {
+    if (!ctx || !mdl || !la || !o || !qa || !out) return fail(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_step_create");
+    *out = nullptr;
+    if (qa->B < 1) return fail(SDFNMPC_E_ARG, "step_create: B must be >= 1");
+    // once eagerly: every workspace is allocated and every argument checked before the capture (no
+    // allocation may happen inside it)
+    if (int rc = step_eager(ctx, net, mdl, la, o, qa, u0, status)) return rc;
+    ScopedDevice sd(ctx->device);
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // capture on a private stream (the context stream may be the legacy null stream, which cannot be
+    // captured); the fork / join events bring the auxiliary stream into the capture
+    hipStream_t cs = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&cs, hipStreamNonBlocking));
+    hipStream_t saved = ctx->stream;
+    const bool timing = ctx->timing;
+    ctx->timing = false;
+    ctx->stream = cs;
+    hipGraph_t g = nullptr;
+    int rc = SDFNMPC_OK;
+    hipError_t e = hipStreamBeginCapture(cs, hipStreamCaptureModeRelaxed);
+    if (e == hipSuccess) {
+        rc = step_eager(ctx, net, mdl, la, o, qa, u0, status);
+        e = hipStreamEndCapture(cs, &g);  // always ends the capture, also after a failed call
+    }
+    ctx->stream = saved;
+    ctx->timing = timing;
+    (void)hipStreamDestroy(cs);
+    if (rc) {
+        if (g) (void)hipGraphDestroy(g);
+        return rc;
+    }
+    if (e != hipSuccess || !g) {
+        if (g) (void)hipGraphDestroy(g);
+        return fail(SDFNMPC_E_HIP, std::string("step_create: stream capture failed: ") + hipGetErrorString(e));
+    }
+    hipGraphExec_t x = nullptr;
+    e = hipGraphInstantiate(&x, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        (void)hipGraphDestroy(g);
+        return fail(SDFNMPC_E_HIP, std::string("step_create: graph instantiation failed: ") + hipGetErrorString(e));
+    }
+    auto* st = new sdfnmpc_step;
+    st->graph = g;
+    st->exec = x;
+    st->device = ctx->device;
+    *out = st;
+    return SDFNMPC_OK;
+}
+
+extern "C" int sdfnmpc_step_launch(sdfnmpc_ctx* ctx, sdfnmpc_step* st) {
+    if (!ctx || !st) return fail(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_step_launch");
+    if (st->device != ctx->device) return fail(SDFNMPC_E_ARG, "step_launch: step captured on another device");
+    ScopedDevice sd(ctx->device);
+    HIPCHK(hipGraphLaunch(st->exec, ctx->stream));
+    return SDFNMPC_OK;
+}
+
+extern "C" void sdfnmpc_step_destroy(sdfnmpc_step* st) {
+    if (!st) return;
+    ScopedDevice sd(st->device);
+    if (st->exec) (void)hipGraphExecDestroy(st->exec);
+    if (st->graph) (void)hipGraphDestroy(st->graph);
+    delete st;
+}
+
 extern "C" int sdfnmpc_pack_refs(sdfnmpc_ctx* ctx, const sdfnmpc_ref_opts* o, const sdfnmpc_ref_args* a) {
     if (!ctx || !o || !a) return fail(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_pack_refs");
     if (a->B < 0 || a->N < 1 || a->np < 17 || (a->ny != 11 && a->ny != 12) || !a->p)

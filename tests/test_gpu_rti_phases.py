@@ -81,10 +81,11 @@ def test_feedback_needs_a_matching_preparation(gpu_ctx, cfg):
     gpu_ctx.synchronize()
 
 
-@pytest.mark.parametrize("B,N", [(1, 40), (8, 20)])
-def test_bound_rti_step_bitwise_equals_per_call_phases(gpu_ctx, cfg, B, N):
-    """_lib.RtiStep (argument blocks bound once, the B = 1 latency leg of bench.py) runs the same three
-    entry points as the per-call wrappers: two closed-loop steps, bitwise the same iterates and outputs."""
+@pytest.mark.parametrize("B,N,graph", [(1, 40, False), (8, 20, False), (1, 40, True), (8, 20, True)])
+def test_bound_rti_step_bitwise_equals_per_call_phases(gpu_ctx, cfg, B, N, graph):
+    """_lib.RtiStep (argument blocks bound once; graph=True: the step captured into a HIP graph by
+    sdfnmpc_step_create and replayed, the B = 1 latency leg of bench.py) runs the same three entry points
+    as the per-call wrappers: closed-loop steps, bitwise the same iterates and outputs."""
     import torch
     net = _lib.Net.siren(gpu_ctx, 0)
     model = _model(cfg, False)
@@ -95,7 +96,11 @@ def test_bound_rti_step_bitwise_equals_per_call_phases(gpu_ctx, cfg, B, N):
     np_ = prob["p"].shape[-1]
     ua = torch.empty((B, 4), dtype=torch.float64, device=ta["x"].device)
     ub = torch.empty_like(ua)
-    step = _lib.RtiStep(gpu_ctx, net, qm, opts, B, N, np_, tb, u0=ub)
+    if graph:  # create runs one step eagerly: the per-call side takes one step first
+        _lib.rti_prepare(gpu_ctx, net, qm, opts, B, N, np_, ta)
+        _lib.qp_feedback(gpu_ctx, opts, B, N, ta)
+        _lib.rti_apply(gpu_ctx, B, N, ta["x"], ta["u"], ta["dx"], ta["du"], ua, ta["status"])
+    step = _lib.RtiStep(gpu_ctx, net, qm, opts, B, N, np_, tb, u0=ub, graph=graph)
     for _ in range(2):
         _lib.rti_prepare(gpu_ctx, net, qm, opts, B, N, np_, ta)
         _lib.qp_feedback(gpu_ctx, opts, B, N, ta)

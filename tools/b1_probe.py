@@ -29,7 +29,8 @@ x1, u1, u0 = b1["x"].clone(), b1["u"].clone(), torch.empty((1, 4), dtype=torch.f
 np_ = prob["p"].shape[-1]
 print("QP kernel:", ctx.qp_kernel(N, 1))
 
-rti1 = _lib.RtiStep(ctx, net, cmodel, qopts, 1, N, np_, b1, u0=u0) if hasattr(_lib, "RtiStep") else None
+rti1 = (_lib.RtiStep(ctx, net, cmodel, qopts, 1, N, np_, b1, u0=u0, graph=bool(os.environ.get("B1_GRAPH")))
+        if hasattr(_lib, "RtiStep") else None)
 
 
 def step():
