@@ -43,6 +43,19 @@ __device__ __forceinline__ dd datan2(dd y, dd x) {
     return {atan2(y.v, x.v), (x.v * y.t - y.v * x.t) / den};
 }
 
+// the value of the partner lane of a pair (lanes 2i, 2i + 1: DPP quad_perm [1, 0, 3, 2])
+__device__ __forceinline__ double pair_swap(double x) {
+    const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+    const unsigned lo = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)u, 0xB1, 0xF, 0xF, false);
+    const unsigned hi = (unsigned)__builtin_amdgcn_mov_dpp((int)(unsigned)(u >> 32), 0xB1, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+// atan2 as a dual number from its value (computed elsewhere)
+__device__ __forceinline__ dd datan2_v(dd y, dd x, double v) {
+    const double den = x.v * x.v + y.v * y.v;
+    return {v, (x.v * y.t - y.v * x.t) / den};
+}
+
 // 1 / sqrt(a) as a dual number (a > 0): the hardware estimate and two Newton steps y += y (1 - a y^2) / 2
 // (each squares the relative error: within an ulp or two of the rounded 1 / sqrt(a), 8 instructions in
 // place of a correctly rounded sqrt and division)
@@ -130,8 +143,16 @@ __global__ __launch_bounds__(256, LIN_WAVES) void linearize_kernel(LinArgs A) {
         for (int i = 0; i < 4; ++i) U[i] = {ur[i], (10 + i == t) ? 1.0 : 0.0};
         const dd gamma = U[0] * m.gamma, roll = U[1] * m.roll, pitch = U[2] * m.pitch, wz = U[3] * m.wz;
         double s_r, c_r, s_p, c_p;
-        sincos(roll.v, &s_r, &c_r);
-        sincos(pitch.v, &s_p, &c_p);
+        {  // the node's lanes share roll and pitch: a lane pair splits the two sincos and swaps results
+            const bool odd = sl & 1;
+            double sa, ca;
+            sincos(odd ? pitch.v : roll.v, &sa, &ca);
+            const double sb = pair_swap(sa), cb = pair_swap(ca);
+            s_r = odd ? sb : sa;
+            c_r = odd ? cb : ca;
+            s_p = odd ? sa : sb;
+            c_p = odd ? ca : cb;
+        }
         const dd sr = {s_r, c_r * roll.t}, cr = {c_r, -s_r * roll.t};
         const dd sp = {s_p, c_p * pitch.t}, cp = {c_p, -s_p * pitch.t};
         // ---- ERK4 (Butcher c = [0, 1/2, 1/2, 1], b = [1/6, 1/3, 1/3, 1/6]); acados-style
@@ -259,8 +280,12 @@ __global__ __launch_bounds__(256, LIN_WAVES) void linearize_kernel(LinArgs A) {
     const dd cx = (e0 * R[0] + e1 * R[3]) + e2 * R[6] + C(m.fov_off[0]);
     const dd cy = (e0 * R[1] + e1 * R[4]) + e2 * R[7] + C(m.fov_off[1]);
     const dd cz = (e0 * R[2] + e1 * R[5]) + e2 * R[8] + C(m.fov_off[2]);
-    const dd hf = datan2(cy, cx) * flag;
-    const dd vf = datan2(cz, dsqrt(cx * cx + cy * cy)) * flag;
+    const dd rho = dsqrt(cx * cx + cy * cy);
+    // a lane pair splits the two atan2 values (the node's lanes share them) and swaps results
+    const bool odd = sl & 1;
+    const double at = atan2(odd ? cz.v : cy.v, odd ? rho.v : cx.v), atp = pair_swap(at);
+    const dd hf = datan2_v(cy, cx, odd ? atp : at) * flag;
+    const dd vf = datan2_v(cz, rho, odd ? at : atp) * flag;
     // rows 0, 1 of columns sl (< 3: d/dp_sl) and 3 + sl (zero); row 2 (sdf) is the SDF kernel's epilogue
     double* J = A.Jh + r * 30;
     if (sl < 3) {
