@@ -53,3 +53,27 @@ for _ in range(int(os.environ.get("STEPS", 50))):
     torch.cuda.synchronize()
     lat.append((time.perf_counter() - t) * 1e3)
 print(f"B=1 N={N}: p50 {np.median(lat):.3f} ms, min {np.min(lat):.3f} ms, iters {int(b1['iters'][0])}")
+
+if os.environ.get("B1_HOSTTIME"):  # host time of each call of the (per-call) step, GPU running behind
+    la = _lib.lin_args(1, N, np_, b1, 0, qopts.nyN, False)
+    qa = _lib.QpArgsC(1, N, *[_lib._ptr(b1.get(k)) for k in _lib.QP_IN + _lib.QP_OUT])
+    lib = _lib.load()
+    import ctypes as C
+    ts = {k: [] for k in ("copies", "prepare", "feedback", "apply", "sync")}
+    for _ in range(50):
+        t0 = time.perf_counter()
+        b1["x"].copy_(x1)
+        b1["u"].copy_(u1)
+        t1 = time.perf_counter()
+        lib.sdfnmpc_rti_prepare(ctx.h, net.h, C.byref(cmodel), C.byref(la), C.byref(qopts), C.byref(qa))
+        t2 = time.perf_counter()
+        lib.sdfnmpc_qp_feedback(ctx.h, C.byref(qopts), C.byref(qa))
+        t3 = time.perf_counter()
+        lib.sdfnmpc_rti_apply(ctx.h, 1, N, b1["x"].data_ptr(), b1["u"].data_ptr(), b1["dx"].data_ptr(),
+                              b1["du"].data_ptr(), u0.data_ptr(), b1["status"].data_ptr())
+        t4 = time.perf_counter()
+        torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        for k, a, b in (("copies", t0, t1), ("prepare", t1, t2), ("feedback", t2, t3), ("apply", t3, t4), ("sync", t4, t5)):
+            ts[k].append((b - a) * 1e6)
+    print("host us (median):", {k: round(float(np.median(v)), 1) for k, v in ts.items()})
