@@ -1296,7 +1296,7 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
 // of C^T waits for the join; with the sdf cost (ny == 12) H and g depend on h[2], so the whole pack
 // follows the join.
 static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl,
-                    const sdfnmpc_lin_args* a, const QpArgs* pk) {
+                    const sdfnmpc_lin_args* a, const QpArgs* pk, bool* split_out = nullptr) {
     if (!ctx || !mdl || !a) return fail(SDFNMPC_E_ARG, "NULL argument");
     const bool no_sdf = a->no_sdf != 0;
     if (!net && !no_sdf) return fail(SDFNMPC_E_ARG, "NULL network (only allowed with lin_args.no_sdf)");
@@ -1343,7 +1343,12 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
     la.JhE = a->JhE;
     la.nyN = nyN;
     QpArgs pa{};
-    const bool split = pk && pk->ny == 11 && !ctx->serial_prep && !no_sdf;  // pack beside the SDF kernel
+    // serial: the linearisation (and the whole pack) after the SDF kernel on the one stream -- the diagnostic
+    // SDFNMPC_SERIAL_PREP, and the few-row latency path (B = 1), where the fork / join's event waits cost
+    // more than the overlap gains (round 5: 0.643 vs 0.646 ms per B = 1 step)
+    const bool serial = ctx->serial_prep || (!no_sdf && !net->wide && rows <= SDF_ROW_PREP_MAX);
+    const bool split = pk && pk->ny == 11 && !serial && !no_sdf;  // pack beside the SDF kernel
+    if (split_out) *split_out = split;
     if (pk) {
         pa = *pk;
         pa.pack_part = split ? 1 : 0;
@@ -1351,12 +1356,12 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
     // the fork: ev_fork marks the main stream's state (the inputs written), the auxiliary stream waits for
     // it and runs the linearisation (+ the pack's first part) beside the SDF kernel
     auto fork_mark = [&]() -> int {
-        if (ctx->serial_prep) return SDFNMPC_OK;
+        if (serial) return SDFNMPC_OK;
         HIPCHK(hipEventRecord(ctx->ev_fork, ctx->stream));
         return SDFNMPC_OK;
     };
     auto fork_launch = [&]() -> int {
-        if (ctx->serial_prep) return SDFNMPC_OK;
+        if (serial) return SDFNMPC_OK;
         HIPCHK(hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
         HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->aux); }, ctx->aux));
         if (split) HIPCHK(timed(ctx, "rti_qp_pack", [&] { return launch_rti_qp_pack(pa, ctx->aux); }, ctx->aux));
@@ -1394,7 +1399,7 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
         rc = run_wide(ctx, net, rows, nullptr, nullptr, a->p + 17, stride, n_inst, a->latent_mode == 0 ? a->N + 1 : 1,
                       sdf4, &cons);
         if (rc) return rc;
-        if (ctx->serial_prep) {
+        if (serial) {
             HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }, ctx->stream));
             return finish_pack();
         }
@@ -1423,7 +1428,7 @@ static int lin_impl(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad
                      a->latent_mode == 0 ? a->N + 1 : 1, sdf4, nullptr, ctx->tile_rows, &cons);
         if (rc) return rc;
     }
-    if (ctx->serial_prep) {
+    if (serial) {
         HIPCHK(timed(ctx, "linearize", [&] { return launch_linearize(la, ctx->stream); }, ctx->stream));
         return finish_pack();
     }
@@ -1553,9 +1558,10 @@ extern "C" int sdfnmpc_rti_prepare(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, con
     ScopedDevice sd(ctx->device);
     QpArgs q;
     if (int rc = qp_build(ctx, o, qa, q)) return rc;
-    if (int rc = lin_impl(ctx, net, mdl, la, &q)) return rc;
+    bool split = false;
+    if (int rc = lin_impl(ctx, net, mdl, la, &q, &split)) return rc;
     ctx->prep.valid = true;
-    ctx->prep.sdf_row_patch = q.ny == 11 && !ctx->serial_prep && !la->no_sdf;  // lin_impl's split: no sdf row in the records
+    ctx->prep.sdf_row_patch = split;  // lin_impl's split pack: no sdf row in the records
     ctx->prep.B = qa->B;
     ctx->prep.N = qa->N;
     ctx->prep.xn = qa->xn;
