@@ -791,10 +791,15 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         ldsd* vv = s.vec;
         double col[NX], inv[NX];
         // L = chol(P_b), one column per lane
+        // column `lane` of the symmetric P_b read as its row: ten contiguous doubles, five 16-byte reads
+        {
+            const ldsd2* pr = (const ldsd2*)(Pb + (lane < NX ? lane : 0) * NX);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            const double v = Pb[i * NX + (lane < NX ? lane : 0)];
-            col[i] = lane < NX ? v : (i == (lane & 7) ? 1.0 : 0.0);
+            for (int l = 0; l < NX / 2; ++l) {
+                const d2 v = pr[l];
+                col[2 * l] = lane < NX ? v.x : (2 * l == (lane & 7) ? 1.0 : 0.0);
+                col[2 * l + 1] = lane < NX ? v.y : (2 * l + 1 == (lane & 7) ? 1.0 : 0.0);
+            }
         }
         chol_cols(col, inv, lane);
         SSTAMP(16);
@@ -833,10 +838,14 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
             if (row < NX && c < NX) win[CP_V + row * NX + c] = S[r];
         }
         wave_sync();
+        {  // column `lane` of the symmetric S read as its row (five 16-byte reads)
+            const ldsd2* sr = (const ldsd2*)(win + CP_V + (lane < NX ? lane : 0) * NX);
 #pragma unroll
-        for (int i = 0; i < NX; ++i) {
-            const double v = win[CP_V + i * NX + (lane < NX ? lane : 0)];
-            col[i] = lane < NX ? v : (i == (lane & 7) ? 1.0 : 0.0);
+            for (int l = 0; l < NX / 2; ++l) {
+                const d2 v = sr[l];
+                col[2 * l] = lane < NX ? v.x : (2 * l == (lane & 7) ? 1.0 : 0.0);
+                col[2 * l + 1] = lane < NX ? v.y : (2 * l + 1 == (lane & 7) ? 1.0 : 0.0);
+            }
         }
         chol_cols(col, inv, lane);
         SSTAMP(18);
