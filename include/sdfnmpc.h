@@ -139,16 +139,19 @@ typedef struct {
                               x0 under it, t / lambda by the cold start's rule; 0 = du = 0 (cold) */
     /* The constraint set (gen_model.py:26-149 under flags.enable_sdf / sdf_constraint / vfov_constraint /
      * recursive_feasibility / stability and sensor.hfov < 3.14; sdf-nmpc_amd/model.py builds it).
-     * Stage rows k < N: nh soft rows in the reference's order, row j = column h_col[j] of h / J_h, with
-     * bounds / slack weights lh[j], uh[j], zl[j], Zl[j] above.  Terminal rows: nhN rows, the first nsN soft
+     * Stage rows k < N: nh rows, row j = column h_col[j] of h / J_h, with bounds / slack weights lh[j], uh[j],
+     * zl[j], Zl[j] above; the first nh - nhs soft, the last nhs hard (slack weight None: add_const_stage,
+     * base_model.py:142-155; zl / Zl unused).  Terminal rows: nhN rows, the first nsN soft
      * (lhN / uhN, slack weights zlN / ZlN, not cost-scaled), the rest hard; row j's value is
      * h[N][hN_col[j]] (if >= 0) + hE[hE_col[j]] (if >= 0), its Jacobian the same sum of columns. */
     int nh;                /* 0..3 (3: [hfov, vfov, sdf], the default flags) */
-    int h_col[3];          /* increasing */
+    int h_col[3];          /* distinct columns 0..2 */
     int nhN, nsN;          /* nhN <= SDFNMPC_NHN_MAX, nsN <= min(nhN, 3), nhN - nsN <= 6 */
     int hN_col[SDFNMPC_NHN_MAX], hE_col[SDFNMPC_NHN_MAX];
     double lhN[SDFNMPC_NHN_MAX], uhN[SDFNMPC_NHN_MAX], zlN[3], ZlN[3];
     int nyN;               /* terminal residual rows (yNref / WN [B][nyN]): 4, or 5 with flags.stability */
+    int nhs;               /* hard stage rows (the last nhs of the nh), 0..nh: mpc.weights.slack_fov / slack_df
+                              None (the terminal copies of those rows are then hard rows of the nhN too) */
 } sdfnmpc_qp_opts;
 
 /* Batched QP of the RTI feedback phase, built from sdfnmpc_linearize outputs. */
@@ -321,7 +324,9 @@ int sdfnmpc_rti_apply(sdfnmpc_ctx* ctx, int B, int N, double* x, double* u, cons
  * (the latency path: the per-call form spends its host time in ≈10 runtime calls per step).  create runs the
  * step once eagerly (workspaces allocated, arguments checked), then captures it on a private stream; launch
  * enqueues the graph on the context stream.  The buffers named in the arguments must stay allocated at the
- * same addresses; results are bitwise those of the three calls.  Timing (sdfnmpc_ctx_enable_timing) does not
+ * same addresses; results are bitwise those of the three calls.  The graph also addresses the context's own
+ * workspaces: a later call on the context that grows them (a larger B or N) reallocates them, and launch then
+ * fails with SDFNMPC_E_ARG instead of running on freed memory (destroy and create the step again).  Timing (sdfnmpc_ctx_enable_timing) does not
  * see graph launches.  (Not a reference interface: the acados solver object's solve() is one call too.) */
 typedef struct sdfnmpc_step sdfnmpc_step;
 int sdfnmpc_step_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* model,

@@ -225,7 +225,8 @@ def qp_ipm_batch(lin, prob, x0, model, lm=10.0, tol=1e-8, max_iter=100, cost_sca
                                         for i, c in enumerate(h_cols)])
     cset = ([len(h_cols)] + pad(h_cols, 3) + [len(rows), sum(1 for r in rows if r[2])] + pad([r[0] for r in rows], 8, -1)
             + pad([r[1] for r in rows], 8, -1) + pad([r[3] for r in rows], 8) + pad([r[4] for r in rows], 8)
-            + pad([r[5] for r in rows if r[2]], 3) + pad([r[6] for r in rows if r[2]], 3) + [arrs["WN"].shape[-1]])
+            + pad([r[5] for r in rows if r[2]], 3) + pad([r[6] for r in rows if r[2]], 3) + [arrs["WN"].shape[-1]]
+            + [int(getattr(model, "nhs", 0))])
     opts = np.concatenate([model.lbu, model.ubu, pad(model.lh, 3), pad(model.uh, 3), pad(model.zl, 3), pad(model.Zl, 3),
                            [lm, tol, float(bool(lm_scaling))],
                            [v for v in {**QP_START, **(start or {}), "ws": float(du_ws is not None)}.values()],

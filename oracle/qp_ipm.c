@@ -40,8 +40,9 @@ typedef struct {
      * that du, t / lambda follow the cold start's rule on the rows there */
     int ws;
     /* the constraint set (include/sdfnmpc.h sdfnmpc_qp_opts): stage rows j < nh = column h_col[j] of h / J_h
-     * (bounds lh .. Zl above); terminal rows j < nhN (the first nsN soft) = h[N][hN_col[j]] + hE[hE_col[j]] */
-    int nh, h_col[3], nhN, nsN, hN_col[NR], hE_col[NR], nyN;
+     * (bounds lh .. Zl above), the last nhs of them hard (slack weight None, base_model.py:142-155); terminal
+     * rows j < nhN (the first nsN soft) = h[N][hN_col[j]] + hE[hE_col[j]] */
+    int nh, h_col[3], nhN, nsN, hN_col[NR], hE_col[NR], nyN, nhs;
     double lhN[NR], uhN[NR], zlN[3], ZlN[3];
 } qp_opts_c;
 
@@ -49,7 +50,7 @@ typedef struct {                  /* stage k < N, or the terminal node k = N (x 
     double A[NX][NX], Bm[NX][NU], c[NX];
     double H[NW][NW], g[NW];
     /* constraint rows j < nrow, the first nsoft soft: C dx + sl + hl >= 0, -C dx + su + hu >= 0 (slacks with
-     * L1 / L2 weights zl / Zl); the rest hard (terminal only): C dx + hl >= 0, -C dx + hu >= 0 */
+     * L1 / L2 weights zl / Zl); the rest hard: C dx + hl >= 0, -C dx + hu >= 0 */
     double C[NR][NX], hl[NR], hu[NR], zl[NR], Zl[NR];
     int nsoft, nrow;
     double dlo[NU], dup[NU];            /* box rows: du + dlo >= 0, -du + dup >= 0 */
@@ -87,10 +88,11 @@ static void chol_solve(int n, const double* L, double* x) {
 }
 
 /* Rows, the order of rti_qp.hip: box rows 8 k + 4 up + i; soft group e (stage groups k ns + j, then the
- * terminal's soft rows) at 8 N + 4 e + q with q = 0 (h lower), 1 (h upper), 2 (sl >= 0), 3 (su >= 0); the
- * hard terminal rows i at RH0 + 2 i (lower), + 1 (upper), RH0 = 8 N + 4 (N ns + nsN). */
+ * terminal's soft rows) at 8 N + 4 e + q with q = 0 (h lower), 1 (h upper), 2 (sl >= 0), 3 (su >= 0); hard
+ * row i (stage rows (k - 1) nhs + j - ns of 0 < k < N, then the terminal's hard rows) at RH0 + 2 i (lower), + 1 (upper),
+ * RH0 = 8 N + 4 (N ns + nsN). */
 typedef struct {
-    int N, m, ns, rh0;            /* ns: soft rows of a stage k < N */
+    int N, m, ns, nhs, rh0;       /* ns / nhs: soft / hard rows of a stage k < N */
     const qp_opts_c* o;
     stage_t* st;
     double x0[NX];                /* dx_0 */
@@ -102,6 +104,9 @@ typedef struct {
 } ipm_t;
 
 static int grp(const ipm_t* Q, int k, int j) { return (k < Q->N ? k * Q->ns : Q->N * Q->ns) + j; }
+/* hard row j (>= the node's soft rows) of node 0 < k <= N: its index among the hard rows (node 0 has none:
+ * acados 0.3.1 takes initial-node nonlinear rows only from con_h_expr_0, which ocp.py does not set) */
+static int hgrp(const ipm_t* Q, int k, int j) { return (k - 1) * Q->nhs + j - Q->st[k].nsoft; }
 
 static void rows_at(const ipm_t* Q, const double* dx, const double* du, const double* sl, const double* su, double* v) {
     const int N = Q->N;
@@ -121,7 +126,7 @@ static void rows_at(const ipm_t* Q, const double* dx, const double* du, const do
                 v[r + 2] = sl[e];
                 v[r + 3] = su[e];
             } else {
-                const int r = Q->rh0 + 2 * (j - Q->st[k].nsoft);
+                const int r = Q->rh0 + 2 * hgrp(Q, k, j);
                 v[r] = cx + Q->st[k].hl[j];
                 v[r + 1] = -cx + Q->st[k].hu[j];
             }
@@ -152,7 +157,7 @@ static void stage_terms(const ipm_t* Q, int k, const double* sig, const double* 
             fg = -(v[r0] * (Zs + sig[r0 + 2]) + sig[r0] * (zs - v[r0 + 2])) / Hl +
                  (v[r0 + 1] * (Zs + sig[r0 + 3]) + sig[r0 + 1] * (zs - v[r0 + 3])) / Hu;
         } else {  /* hard row: the two sides fold like box rows */
-            const int r = Q->rh0 + 2 * (j - S->nsoft);
+            const int r = Q->rh0 + 2 * hgrp(Q, k, j);
             fw = sig[r] + sig[r + 1];
             fg = -v[r] + v[r + 1];
         }
@@ -569,10 +574,10 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
                      const double* x0, const double* yref, const double* W, const double* yNref, const double* WN,
                      const double* dtv, const qp_opts_c* o, int ny, double* dx, double* du, double* slack, int* conv,
                      double* res) {
-    const int N1 = N + 1, nsl = N * o->nh + o->nsN;
-    const int m = 8 * N + 4 * nsl + 2 * (o->nhN - o->nsN);
+    const int N1 = N + 1, nsl = N * (o->nh - o->nhs) + o->nsN;
+    const int m = 8 * N + 4 * nsl + 2 * ((N - 1) * o->nhs + o->nhN - o->nsN);
     ipm_t Q;
-    Q.N = N; Q.m = m; Q.o = o; Q.ns = o->nh; Q.rh0 = 8 * N + 4 * nsl;
+    Q.N = N; Q.m = m; Q.o = o; Q.ns = o->nh - o->nhs; Q.nhs = o->nhs; Q.rh0 = 8 * N + 4 * nsl;
     Q.st = (stage_t*)calloc((size_t)N1, sizeof(stage_t));
     Q.P = (double*)malloc(sizeof(double) * (size_t)N1 * NX * NX);
     Q.p = (double*)malloc(sizeof(double) * (size_t)N1 * NX);
@@ -600,7 +605,8 @@ static int solve_one(int N, const double* xn, const double* AB, const double* y,
         stage_t* S = &Q.st[k];
         S->s = (o->cost_scaling && k < N) ? dtv[k] : 1.0;
         if (k < N) {  /* stage rows: columns h_col of h / J_h */
-            S->nsoft = S->nrow = o->nh;
+            S->nsoft = o->nh - o->nhs;
+            S->nrow = k > 0 ? o->nh : S->nsoft;  /* node 0: no hard row (hgrp) */
             for (int j = 0; j < o->nh; ++j) {
                 const int c = o->h_col[j];
                 for (int l = 0; l < NX; ++l) S->C[j][l] = Jh[((size_t)k * NX + l) * NS + c];
@@ -842,7 +848,8 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
     o.nseg = (int)opts[28];
     o.gk = (int)opts[29]; o.ga = opts[30]; o.gd = opts[31]; o.gbmin = opts[32]; o.gbmax = opts[33];
     o.ws = opts[34] != 0.0;
-    /* the constraint set: opts[35 ..] = nh, h_col 3, nhN, nsN, hN_col 8, hE_col 8, lhN 8, uhN 8, zlN 3, ZlN 3, nyN */
+    /* the constraint set: opts[35 ..] = nh, h_col 3, nhN, nsN, hN_col 8, hE_col 8, lhN 8, uhN 8, zlN 3, ZlN 3, nyN,
+     * nhs */
     const double* cs = opts + 35;
     o.nh = (int)cs[0];
     for (int j = 0; j < 3; ++j) o.h_col[j] = (int)cs[1 + j];
@@ -856,6 +863,7 @@ void orc_qp_ipm_batch(int B, int N, const double* xn, const double* AB, const do
     }
     for (int j = 0; j < 3; ++j) { o.zlN[j] = cs[38 + j]; o.ZlN[j] = cs[41 + j]; }
     o.nyN = (int)cs[44];
+    o.nhs = (int)cs[45];
     o.max_iter = max_iter;
     o.cost_scaling = cost_scaling;
     const int N1 = N + 1;

@@ -10,7 +10,8 @@ nonlinear constraints idxsh with L1/L2 slack penalties, input box constraints, x
   s.t. dx_0 = x0 - xbar_0,  dx_{k+1} = A_k dx_k + B_k du_k + (xn_k - xbar_{k+1})
        lbu - ubar_k <= du_k <= ubu - ubar_k
        lh - h_k - sl_k <= J_h,k dx_k <= uh - h_k + su_k,  sl_k, su_k >= 0   (the soft rows of the constraint set)
-       lhN - h_N <= J_hN dx_N <= uhN - h_N                                 (hard terminal rows: rec_feas / stability)
+       lh - h_k <= J_h,k dx_k <= uh - h_k              (hard rows: slack weight None, base_model.py:142-168;
+                                                          rec_feas / stability terminal rows)
   w_k = [dx_k; du_k], r_k = y_k - yref_k, s_k = cost scaling (acados default: dt_k for k < N, 1 at N)
 
 HPIPM's algorithm (Riccati-based IPM) is not reproducible here (acados is absent; parity at the
@@ -26,9 +27,9 @@ def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=Non
 
     lin: dict with xn [N,10], AB [N,14,10], y [N,11], Jy [N,14,11], yN [nyN], JyN [10,nyN], h [N+1,3],
     Jh [N+1,10,3] (+ hE [6], JhE [10,6] when a terminal row reads them) -- the sdfnmpc_linearize layouts,
-    column-major blocks.  The constraint set is model's (model.Quad: h_cols, term_rows): stage k < N has
-    the soft rows h[k][h_cols]; the terminal node the rows of term_rows (soft first, then hard), each the
-    sum of an h[N] column and an hE column (gen_model.py:26-149).
+    column-major blocks.  The constraint set is model's (model.Quad: h_cols, nhs, term_rows): stage k < N has
+    the rows h[k][h_cols], the last nhs of them hard; the terminal node the rows of term_rows (soft first,
+    then hard), each the sum of an h[N] column and an hE column (gen_model.py:26-149).
     """
     N = xbar.shape[0] - 1
     s = np.concatenate([dt, [1.0]]) if scaling is None else np.asarray(scaling, float)
@@ -52,10 +53,11 @@ def stage_qp(lin, xbar, ubar, x0, yref, W, yNref, WN, dt, model, lm, scaling=Non
     rN = lin["yN"] - yNref
     q["HN"] = JyN.T @ np.diag(WN) @ JyN * s[N] + lm * np.eye(10)
     q["gN"] = JyN.T @ (WN * rN) * s[N]
-    # stage rows (soft)
+    # stage rows: the first ns soft, the last nhs hard
     hc = list(getattr(model, "h_cols", [0, 1, 2]))
-    q["ns"] = len(hc)
-    q["C"] = np.transpose(lin["Jh"][:N][:, :, hc], (0, 2, 1))  # [N,ns,10]
+    q["nhs"] = int(getattr(model, "nhs", 0))
+    q["ns"] = len(hc) - q["nhs"]
+    q["C"] = np.transpose(lin["Jh"][:N][:, :, hc], (0, 2, 1))  # [N,nh,10]
     q["hl"] = lin["h"][:N][:, hc] - np.asarray(model.lh)      # constant of the lower soft row
     q["hu"] = np.asarray(model.uh) - lin["h"][:N][:, hc]
     q["zl"], q["Zl"] = np.asarray(model.zl, float), np.asarray(model.Zl, float)
@@ -141,6 +143,10 @@ def dense_problem(q):
         a = np.zeros(nz); a[ix(k):ix(k) + nx] = -C; a[L["o_su"] + e_] = 1.0; rows.append(a); d.append(hu)
         a = np.zeros(nz); a[L["o_sl"] + e_] = 1.0; rows.append(a); d.append(0.0)
         a = np.zeros(nz); a[L["o_su"] + e_] = 1.0; rows.append(a); d.append(0.0)
+    for k in range(1, N):  # hard stage rows: none at node 0 (acados 0.3.1: initial-node h rows come only
+        for j in range(ns, ns + q["nhs"]):  # from con_h_expr_0, which the reference's ocp.py never sets)
+            a = np.zeros(nz); a[ix(k):ix(k) + nx] = q["C"][k, j]; rows.append(a); d.append(q["hl"][k, j])
+            a = np.zeros(nz); a[ix(k):ix(k) + nx] = -q["C"][k, j]; rows.append(a); d.append(q["hu"][k, j])
     for j in range(q["nsN"], q["nhN"]):  # hard terminal rows
         a = np.zeros(nz); a[ix(N):ix(N) + nx] = q["CN"][j]; rows.append(a); d.append(q["hlN"][j])
         a = np.zeros(nz); a[ix(N):ix(N) + nx] = -q["CN"][j]; rows.append(a); d.append(q["huN"][j])
@@ -219,7 +225,18 @@ def polish_active_set(q, sol, act_tol=1e-7, max_swaps=200):
     out = _unpack(q, z)
     out["min_dual"] = lam.min() if na else 0.0
     out["max_violation"] = max(0.0, -viol.min())
+    out["lam_l1"] = float(np.abs(lam).sum()) if na else 0.0  # |lambda*|_1: prices a primal residual (objective_bound)
     return out
+
+
+def objective_bound(m, tol, lam_l1, rp):
+    """How far above the optimum F* an IPM point stopped at max_i t_i lambda_i < tol with primal residual rp
+    (max abs) may lie: F(z) - F* <= lambda' (G z + d) + r_d' (z - z*) (convexity, E z = e exactly), and
+    lambda' (G z + d) = lambda' t + lambda' r_p <= m tol + |lambda|_1 rp.  The stationarity residual r_d
+    decays with the step lengths (the stop test's gap term) and is left out; |lambda|_1 is the exact
+    solution's (the IPM's multipliers converge to it).  On hard rows with large multipliers the second
+    term is the larger."""
+    return m * tol + lam_l1 * max(rp, tol)
 
 
 def solve_dense(q, tol=1e-11, max_iter=100):

@@ -71,7 +71,8 @@ class QpOptsC(C.Structure):
                 ("max_iter", C.c_int), ("tol", C.c_double), ("ny", C.c_int), ("lm_scaling", C.c_int),
                 ("warm_start", C.c_int), ("nh", C.c_int), ("h_col", C.c_int * 3), ("nhN", C.c_int), ("nsN", C.c_int),
                 ("hN_col", C.c_int * NHN_MAX), ("hE_col", C.c_int * NHN_MAX), ("lhN", C.c_double * NHN_MAX),
-                ("uhN", C.c_double * NHN_MAX), ("zlN", C.c_double * 3), ("ZlN", C.c_double * 3), ("nyN", C.c_int)]
+                ("uhN", C.c_double * NHN_MAX), ("zlN", C.c_double * 3), ("ZlN", C.c_double * 3), ("nyN", C.c_int),
+                ("nhs", C.c_int)]
 
 
 class RefOptsC(C.Structure):
@@ -416,7 +417,8 @@ def qp_opts(model, lm=10.0, cost_scaling=True, max_iter=100, tol=1e-8, lm_scalin
                    v(model.Zl, 3), float(lm), int(bool(cost_scaling)), int(max_iter), float(tol), int(model.ny),
                    int(bool(lm_scaling)), int(bool(warm_start)), int(model.nh), iv(model.h_cols, 3), int(model.nhN),
                    int(model.nsN), iv([r[0] for r in rows], NHN_MAX), iv([r[1] for r in rows], NHN_MAX),
-                   v(model.lhN, NHN_MAX), v(model.uhN, NHN_MAX), v(model.zlN, 3), v(model.ZlN, 3), int(model.nyN))
+                   v(model.lhN, NHN_MAX), v(model.uhN, NHN_MAX), v(model.zlN, 3), v(model.ZlN, 3), int(model.nyN),
+                   int(getattr(model, "nhs", 0)))
 
 
 def qp_solve(ctx: Context, opts: QpOptsC, B: int, N: int, bufs: dict):

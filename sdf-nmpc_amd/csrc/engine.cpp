@@ -50,11 +50,13 @@ extern "C" const char* sdfnmpc_last_error(void) { return g_err.c_str(); }
 struct DevBuf {
     void* p = nullptr;
     size_t bytes = 0;
+    unsigned long long gen = 0;  // reallocations so far (a captured step graph holds the pointer of its time)
     hipError_t ensure(size_t n) {
         if (n <= bytes) return hipSuccess;
         if (p) (void)hipFree(p);
         p = nullptr;
         bytes = 0;
+        ++gen;
         hipError_t e = hipMalloc(&p, n);
         if (e == hipSuccess) bytes = n;
         return e;
@@ -336,12 +338,23 @@ extern "C" int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel) {
 // the serial kernel at N = 40, 24 % at N = 60, equal at N = 30, 30 % slower at N = 20 where the three
 // couplings outweigh five-node segments), the serial one otherwise (one wavefront per instance: at
 // B = 1024 it fills every SIMD once and is 1.6x faster than four wavefronts per instance)
-// the segmented kernel covers the default row set (h = [hfov, vfov, sdf] at every node); any other
-// constraint set runs on the serial kernel
-static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, QpRows q) {
-    const QpRows d = qp_rows_default();
-    if (q.ns != d.ns || q.nhN != d.nhN || q.nsN != d.nsN) return (ctx && N >= 1 && B >= 0) ? SDFNMPC_QP_SERIAL : -1;
+// the segmented kernel covers the default row set only (h = [hfov, vfov, sdf] soft at every node, the
+// terminal rows the stage rows' copies: qp_is_default_set); any other constraint set runs on the serial kernel
+static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, bool default_set) {
+    if (!default_set) return (ctx && N >= 1 && B >= 0) ? SDFNMPC_QP_SERIAL : -1;
     return sdfnmpc_ctx_qp_kernel(ctx, N, B);
+}
+// exactly the default row set (qp_default_rows): the segmented kernel reads the stage bounds / weights for
+// the terminal rows and h[N][0..2] as their values, so a set whose terminal rows differ in any
+// field -- columns, hE terms, bounds, weights -- is not it.  T: sdfnmpc_qp_opts or QpArgs (same field names)
+template <class T>
+static bool qp_is_default_set(const T& o) {
+    if (o.nh != 3 || o.nhs != 0 || o.nhN != 3 || o.nsN != 3) return false;
+    for (int j = 0; j < 3; ++j)
+        if (o.h_col[j] != j || o.hN_col[j] != j || o.hE_col[j] != -1 || o.lhN[j] != o.lh[j] || o.uhN[j] != o.uh[j] ||
+            o.zlN[j] != o.zl[j] || o.ZlN[j] != o.Zl[j])
+            return false;
+    return true;
 }
 
 extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B) {
@@ -364,7 +377,6 @@ extern "C" long long sdfnmpc_qp_lds_bytes(int N) {
 // rti_qp.hip: one 64-lane workgroup per instance, rti_qp_seg.hip: one workgroup of NSEG waves).
 static int qp_cset_check(const sdfnmpc_qp_opts* o);
 static QpRows qp_rows_of(const sdfnmpc_qp_opts* o);
-static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, QpRows q);
 
 extern "C" long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N) { return sdfnmpc_qp_capacity_for(ctx, N, nullptr); }
 
@@ -374,7 +386,7 @@ extern "C" long long sdfnmpc_qp_capacity_for(const sdfnmpc_ctx* ctx, int N, cons
     if (o && qp_cset_check(o)) return -1;
     const QpRows rows = o ? qp_rows_of(o) : qp_rows_default();
     // a batch that fills the device: the kernel AUTO picks above SDFNMPC_QP_SEG_AUTO_MAX_B
-    const bool seg = qp_kernel_for(ctx, N, 1 << 30, rows) == SDFNMPC_QP_SEGMENTED;
+    const bool seg = qp_kernel_for(ctx, N, 1 << 30, o ? qp_is_default_set(*o) : true) == SDFNMPC_QP_SEGMENTED;
     const size_t per = seg ? qp_seg_lds_bytes(N) : qp_lds_bytes(N, rows);
     if (per == 0 || per > ctx->lds_per_cu) return 0;  // the horizon does not fit one CU's LDS
     // the runtime's occupancy of the kernel (LDS, registers and waves at once): the serial kernel's 375
@@ -1448,8 +1460,9 @@ extern "C" int sdfnmpc_linearize(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const
 static int qp_cset_check(const sdfnmpc_qp_opts* o) {
     if (o->nh < 0 || o->nh > 3) return fail(SDFNMPC_E_ARG, "qp opts: nh must be 0..3");
     for (int j = 0; j < o->nh; ++j)
-        if (o->h_col[j] < 0 || o->h_col[j] > 2 || (j && o->h_col[j] <= o->h_col[j - 1]))
-            return fail(SDFNMPC_E_ARG, "qp opts: h_col must be increasing columns 0..2");
+        if (o->h_col[j] < 0 || o->h_col[j] > 2 || (j && o->h_col[j] == o->h_col[0]) || (j == 2 && o->h_col[2] == o->h_col[1]))
+            return fail(SDFNMPC_E_ARG, "qp opts: h_col must be distinct columns 0..2");
+    if (o->nhs < 0 || o->nhs > o->nh) return fail(SDFNMPC_E_ARG, "qp opts: nhs (hard stage rows) must be 0..nh");
     if (o->nhN < 0 || o->nhN > SDFNMPC_NHN_MAX || o->nsN < 0 || o->nsN > 3 || o->nsN > o->nhN || o->nhN - o->nsN > 6)
         return fail(SDFNMPC_E_ARG, "qp opts: terminal rows nhN <= 8 with nsN <= 3 soft and <= 6 hard");
     for (int j = 0; j < o->nhN; ++j) {
@@ -1461,7 +1474,7 @@ static int qp_cset_check(const sdfnmpc_qp_opts* o) {
     if (o->nyN != 4 && o->nyN != 5) return fail(SDFNMPC_E_ARG, "qp opts: nyN must be 4 or 5");
     return SDFNMPC_OK;
 }
-static QpRows qp_rows_of(const sdfnmpc_qp_opts* o) { return QpRows{o->nh, o->nhN, o->nsN}; }
+static QpRows qp_rows_of(const sdfnmpc_qp_opts* o) { return QpRows{o->nh, o->nhN, o->nsN, o->nhs}; }
 // the network is read by a constraint row (stage h_col or terminal hN_col == 2) or the sdf cost
 static bool qp_needs_sdf(const sdfnmpc_qp_opts* o) {
     bool need = o->ny == 12;
@@ -1504,7 +1517,8 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
     q.lm = o->lm; q.tol = o->tol; q.max_iter = o->max_iter; q.cost_scaling = o->cost_scaling; q.ny = o->ny;
     q.lm_scaling = o->lm_scaling;
     q.warm_start = o->warm_start ? 1 : 0;
-    q.nh = o->nh; q.nhN = o->nhN; q.nsN = o->nsN; q.nyN = o->nyN;
+    q.nh = o->nh; q.nhN = o->nhN; q.nsN = o->nsN; q.nyN = o->nyN; q.nhs = o->nhs;
+    q.default_rows = qp_is_default_set(*o) ? 1 : 0;
     q.sdf_row = -1;
     for (int j = 0; j < 3; ++j) {
         q.h_col[j] = j < o->nh ? o->h_col[j] : 0;
@@ -1519,16 +1533,21 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
     return SDFNMPC_OK;
 }
 
-// what the stage / terminal records depend on besides H, g: the stage rows' columns and the terminal residual width
+// the constraint set a preparation packed its records under (stage rows' columns and kinds, terminal rows'
+// columns, the terminal residual width) and the feedback must match: an FNV-1a hash of those fields
 static long long cset_key(const QpArgs& q) {
-    return q.nh | (long long)q.h_col[0] << 4 | (long long)q.h_col[1] << 8 | (long long)q.h_col[2] << 12 |
-           (long long)q.nyN << 16;
+    unsigned long long h = 1469598103934665603ull;
+    auto mix = [&](long long v) { h = (h ^ (unsigned long long)(v + 7)) * 1099511628211ull; };
+    mix(q.nh); mix(q.nhs); mix(q.nhN); mix(q.nsN); mix(q.nyN);
+    for (int j = 0; j < 3; ++j) mix(q.h_col[j]);
+    for (int j = 0; j < QP_NHN; ++j) { mix(q.hN_col[j]); mix(q.hE_col[j]); }
+    return (long long)(h >> 1);
 }
 
 // the IPM kernel of this context and horizon: the segmented one (four wavefronts per instance,
 // rti_qp_seg.hip) where it supports N, unless the context asks for the serial one (rti_qp.hip)
 static hipError_t qp_launch(sdfnmpc_ctx* ctx, const QpArgs& q) {
-    if (qp_kernel_for(ctx, q.N, q.B, QpRows{q.nh, q.nhN, q.nsN}) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
+    if (qp_kernel_for(ctx, q.N, q.B, q.default_rows != 0) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
     return launch_rti_qp(q, ctx->stream);
 }
 
@@ -1599,7 +1618,15 @@ struct sdfnmpc_step {
     hipGraph_t graph = nullptr;
     hipGraphExec_t exec = nullptr;
     int device = 0;
+    const sdfnmpc_ctx* ctx = nullptr;  // the context whose workspaces the graph's kernels address
+    unsigned long long ws_gen = 0;     // ctx_ws_gen at capture
 };
+// The graph's kernels hold the context's device workspaces as they were at capture.  Every reallocation
+// (a later call with a larger B or N grows them: DevBuf::ensure frees the old buffer) bumps a DevBuf's
+// generation, so the sum over the workspaces changes exactly when one of them moved.
+static unsigned long long ctx_ws_gen(const sdfnmpc_ctx* c) {
+    return c->c13.gen + c->sdf4.gen + c->lat.gen + c->out4.gen + c->glat.gen + c->qpw.gen + c->qpst.gen + c->wws.gen;
+}
 
 static int step_eager(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, const sdfnmpc_quad_model* mdl, const sdfnmpc_lin_args* la,
                       const sdfnmpc_qp_opts* o, const sdfnmpc_qp_args* qa, double* u0, const int* status) {
@@ -1657,13 +1684,18 @@ extern "C" int sdfnmpc_step_create(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, con
     st->graph = g;
     st->exec = x;
     st->device = ctx->device;
+    st->ctx = ctx;
+    st->ws_gen = ctx_ws_gen(ctx);
     *out = st;
     return SDFNMPC_OK;
 }
 
 extern "C" int sdfnmpc_step_launch(sdfnmpc_ctx* ctx, sdfnmpc_step* st) {
     if (!ctx || !st) return fail(SDFNMPC_E_ARG, "NULL argument to sdfnmpc_step_launch");
-    if (st->device != ctx->device) return fail(SDFNMPC_E_ARG, "step_launch: step captured on another device");
+    if (st->device != ctx->device || st->ctx != ctx) return fail(SDFNMPC_E_ARG, "step_launch: step captured on another context");
+    if (ctx_ws_gen(ctx) != st->ws_gen)
+        return fail(SDFNMPC_E_ARG, "step_launch: a context workspace was reallocated since the capture (a call with a larger "
+                                   "B or N); destroy the step and create it again");
     ScopedDevice sd(ctx->device);
     HIPCHK(hipGraphLaunch(st->exec, ctx->stream));
     return SDFNMPC_OK;

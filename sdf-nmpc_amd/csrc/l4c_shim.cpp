@@ -171,6 +171,19 @@ extern "C" {
 
 int sdf_l4c_configure(const char* weights_path, int device) {
     std::lock_guard<std::mutex> lk(g_mu);
+    // CasADi keeps the sparsity patterns it was handed and sizes its argument / result buffers from them:
+    // once a pattern of width hw is out, a network of another width would read past the caller's input and
+    // write past its Jacobian buffer.  Refused before anything is freed; the loaded network stays.
+    const int hw = g_handed.load();
+    if (hw) {
+        const int w = header_width(::weights_path(weights_path));
+        if (w != hw) {
+            g_err = "sdf_l4c_configure: a sparsity pattern of width " + std::to_string(hw) +
+                    " was handed out; the network takes " + (w ? std::to_string(w) : std::string("(unreadable)")) +
+                    " inputs (one width per process)";
+            return 1;
+        }
+    }
     g_gen++;  // every thread's cached value / gradient belongs to the previous network
     if (g_net) {
         sdfnmpc_net_free(g_net);
@@ -181,7 +194,6 @@ int sdf_l4c_configure(const char* weights_path, int device) {
         g_ctx = nullptr;
     }
     g_D.store(0);
-    g_handed.store(0);  // an explicit reconfiguration: the caller sizes its buffers anew
     g_cfg_path = weights_path ? weights_path : "";
     return init_locked(weights_path, device) ? 1 : 0;
 }

@@ -37,11 +37,13 @@ struct QpArgs {
                     // rti_qp_kernel then copies from J_h itself (sdf_row_patch)
     int sdf_row_patch;  // rti_qp_kernel: copy J_h[.][2] into the records' C^T row 2 before the sweeps
     int warm_start;     // 1: the IPM starts from the du found in du on entry (qp_solver_warm_start, ocp.py:116)
+    int nhs;            // hard stage rows: the last nhs of the nh (slack weight None, base_model.py:142-155)
+    int default_rows;   // 1: exactly qp_default_rows' set (the segmented kernel's only one)
 };
 
 // the default constraint set (h = [hfov, vfov, sdf] at every node, soft) from lh .. Zl (diagnostic drivers)
 inline void qp_default_rows(QpArgs& q) {
-    q.nh = 3; q.nhN = 3; q.nsN = 3; q.nyN = 4; q.sdf_row = 2;
+    q.nh = 3; q.nhN = 3; q.nsN = 3; q.nyN = 4; q.sdf_row = 2; q.nhs = 0; q.default_rows = 1;
     for (int j = 0; j < 3; ++j) {
         q.h_col[j] = j; q.zlN[j] = q.zl[j]; q.ZlN[j] = q.Zl[j];
     }
@@ -70,12 +72,20 @@ __host__ __device__ inline size_t qp_work_doubles(int N) {
     return (size_t)(N + 1) * (QP_REC + QP_FRECS) + 3 * (size_t)QP_CPL + QP_NSEG * (size_t)QP_PARK;
 }
 // The row set of one instance: 8 box rows per stage k < N; 4 rows (h lower, h upper, sl >= 0, su >= 0) per
-// soft group -- ns per stage, nsN at the terminal node; 2 rows (lower, upper) per hard terminal row.
-// Groups (one fold / C dx / h entry each): the N ns stage groups (k ns + j), then the nhN terminal rows.
+// soft group -- ns - nhs per stage, nsN at the terminal node; 2 rows (lower, upper) per hard row -- nhs per
+// stage 0 < k < N, nhN - nsN at the terminal node.  Node 0 has no hard row: acados (0.3.1, the reference's,
+// README.md:50) imposes nonlinear rows at the initial node only through con_h_expr_0, which ocp.py never
+// sets, and with x_0 fixed a violated one would make the QP infeasible; its soft rows, kept, only add a
+// slack term decoupled from (dx, du).  Row order: boxes, soft groups (stage, then terminal), hard rows
+// (stage, then terminal).  Groups (one fold / C dx / h entry each): the N ns stage groups (k ns + j; a
+// stage's soft rows first), then the nhN terminal rows (soft first).
 struct QpRows {
-    int ns, nhN, nsN;  // stage soft rows; terminal rows, soft among them
+    int ns, nhN, nsN;  // stage rows; terminal rows, soft among them
+    int nhs = 0;       // hard stage rows (the last nhs of the ns)
     __host__ __device__ int groups(int N) const { return N * ns + nhN; }
-    __host__ __device__ int rows(int N) const { return 8 * N + 4 * (N * ns + nsN) + 2 * (nhN - nsN); }
+    __host__ __device__ int soft(int N) const { return N * (ns - nhs) + nsN; }
+    __host__ __device__ int hard(int N) const { return (N - 1) * nhs + nhN - nsN; }
+    __host__ __device__ int rows(int N) const { return 8 * N + 4 * soft(N) + 2 * hard(N); }
 };
 __host__ __device__ inline QpRows qp_rows_default() { return QpRows{3, 3, 3}; }  // h = [hfov, vfov, sdf] everywhere
 // LDS per instance (one wavefront); the order and sizes mirror carve() in rti_qp.hip (every block

@@ -327,20 +327,42 @@ __global__ __launch_bounds__(64 * PACK_NODES) void rti_qp_pack_kernel(QpArgs A) 
 #ifndef QP_LB_WAVES  // diagnostic: minimum waves per SIMD the register allocation must allow
 #define QP_LB_WAVES 1
 #endif
-template <int NSS, bool HARD>  // stage soft rows (0..3); hard terminal rows present (rec_feas / stability)
+// small unsigned division x / d for d in 1..3 (x < 2^17): the row phases' group maps of a HARD kernel
+__device__ __forceinline__ int div123(int x, int d) {
+    return d == 1 ? x : d == 2 ? x >> 1 : (int)(((unsigned)x * 0xAAABu) >> 17);
+}
+template <int NSS, bool HARD>  // stage rows (0..3); hard rows present (stage rows with slack None, rec_feas, stability)
 __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     extern __shared__ __align__(16) double lds_q[];
     STAMP_DECL
     constexpr int NS = NSS;  // this kernel's stage rows (shadows qpd::NS, the width of the h / J_h arrays)
     const int b = blockIdx.x, lane = threadIdx.x;
     const int N = A.N, N1 = N + 1;
-    const QpRows rw{NSS, A.nhN, A.nsN};
+    const int nhs = HARD ? A.nhs : 0;  // hard stage rows: the last nhs of a stage's NSS
+    const int nss = NSS - nhs;         // soft stage rows
+    const QpRows rw{NSS, A.nhN, A.nsN, nhs};
     const int m = rw.rows(N);
-    const int NGS = N * NSS;          // stage groups
-    const int NG1 = NGS + A.nsN;      // soft groups (stage, then terminal)
-    const int NHH = HARD ? A.nhN - A.nsN : 0;  // hard terminal rows: rows RH0 + 2 i (lower), + 1 (upper); group NG1 + i
-    const int RH0 = 8 * N + 4 * NG1;
+    const int NGS = N * NSS;          // stage groups (group e = k NSS + j; soft rows j < nss first)
+    const int NSG = N * nss;          // soft stage groups
+    const int NG1 = rw.soft(N);       // soft groups: soft index si = stage (k nss + j), then terminal (NSG + j)
+    const int NHG = (N - 1) * nhs;    // hard stage rows (nodes 0 < k < N: qp_kernels.h QpRows)
+    const int NHT = HARD ? rw.hard(N) : 0;  // hard rows: hard index i = stage ((k - 1) nhs + j - nss), then terminal
+    const int RH0 = 8 * N + 4 * NG1;  // hard row i: rows RH0 + 2 i (lower), + 1 (upper)
     const int nhN = A.nhN;
+    // group of soft index si / of hard index i
+    auto soft_e = [&](int si) -> int {
+        if constexpr (!HARD) return si;
+        else {
+            if (si >= NSG) return NGS + si - NSG;
+            const int k = div123(si, nss);
+            return k * NSS + si - k * nss;
+        }
+    };
+    auto hard_e = [&](int i) -> int {
+        if (i >= NHG) return NGS + A.nsN + i - NHG;
+        const int k = div123(i, nhs);
+        return (k + 1) * NSS + nss + i - k * nhs;
+    };
     const Smem s = carve<NSS>((ldsd*)lds_q, N, rw);
     // node and row of soft group e (stage groups first, then the terminal's)
     auto gnode = [&](int e) -> int {
@@ -431,6 +453,10 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     }
     if (lane < NX) s.dx[lane] = A.x0[(size_t)b * 10 + lane] - A.x[(size_t)b * N1 * 10 + lane];
     if (lane < 48) s.zero[lane] = 0.0;
+    if (HARD && lane >= nss && lane < NSS) {  // node 0's hard groups: no row, a zero fold (QpRows)
+        s.fw[lane] = 0.0;
+        s.fg[lane] = 0.0;
+    }
     __syncthreads();
     STAMP(0);
 
@@ -795,7 +821,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             const int k = r >> 3, q = r & 7, i = q & 3, up = q >> 2;
             v = box_d(k, i, up) + (up ? -s.du[k * NU + i] : s.du[k * NU + i]);
         } else {
-            const int e = (r - 8 * N) >> 2, kind = (r - 8 * N) & 3, k = gnode(e);
+            const int e = soft_e((r - 8 * N) >> 2), kind = (r - 8 * N) & 3, k = gnode(e);
             const ldsd* gc = gcst(e);
             const double h = s.hv[e];
             v = kind == 0 ? s.cxa[e] + (h - gc[0]) : kind == 1 ? -s.cxa[e] + (gc[1] - h) : 0.0;
@@ -806,8 +832,8 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         s.lam[r] = l0;
         rp = fmax(rp, fabs(v - t));
     }
-    if constexpr (HARD) for (int r = RH0 + lane; r < m; r += 64) {  // hard terminal rows: lower, upper
-        const int i = (r - RH0) >> 1, up = (r - RH0) & 1, e = NG1 + i;
+    if constexpr (HARD) for (int r = RH0 + lane; r < m; r += 64) {  // hard rows: lower, upper
+        const int i = (r - RH0) >> 1, up = (r - RH0) & 1, e = hard_e(i);
         const ldsd* gc = gcst(e);
         const double v = up ? -s.cxa[e] + (gc[1] - s.hv[e]) : s.cxa[e] + (s.hv[e] - gc[0]);
         const double t = fmax(v, T0);
@@ -824,9 +850,8 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     struct Grp {
         double s1, s2, s3, s4, v1, v2, v3, v4, Hl, Hu, iHl, iHu, gl, gu;
     };
-    auto group = [&](int e, int phase, double sigmu) -> Grp {
+    auto group = [&](int e, int r0, int phase, double sigmu) -> Grp {  // group e, rows r0 .. r0 + 3
         Grp g;
-        const int r0 = 8 * N + 4 * e;
         const double sk = s.skv[gnode(e)];
         const ldsd* gc = gcst(e);
         const double t1 = s.t[r0], t2 = s.t[r0 + 1], t3 = s.t[r0 + 2], t4 = s.t[r0 + 3];
@@ -869,9 +894,9 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         }
         return v;
     };
-    // hard terminal row i, side up: the constant d of t = +-C dx + d, and the value at C dx = cxs
+    // hard row i, side up: the constant d of t = +-C dx + d, and the value at C dx = cxs
     auto hard_d = [&](int i, int up) -> double {
-        const int e = NG1 + i;
+        const int e = hard_e(i);
         const ldsd* gc = gcst(e);
         return up ? gc[1] - s.hv[e] : s.hv[e] - gc[0];
     };
@@ -880,7 +905,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         const double t = s.t[r], l = s.lam[r], it = rcp_nr(t), sg = l * it, d = hard_d(i, up);
         double v = sg * (t - d);
         if (phase) {
-            const double cxa = s.cxa[NG1 + i];
+            const double cxa = s.cxa[hard_e(i)];
             const double da = (up ? -cxa : cxa) + d - t;
             v -= (da * (-sg * da - l) - sigmu) * it;
         }
@@ -888,8 +913,9 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     };
     // all groups at once, before a backward sweep: fw = w (factor only), fg = gamma, box diag / v
     auto terms = [&](int phase, double sigmu) {
-        for (int e = lane; e < NG1; e += 64) {
-            const Grp g = group(e, phase, sigmu);
+        for (int si = lane; si < NG1; si += 64) {
+            const int e = soft_e(si);
+            const Grp g = group(e, 8 * N + 4 * si, phase, sigmu);
             // fold of the eliminated slack pair, written without the cancellation of H - s1 (H = Zs + s1 + s2
             // with s1 -> inf on an active row):  w = s1 (Zs + s2) / Hl + ...,  gamma = -(v1 + s1 gl / Hl) + ...
             const ldsd* gc = gcst(e);
@@ -898,11 +924,12 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             if (!phase) s.fw[e] = g.s1 * (Zs + g.s2) * g.iHl + g.s3 * (Zs + g.s4) * g.iHu;
             s.fg[e] = -(g.v1 * (Zs + g.s2) + g.s1 * (zs - g.v2)) * g.iHl + (g.v3 * (Zs + g.s4) + g.s3 * (zs - g.v4)) * g.iHu;
         }
-        if (HARD && lane < NHH) {  // hard rows fold like box rows: w = sigma_l + sigma_u, gamma = -v_l + v_u
-            const int r = RH0 + 2 * lane;
-            if (!phase) s.fw[NG1 + lane] = s.lam[r] * rcp_nr(s.t[r]) + s.lam[r + 1] * rcp_nr(s.t[r + 1]);
-            s.fg[NG1 + lane] = -hard_v(lane, 0, phase, sigmu) + hard_v(lane, 1, phase, sigmu);
-        }
+        if constexpr (HARD)  // hard rows fold like box rows: w = sigma_l + sigma_u, gamma = -v_l + v_u
+            for (int i = lane; i < NHT; i += 64) {
+                const int r = RH0 + 2 * i, e = hard_e(i);
+                if (!phase) s.fw[e] = s.lam[r] * rcp_nr(s.t[r]) + s.lam[r + 1] * rcp_nr(s.t[r + 1]);
+                s.fg[e] = -hard_v(i, 0, phase, sigmu) + hard_v(i, 1, phase, sigmu);
+            }
         for (int e = lane; e < N * NU; e += 64) {
             const int k = e >> 2, i = e & 3;
             if (!phase) s.bd[e] = s.lam[8 * k + i] * rcp_nr(s.t[8 * k + i]) + s.lam[8 * k + 4 + i] * rcp_nr(s.t[8 * k + 4 + i]);
@@ -948,7 +975,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         // hard rows (lane 2 i + up)
         auto hard_dir = [&](int r, double& dt, double& dl) {
             const int i = (r - RH0) >> 1, up = (r - RH0) & 1;
-            const double t = s.t[r], l = s.lam[r], cxa = s.cxa[NG1 + i];
+            const double t = s.t[r], l = s.lam[r], cxa = s.cxa[hard_e(i)];
             dt = (up ? -cxa : cxa) + hard_d(i, up) - t;
             dl = -(l * rcp_nr(t)) * dt - l;
         };
@@ -958,10 +985,10 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
                 hard_dir(r, dt, dl);
                 bound(s.t[r], s.lam[r], dt, dl);
             }
-        // affine direction of the four rows of soft group e: dt = val(z_a) - t, dl = -(lambda / t) dt - lambda
-        auto soft_dir = [&](int e, double* dt, double* dl) {
-            const int r0 = 8 * N + 4 * e;
-            const Grp g = group(e, 0, 0.0);
+        // affine direction of the four rows of soft group si: dt = val(z_a) - t, dl = -(lambda / t) dt - lambda
+        auto soft_dir = [&](int si, double* dt, double* dl) {
+            const int r0 = 8 * N + 4 * si, e = soft_e(si);
+            const Grp g = group(e, r0, 0, 0.0);
             double v[4];
             soft_vals(g, e, s.cxa[e], v);
 #pragma unroll
@@ -1003,10 +1030,10 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
                 hard_dir(r, dt, dl);
                 lmua += (s.t[r] + aa * dt) * (s.lam[r] + aa * dl);
             }
-        auto soft_mu = [&](int e, const double* dt, const double* dl) {
+        auto soft_mu = [&](int si, const double* dt, const double* dl) {
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
-                const double t = s.t[8 * N + 4 * e + q], l = s.lam[8 * N + 4 * e + q];
+                const double t = s.t[8 * N + 4 * si + q], l = s.lam[8 * N + 4 * si + q];
                 lmua += (t + aa * dt[q]) * (l + aa * dl[q]);
             }
         };
@@ -1060,7 +1087,8 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         auto hard_dir = [&](int r, double& dt, double& dl) {
             const int i = (r - RH0) >> 1, up = (r - RH0) & 1;
             const double t = s.t[r], l = s.lam[r], d = hard_d(i, up);
-            const double cc = s.cxc[NG1 + i], ca = s.cxa[NG1 + i];
+            const int e = hard_e(i);
+            const double cc = s.cxc[e], ca = s.cxa[e];
             dt = (up ? -cc : cc) + d - t;
             const double dta = (up ? -ca : ca) + d - t;
             const double it = rcp_nr(t), sg = l * it;
@@ -1072,9 +1100,9 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
                 hard_dir(r, dt, dl);
                 bound(s.t[r], s.lam[r], dt, dl);
             }
-        auto soft_dir = [&](int e, double* dt, double* dl) {
-            const int r0 = 8 * N + 4 * e;
-            const Grp ga = group(e, 0, 0.0), gc = group(e, 1, sigmu);
+        auto soft_dir = [&](int si, double* dt, double* dl) {
+            const int r0 = 8 * N + 4 * si, e = soft_e(si);
+            const Grp ga = group(e, r0, 0, 0.0), gc = group(e, r0, 1, sigmu);
             double va[4], vc[4];
             soft_vals(ga, e, s.cxa[e], va);
             soft_vals(gc, e, s.cxc[e], vc);
@@ -1125,9 +1153,6 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
             s.lam[r] = ln;
         }
         {
-            double hdt = 0.0, hdl = 0.0;  // hard rows: one per lane (2 NHH <= 12 < 64)
-            const int r = RH0 + lane;
-            if (HARD && r < m) hard_dir(r, hdt, hdl);
             auto soft_upd = [&](int e, const double* dt, const double* dl) {
                 const int r0 = 8 * N + 4 * e;
                 double tn[4], ln[4];
@@ -1157,13 +1182,16 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
                     soft_upd(e, dt, dl);
                 }
             }
-            if (HARD && r < m) {
-                const double tn = s.t[r] + al * hdt, ln = s.lam[r] + al * hdl;
-                lmu += tn * ln;
-                lcm = fmax(lcm, tn * ln);
-                s.t[r] = tn;
-                s.lam[r] = ln;
-            }
+            if constexpr (HARD)
+                for (int r = RH0 + lane; r < m; r += 64) {
+                    double hdt, hdl;
+                    hard_dir(r, hdt, hdl);
+                    const double tn = s.t[r] + al * hdt, ln = s.lam[r] + al * hdl;
+                    lmu += tn * ln;
+                    lcm = fmax(lcm, tn * ln);
+                    s.t[r] = tn;
+                    s.lam[r] = ln;
+                }
         }
         for (int e = lane; e < N1 * NX; e += 64) s.dx[e] += al * (s.dxc[e] - s.dx[e]);
         for (int e = lane; e < N * NU; e += 64) s.du[e] += al * (s.duc[e] - s.du[e]);
@@ -1285,7 +1313,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     if (A.slack)  // slacks = the t of rows sl >= 0, su >= 0 (equal to the iterate's sl, su up to r_p); [N+1][3][2]
         for (int e = lane; e < N1 * 3; e += 64) {
             const int k = e / 3, j = e - 3 * k;
-            const int g = k < N ? (j < NS ? k * NS + j : -1) : (j < A.nsN ? NGS + j : -1);
+            const int g = k < N ? (j < nss ? k * nss + j : -1) : (j < A.nsN ? NSG + j : -1);  // soft index
             A.slack[((size_t)b * N1 * 3 + e) * 2] = g >= 0 ? s.t[8 * N + 4 * g + 2] : 0.0;
             A.slack[((size_t)b * N1 * 3 + e) * 2 + 1] = g >= 0 ? s.t[8 * N + 4 * g + 3] : 0.0;
         }
@@ -1343,7 +1371,9 @@ static const void* rti_qp_fn_h(int nh) {
     }
 }
 // the kernel instantiation of a row set
-static const void* rti_qp_fn(QpRows q) { return q.nhN > q.nsN ? rti_qp_fn_h<true>(q.ns) : rti_qp_fn_h<false>(q.ns); }
+static const void* rti_qp_fn(QpRows q) {
+    return (q.nhN > q.nsN || q.nhs > 0) ? rti_qp_fn_h<true>(q.ns) : rti_qp_fn_h<false>(q.ns);
+}
 
 int rti_qp_blocks_per_cu(int N, QpRows q) {
     // every limit at once (LDS per instance, the register allocation: one wave per SIMD, waves per CU), as the
@@ -1359,9 +1389,9 @@ int rti_qp_blocks_per_cu(int N, QpRows q) {
 hipError_t launch_rti_qp(const QpArgs& a, hipStream_t s) {
     if (a.B <= 0) return hipSuccess;
     if (a.nh < 0 || a.nh > 3 || a.nhN < 0 || a.nhN > QP_NHN || a.nsN < 0 || a.nsN > 3 || a.nsN > a.nhN ||
-        a.nhN - a.nsN > 6)
+        a.nhN - a.nsN > 6 || a.nhs < 0 || a.nhs > a.nh)
         return hipErrorInvalidValue;
-    const QpRows q{a.nh, a.nhN, a.nsN};
+    const QpRows q{a.nh, a.nhN, a.nsN, a.nhs};
     const size_t lds = qp_lds_bytes(a.N, q);
     const void* fn = rti_qp_fn(q);
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -109,8 +109,10 @@ class Quad:
     (gen_model.py:26-149, cost_const_helpers.py:48-102, quad_rollpitchyawrate.py:48-55).
 
     Node functions (fixed columns of the preparation phase's h / J_h): 0 hfov, 1 vfov, 2 sdf.
-    Stage rows (soft, in the order the reference adds them): hfov if sensor.hfov < 3.14, vfov if
-    flags.vfov_constraint, sdf if flags.sdf_constraint -- all only with flags.enable_sdf.
+    Stage rows (in the order the reference adds them): hfov if sensor.hfov < 3.14, vfov if
+    flags.vfov_constraint, sdf if flags.sdf_constraint -- all only with flags.enable_sdf; soft with the
+    slack weights mpc.weights.slack_fov / slack_df, hard where that weight is None (base_model.py:142-155),
+    and then ordered soft first (h_cols; nhs = the hard ones at the end).
     Terminal rows: the same fov rows, the sdf row unless recursive_feasibility; with
     recursive_feasibility the braking row sdf - flag poly(v) in [size.xy, max_df] (soft with
     slack_brake, else hard) and the hard fov rows at Co_p_E; with stability the hard terminal velocity
@@ -149,21 +151,21 @@ class Quad:
         sf, sd = _slack(cfg.mpc.weights.slack_fov), _slack(cfg.mpc.weights.slack_df)
         fun_l = [-hfov_lim, -vfov_lim, cfg.robot.size.xy + cfg.mpc.bound_margin]
         fun_u = [hfov_lim, vfov_lim, self.max_df + 0.2]
-        fun_w = [sf, sf, sd]
-        for c in range(3):
-            if fun_w[c] is None:
-                raise UnsupportedConfig("hard fov / sdf stage rows (slack None) are not built: the reference's "
-                                        "defaults soften them (default.yaml:49-50)")
-        # stage rows
-        self.h_cols = [c for c, on in ((0, H), (1, V), (2, S)) if on]
+        fun_w = [sf, sf, sd]  # None: a hard row (add_const_stage / add_const_term soften only `if slack_weights`)
+        # stage rows: the soft ones first, then the hard ones (slack weight None), each kind in the reference's
+        # order -- the QP's row order does not change its solution, and the kernels fold the hard rows like
+        # box rows after the soft groups (rti_qp.hip)
+        on = [c for c, f in ((0, H), (1, V), (2, S)) if f]
+        self.h_cols = [c for c in on if fun_w[c] is not None] + [c for c in on if fun_w[c] is None]
         self.nh = len(self.h_cols)
+        self.nhs = sum(1 for c in on if fun_w[c] is None)  # hard stage rows (the last nhs of h_cols)
         self.lh = np.array([fun_l[c] for c in self.h_cols], dtype=float)
         self.uh = np.array([fun_u[c] for c in self.h_cols], dtype=float)
-        self.zl = np.array([fun_w[c][0] for c in self.h_cols], dtype=float)
-        self.Zl = np.array([fun_w[c][1] for c in self.h_cols], dtype=float)
+        self.zl = np.array([(fun_w[c] or (0.0, 0.0))[0] for c in self.h_cols], dtype=float)
+        self.Zl = np.array([(fun_w[c] or (0.0, 0.0))[1] for c in self.h_cols], dtype=float)
         # terminal rows (hN_col, hE_col, soft, lh, uh, zl, Zl), soft ones first (as the reference adds them)
-        rows = [(c, -1, True, fun_l[c], fun_u[c], fun_w[c][0], fun_w[c][1])
-                for c in self.h_cols if not (c == 2 and RF)]
+        rows = [(c, -1, fun_w[c] is not None, fun_l[c], fun_u[c], *(fun_w[c] or (0.0, 0.0)))
+                for c in on if not (c == 2 and RF)]
         if RF:
             sb = _slack(cfg.mpc.weights.get("slack_brake"))
             rows.append((2, 0, sb is not None, float(cfg.robot.size.xy), self.max_df, *(sb or (0.0, 0.0))))

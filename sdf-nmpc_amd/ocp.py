@@ -127,7 +127,7 @@ class _Part:
 class Ocp:
     def __init__(self, model: Quad, build=False, batch: int = 1, device: int = 0, net=None, ctx=None,
                  weights=None, lm=None, qp_tol=1e-8, qp_iter_max=100, devices=None, lm_scaling=True,
-                 qp_warm_start=False):
+                 qp_warm_start=True):
         self.model = model
         cfg = model.cfg
         self.T = cfg.mpc.T
@@ -141,9 +141,10 @@ class Ocp:
             build_solver(weights=weights)
         self.cmodel = _lib.quad_model(cfg, model)
         # QP data of the model + solver options (ocp.py:113-120: LM regularisation, <= 100 iterations)
-        # qp_warm_start: HPIPM's primal warm start (ocp.py:116 sets qp_solver_warm_start = 1): each QP starts
-        # from the previous one's du.  Off by default: on the C3 problem in closed loop it leaves the mean
-        # iteration count unchanged and the tail slightly longer (tools/ws_probe.py)
+        # qp_warm_start: HPIPM's primal warm start, on by default as the reference configures its solver
+        # (ocp.py:116 sets qp_solver_warm_start = 1): each QP starts from the previous one's du (the solver
+        # object keeps it; zero after init).  The solution is unique (lm > 0), so the start changes iteration
+        # counts, not the step beyond the QP tolerance (tools/ws_probe.py)
         self.qp_opts = _lib.qp_opts(model, lm=float(cfg.mpc.lm_reg if lm is None else lm), max_iter=qp_iter_max,
                                     tol=qp_tol, lm_scaling=lm_scaling, warm_start=qp_warm_start)
         devs = list(devices) if devices else [device]

@@ -51,10 +51,37 @@ def plant(O, onet, cfg, x, u, dt):
     return lin["xn"][:, 0]
 
 
-def oracle_loop(O, onet, n, cfg, x0, K, warm=False):
+def hard_rows_active(model, lin, r, tol=1e-6):
+    """Per instance: how many hard constraint rows (stage rows with slack None at nodes 0 < k < N, hard
+    terminal rows) and rec_feas braking rows (hard, or soft with slack_brake) bind at the QP solution r
+    (the linearised row within tol of a bound, or beyond it on its slack), from the linearisation lin."""
+    N = r["du"].shape[1]
+    cnt = np.zeros(r["du"].shape[0], int)
+    for j in range(model.nh - model.nhs, model.nh):
+        c = model.h_cols[j]
+        v = lin["h"][:, 1:N, c] + np.einsum("bki,bki->bk", lin["Jh"][:, 1:N, :, c], r["dx"][:, 1:N])
+        cnt += ((v - model.lh[j] < tol) | (model.uh[j] - v < tol)).sum(axis=1)
+    for j, (c1, c2, soft, lo, hi, _, _) in enumerate(model.term_rows):
+        if soft and c2 != 0:
+            continue
+        v = np.zeros(len(cnt))
+        g = np.zeros((len(cnt), 10))
+        if c1 >= 0:
+            v += lin["h"][:, N, c1]
+            g += lin["Jh"][:, N, :, c1]
+        if c2 >= 0:
+            v += lin["hE"][:, c2]
+            g += lin["JhE"][:, :, c2]
+        v = v + np.einsum("bi,bi->b", g, r["dx"][:, N])
+        cnt += (v - lo < tol) | (hi - v < tol)
+    return cnt
+
+
+def oracle_loop(O, onet, n, cfg, x0, K, warm=False, strict=True):
     """The oracle pipeline run as the controller runs it, with per-step diagnostics of the SDF rows:
     h2min = min over nodes of the flagged SDF value at the linearisation point, sdf_slack = max over nodes of
-    the QP's SDF lower slack (> 0: the soft row is active), and the plant state before the step."""
+    the QP's SDF lower slack (> 0: the soft row is active), hard_active = binding hard rows
+    (hard_rows_active), and the plant state before the step.  strict: every QP must converge."""
     Bn, N, dt, shift = x0.shape[0], n.N, n.ocp.dt, int(cfg.mpc.shift)
     xs = np.repeat(x0[:, None], N + 1, axis=1)
     us = np.broadcast_to(n.model.u_hover, (Bn, N, 4)).copy()
@@ -65,13 +92,14 @@ def oracle_loop(O, onet, n, cfg, x0, K, warm=False):
             xs[:, : N - shift] = xs[:, shift:N].copy()
             us[:, : N - shift] = us[:, shift:N].copy()
         xs[:, 0] = xo
-        lin = O.linearize_batch(O.quad_model(cfg), onet, xs, us, n.p, dt)
+        lin = O.linearize_batch(O.quad_model(cfg), onet, xs, us, n.p, dt, model=n.model)
         r = O.qp_ipm_batch(lin, dict(prob, x=xs, u=us), xo, n.model, nthreads=4,
                            du_ws=(np.zeros((Bn, N, 4)) if du is None else du) if warm else None)
-        assert (r["status"] == 0).all()
+        assert not strict or (r["status"] == 0).all()
         du = r["du"].copy()
         hist.append({"x0": xo.copy(), "h2min": lin["h"][..., 2].min(axis=1), "sdf_slack": r["slack"][:, :, 2, 0].max(axis=1),
-                     "iters": r["iters"].copy()})
+                     "iters": r["iters"].copy(), "status": r["status"].copy(),
+                     "hard_active": hard_rows_active(n.model, lin, r)})
         xs, us = xs + r["dx"], us + r["du"]
         hist[-1]["u0"] = us[:, 0].copy()
         xo = plant(O, onet, cfg, xo, us[:, 0], dt[0])

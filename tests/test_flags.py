@@ -63,6 +63,10 @@ def test_constraint_set_of_each_flag_set(name):
     assert q.h_cols == cols and q.nh == len(cols)
     assert [r[:3] for r in q.term_rows] == rows and q.nhN == len(rows)
     assert q.nsN == sum(1 for r in rows if r[2]) and all(r[2] for r in q.term_rows[:q.nsN])
+    # hard stage rows: the columns whose slack weight is None (fov: 0, 1; sdf: 2), after the soft ones
+    hard = {0: cfg.mpc.weights.slack_fov is None, 1: cfg.mpc.weights.slack_fov is None, 2: cfg.mpc.weights.slack_df is None}
+    assert q.nhs == sum(hard[c] for c in cols) and all(hard[c] for c in cols[q.nh - q.nhs:])
+    assert all((q.zl[j], q.Zl[j]) == (0.0, 0.0) for j in range(q.nh - q.nhs, q.nh))
     # bounds: fov rows +-fov_ratio fov, the sdf row [size.xy + bound_margin, max_df + 0.2] (gen_model.py:35),
     # the braking row [size.xy, max_df] (gen_model.py:118), the velocity bounds +-limits (add_vel_const)
     lims = {0: cfg.sensor.hfov * cfg.mpc.fov_ratio, 1: cfg.sensor.vfov * cfg.mpc.fov_ratio}
@@ -146,12 +150,22 @@ def test_terminal_extras_oracle(oracle_lib):
             np.testing.assert_allclose(JyN5[:, j], (yp - ym) / 2e-6, rtol=1e-5, atol=1e-6)
 
 
+def _net(oracle_lib, q):
+    if F.uses_scene(q):
+        import scene_setup as S
+        with open(S.SCENE, "rb") as f:
+            return oracle_lib.Net(*W.unpack(f.read()))
+    return oracle_lib.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
+
+
 def _problem(oracle_lib, name, B, N, seed, noise=0.05):
     cfg = F.config(name, mpc__N=N)
     q = F.quad(name, cfg)
-    prob = synth.make_problem(cfg, B, N, seed=seed, sdf_cost=q.sdf_cost, nyN=q.nyN)
+    # the flight along the camera's view (hard fov rows: random v0 can leave the cone before any input acts,
+    # which makes a hard row infeasible -- for the reference's HPIPM too); sets with hard rows on the scene net
+    prob = F.problem(cfg, q, B, N, seed)
     x0 = prob["x"][:, 0] + np.random.default_rng(seed).normal(0, noise, (B, 10))
-    net = oracle_lib.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
+    net = _net(oracle_lib, q)
     lin = oracle_lib.linearize_batch(oracle_lib.quad_model(cfg), net, prob["x"], prob["u"], prob["p"], prob["dt"], model=q)
     return cfg, q, prob, x0, lin
 
@@ -167,7 +181,7 @@ def test_riccati_ipm_matches_exact_solution_per_flag_set(oracle_lib, name):
     cfg, q, prob, x0, lin = _problem(oracle_lib, name, 3, 20, seed=3)
     r = oracle_lib.qp_ipm_batch(lin, prob, x0, q, tol=QP_TOL)
     assert (r["status"] == 0).all(), r["iters"]
-    close = 0
+    close = hard_active = 0
     for b in range(3):
         qq = qp_oracle.stage_qp({k: v[b] for k, v in lin.items() if k != "sdf"}, prob["x"][b], prob["u"][b], x0[b],
                                 prob["yref"][b], prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], q, 10.0)
@@ -179,16 +193,21 @@ def test_riccati_ipm_matches_exact_solution_per_flag_set(oracle_lib, name):
         Fz, Fs = 0.5 * z @ H @ z + g @ z, 0.5 * zs @ H @ zs + g @ zs
         assert (G @ z + d).min() > -1e-7 and np.abs(E @ z - e).max() < 1e-8  # feasible
         m = G.shape[0]
-        assert Fz - Fs <= m * QP_TOL, (b, Fz - Fs)
+        assert Fz - Fs <= qp_oracle.objective_bound(m, QP_TOL, ex["lam_l1"], r["res"][b, 1]), (b, Fz - Fs)
         n_xu = 10 * (cfg.mpc.N + 1) + 4 * cfg.mpc.N
         mu = np.linalg.eigvalsh(H[:n_xu, :n_xu]).min()
         ball = np.sqrt(2 * max(Fz - Fs, 0.0) / mu) + 1e-6  # + the exact solution's own rounding level
         assert np.linalg.norm(z[:n_xu] - zs[:n_xu]) <= ball
         close += np.abs(sol["du"] - ex["du"]).max() <= SOL_ATOL
+        if q.nhs:  # hard stage rows: some bind at the exact solution, none is violated by the C IPM's point
+            nb = 8 * cfg.mpc.N + 4 * (cfg.mpc.N * (q.nh - q.nhs) + q.nsN)
+            hard_active += int(((G @ zs + d)[nb:] < 1e-7).sum())
     assert close >= (1 if q.nhN > q.nsN else 2)
+    if q.nhs:
+        assert hard_active > 0
 
 
-@pytest.mark.parametrize("name", ["no_vfov", "lidar_sdf_only", "rec_feas", "rec_feas_soft_brake"])
+@pytest.mark.parametrize("name", ["no_vfov", "lidar_sdf_only", "rec_feas", "rec_feas_soft_brake", "hard_fov", "hard_df_rec_feas"])
 def test_segments_match_serial_riccati(oracle_lib, name):
     """The C restatement's partitioned Riccati (P = 4) on the terminal rows of a flag set: the same iterates
     as the serial recursion (the terminal node is in the last, serial segment)."""

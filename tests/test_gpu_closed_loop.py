@@ -4,10 +4,9 @@ control of each step, against the CPU oracle pipeline run the same way -- oracle
 the structured C IPM from the same carried iterate (controller.py:72-81, ocp.py:144-170).
 
 Warm start: acados keeps the SQP iterate between RTI steps (the NLP warm start, reproduced here: the
-solver object's x / u persist across steps) and, with qp_solver_warm_start = 1, starts HPIPM from the
-previous QP's primal solution.  The GPU IPM starts every QP from its own starting point instead; the QP
-solution is unique (lm > 0), so this changes only the iteration count, never the step (to the QP
-tolerance) -- the oracle below cold-starts the same way.
+solver object's x / u persist across steps) and, with qp_solver_warm_start = 1 (ocp.py:116, Ocp's
+default), starts HPIPM from the previous QP's primal solution; the oracle loop below starts its C IPM
+from its own previous du the same way.
 
 With the SDF flag off the loop is contractive (a 1e-10 change of x_0 shrinks step by step), and the
 GPU and the oracle agree to U0_ATOL at every step.  With the flag on, the soft FOV / SDF rows under
@@ -47,15 +46,16 @@ def _oracle_loop(O, onet, n, cfg, x0, p, K):
     xs = np.repeat(x0[:, None], N + 1, axis=1)
     us = np.broadcast_to(n.model.u_hover, (B, N, 4)).copy()
     prob = {"yref": n.y, "W": n.W, "yN": n.yN, "WN": n.WN, "dt": dt}
-    xo, u_hist = x0.copy(), []
+    xo, u_hist, du = x0.copy(), [], np.zeros((B, N, 4))
     for _ in range(K):
         if 0 < shift < N:
             xs[:, : N - shift] = xs[:, shift:N].copy()
             us[:, : N - shift] = us[:, shift:N].copy()
         xs[:, 0] = xo
         lin = O.linearize_batch(O.quad_model(cfg), onet, xs, us, p, dt)
-        r = O.qp_ipm_batch(lin, dict(prob, x=xs, u=us), xo, n.model, nthreads=4)
+        r = O.qp_ipm_batch(lin, dict(prob, x=xs, u=us), xo, n.model, nthreads=4, du_ws=du)
         assert (r["status"] == 0).all()
+        du = r["du"].copy()
         xs, us = xs + r["dx"], us + r["du"]
         u_hist.append(us[:, 0].copy())
         xo = _plant(O, onet, cfg, xo, us[:, 0], dt[0])

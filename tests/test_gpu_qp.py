@@ -188,7 +188,7 @@ def test_qp_nan_instance_fails_alone(gpu_ctx, cfg):
     assert np.array_equal(t["du"].cpu().numpy()[others], good_du[others]) and np.array_equal(it[others], good_it[others])
 
 
-def _agree(prob, x0, lin, model, got, ref, atol=ORC_ATOL):
+def _agree(prob, x0, lin, model, got, ref, atol=ORC_ATOL, lam_l1=None):
     """GPU vs the C restatement of the same IPM, instance by instance.  Both stop at the same iteration;
     on most instances the iterates agree to ~1e-7.  On a degenerate instance (a row with both its slack
     and its dual -> 0) the stopped iterate still moves along the flat direction by up to ~1e-4 at tol
@@ -201,11 +201,13 @@ def _agree(prob, x0, lin, model, got, ref, atol=ORC_ATOL):
         q = qp_oracle.stage_qp({k: v[b] for k, v in lin.items()}, prob["x"][b], prob["u"][b], x0[b], prob["yref"][b],
                                prob["W"][b], prob["yN"][b], prob["WN"][b], prob["dt"], model, 10.0)
         H, g, E, e, G, dd = qp_oracle.dense_problem(q)
-        z = [np.concatenate([s["dx"][b].ravel(), s["du"][b].ravel(), s["slack"][b][..., 0].ravel(),
-                             s["slack"][b][..., 1].ravel()]) for s in (got, ref)]
+        z = [qp_oracle.z_of(q, dict(dx=s["dx"][b], du=s["du"][b], sl=s["slack"][b][..., 0], su=s["slack"][b][..., 1]))
+             for s in (got, ref)]
         f = [0.5 * v @ H @ v + g @ v for v in z]
-        # each stopped iterate is within its duality gap sum_i t_i lambda_i <= m * tol of the optimum
-        gap = G.shape[0] * QP_TOL
+        # each stopped iterate is within its duality gap sum_i t_i lambda_i <= m * tol of the optimum (plus the
+        # primal residual priced by the multipliers, qp_oracle.objective_bound, where the caller has them)
+        gap = G.shape[0] * QP_TOL if lam_l1 is None else qp_oracle.objective_bound(
+            G.shape[0], QP_TOL, lam_l1[b], max(got["res"][b, 1], ref["res"][b, 1]))
         assert abs(f[0] - f[1]) <= 2 * gap, f"instance {b}: objective {f[0]} vs {f[1]} (gap bound {gap:.1e})"
         for v in z:
             assert np.abs(E @ v - e).max() < 1e-9 and (G @ v + dd).min() > -1e-8

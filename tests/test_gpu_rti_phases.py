@@ -110,3 +110,28 @@ def test_bound_rti_step_bitwise_equals_per_call_phases(gpu_ctx, cfg, B, N, graph
     for k in OUT + ("x", "u"):
         np.testing.assert_array_equal(ta[k].cpu().numpy(), tb[k].cpu().numpy(), err_msg=k)
     np.testing.assert_array_equal(ua.cpu().numpy(), ub.cpu().numpy())
+
+
+def test_graph_step_refuses_launch_after_workspace_growth(gpu_ctx, cfg):
+    """a captured step addresses the context's workspaces; a later call with a larger batch grows
+    (reallocates) them, and the launch then fails instead of running on freed device memory."""
+    import torch
+    B, N = 1, 40
+    ctx = _lib.Context(gpu_ctx.device)  # a fresh context: its workspaces are sized by this test's calls only
+    net = _lib.Net.siren(ctx, 0)
+    qm = _lib.quad_model(cfg)
+    opts = _lib.qp_opts(Quad(cfg))
+    prob, tb = _bufs(ctx, cfg, B, N, 11, False)
+    ub = torch.empty((B, 4), dtype=torch.float64, device=tb["x"].device)
+    step = _lib.RtiStep(ctx, net, qm, opts, B, N, prob["p"].shape[-1], tb, u0=ub, graph=True)
+    step()
+    ctx.synchronize()
+    prob2, t2 = _bufs(ctx, cfg, 64, N, 11, False)  # grows the QP workspace and the SDF buffers
+    _lib.rti_prepare(ctx, net, qm, opts, 64, N, prob2["p"].shape[-1], t2)
+    _lib.qp_feedback(ctx, opts, 64, N, t2)
+    ctx.synchronize()
+    with pytest.raises(_lib.SdfnmpcError, match="reallocated"):
+        step()
+    del step
+    net.close()
+    ctx.close()

@@ -132,7 +132,12 @@ def test_l4c_shim_any_latent_size(golden, tmp_path, name):
     D = 3 + spec.size_latent
     wpath = tmp_path / f"{name}.sdfw"
     W.save(str(wpath), spec, W.siren_weights(spec, SEED, bias_gain=BIAS_GAIN))
-    lib = ctypes.CDLL(_lib.L4C_PATH)
+    # a private copy of the library: its own shim state (the width of the patterns it hands out is fixed per
+    # library instance, as CasADi keeps them; this process's other tests hand out the deployed width)
+    import shutil
+    so = tmp_path / f"libsdf_l4c_{name}.so"
+    shutil.copy(_lib.L4C_PATH, so)
+    lib = ctypes.CDLL(str(so))
     lib.sdf_l4c_configure.argtypes = [ctypes.c_char_p, ctypes.c_int]
     lib.sdf_l4c_last_error.restype = ctypes.c_char_p
     assert lib.sdf_l4c_configure(str(wpath).encode(), 0) == 0, lib.sdf_l4c_last_error()
@@ -164,8 +169,17 @@ def test_l4c_shim_any_latent_size(golden, tmp_path, name):
         df[i], gr[i] = out[0], jac
     sub = {k: (g[k][:n] if k.startswith(name + "/") else g[k]) for k in g.files if k.startswith(name + "/")}
     _check(df, gr, sub, name, cols=D)
-    # back to the deployed net: the width follows the configured network
+    # CasADi keeps the patterns it was handed (width D here), so a reconfiguration to a network of
+    # another width (the deployed net, 131) is refused, and the loaded network keeps serving unchanged
     wdef = tmp_path / "sdf_l4c.sdfw"
     W.save(str(wdef), W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, 0))
-    assert lib.sdf_l4c_configure(str(wdef).encode(), 0) == 0
-    assert lib.sdf_l4c_sparsity_in(0)[0] == 131
+    if D != 131:
+        assert lib.sdf_l4c_configure(str(wdef).encode(), 0) != 0
+        assert b"was handed out" in lib.sdf_l4c_last_error()
+        assert lib.sdf_l4c_sparsity_in(0)[0] == D
+        x = np.ascontiguousarray(inp[0])
+        out = np.zeros(1)
+        assert lib.sdf_l4c((P * 1)(x.ctypes.data_as(P)), (P * 1)(out.ctypes.data_as(P)), None, None, 0) == 0
+        assert out[0] == df[0]
+    # a network of the same width is accepted (here: the same file again)
+    assert lib.sdf_l4c_configure(str(wpath).encode(), 0) == 0 and lib.sdf_l4c_sparsity_in(0)[0] == D
