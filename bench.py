@@ -99,6 +99,7 @@ def main():
     ap.add_argument("--no-c2", action="store_true", help="skip the CasADi-external (libsdf_l4c.so) call leg")
     ap.add_argument("--no-c1", action="store_true", help="skip the B=1, N=20 controller-step leg (config C1)")
     ap.add_argument("--no-scene", action="store_true", help="skip the obstacle-scene SDF side leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the config-C5 sub-block of the default line")
     ap.add_argument("--config", choices=("c3", "c5"), default="c3",
                     help="c3: the headline 1024 x 40 RTI (default); c5: 4x-wide SDF MLP + in-loop VAE encode, "
                          "N = 60, 4096 instances over 8 GPUs (512 per GPU)")
@@ -310,6 +311,13 @@ def main():
     scene = None
     if rank == 0 and not args.no_scene:
         scene = bench_scene(local, B, N)
+    # config C5 at its per-GPU size (512 instances x N = 60, VAE encode + 4x-wide SDF + RTI), under the
+    # driver's clock: the same leg as `bench.py --config c5` (c5_leg), 10 timed steps
+    c5 = None
+    if rank == 0 and world == 1 and not args.no_c5:
+        c5 = c5_leg(local, dev, 1, 0, 512, 60, 10, 3, args.no_cpu_baseline)
+        for k in ("metric", "n_gpus", "higher_is_better", "vs_baseline", "data"):
+            c5.pop(k, None)
     # traffic from the committed PMC profile of this same command (profiles/)
     traffic = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_summary.json")
@@ -319,6 +327,10 @@ def main():
                 pmc = json.load(f)
             if pmc.get("B") == B and pmc.get("N") == N and pmc.get("tile_rows") == args.tile_rows:
                 traffic = {k: pmc["kernels"][k]["hbm_bytes_per_launch"] for k in ("rti_qp", "sdf_mlp")}
+                sys.path.insert(0, os.path.join(ROOT, "tools"))
+                from pmc_summary import kernel_sources_sha16
+                traffic["source"] = {"file": "profiles/pmc_summary.json", "commit": pmc.get("commit"),
+                                     "kernel_sources_match": pmc.get("kernel_sources_sha16") == kernel_sources_sha16(ROOT)}
         except Exception:
             traffic = None
 
@@ -384,6 +396,7 @@ def main():
         "roofline": {"bound": "mfma", "kernel": "rti_qp", "achieved": qp_tf, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": qp_tf / FP64_PEAK_TFLOPS,
                      "traffic": traffic["rti_qp"] if traffic else None, "flop_per_launch": qp_flop,
+                     "traffic_source": traffic["source"] if traffic else None,
                      "note": "latency-bound serial Riccati recursion (one wavefront per instance); f64 peak"},
         "roofline_sdf": {"bound": "mfma", "kernel": "sdf_mlp", "achieved": sdf_tf, "peak": FP32_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": sdf_tf / FP32_MFMA_PEAK_TFLOPS,
@@ -399,6 +412,7 @@ def main():
         "c2": c2,
         "c1": c1,
         "scene": scene,
+        "c5": c5,
     }
     if rank == 0:
         print(json.dumps(out))
@@ -620,15 +634,30 @@ def main_c5(args):
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(backend)
-    from sdf_nmpc_amd import _lib, shard, synth, vae as V, weights as W
-    from sdf_nmpc_amd.config import Config
-    from sdf_nmpc_amd.model import Quad
-
+    from sdf_nmpc_amd import shard
     N = args.horizon if args.horizon != 40 else 60
     B = args.batch if args.batch != 1024 else 512
     if args.global_batch > 0:
         lo, hi = shard.instance_range(args.global_batch, world, rank)
         B = hi - lo
+    steps = args.steps if args.steps != 50 else 10
+    warm = args.warmup if args.warmup != 10 else 3
+    out = c5_leg(local, dev, world, rank, B, N, steps, warm, args.no_cpu_baseline, args.global_batch)
+    if rank == 0:
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def c5_leg(local, dev, world, rank, B, N, steps, warm, no_cpu, global_batch=0):
+    """Config C5 on this GPU (main_c5, and the c5 sub-block of the default line): B instances at horizon N,
+    per step the VAE encode of B depth images, the latents packed into p on the device, one SQP-RTI solve
+    with the 4x-wide SDF.  Returns the C5 result dict (value over all ranks)."""
+    import torch
+    import torch.distributed as dist
+    from sdf_nmpc_amd import _lib, shard, synth, vae as V, weights as W
+    from sdf_nmpc_amd.config import Config
+    from sdf_nmpc_amd.model import Quad
     cfg = Config(mpc__N=N)
     ctx = _lib.Context(local, stream=torch.cuda.current_stream(dev).cuda_stream)
     blob = W.pack(W.WIDE_SPEC, W.siren_weights(W.WIDE_SPEC, seed=0)) if rank == 0 else None
@@ -694,12 +723,10 @@ def main_c5(args):
         el = time.perf_counter() - t0
         return shard.max_over_ranks(el, dev) if world > 1 else el
 
-    steps = args.steps if args.steps != 50 else 10
-    warm = args.warmup if args.warmup != 10 else 3
     for _ in range(warm):
         step()
     el = timed(step, steps)
-    total = args.global_batch if args.global_batch > 0 else world * B
+    total = global_batch if global_batch > 0 else world * B
     it = bufs["iters"].cpu().numpy()
     st = bufs["status"].cpu().numpy()
     ctx.enable_timing(True)
@@ -725,7 +752,7 @@ def main_c5(args):
         "value": total * steps / el,
         "unit": "instance-RTI-solves/s (incl. VAE encode)",
         "n_gpus": world, "steps": steps, "warmup": warm, "ms_per_step": el / steps * 1e3,
-        "higher_is_better": True, "scaling": "strong" if args.global_batch > 0 else "weak", "vs_baseline": None,
+        "higher_is_better": True, "scaling": "strong" if global_batch > 0 else "weak", "vs_baseline": None,
         "dtype": "f32 (VAE convs as fp32-exact bf16 splits on the bf16 MFMA; wide SDF MLP on the f32 MFMA) + f64 "
                  "(linearisation, QP)",
         "data": "synthetic depth images (seeded scenes + noise), synthetic VAE weights, SIREN-init wide SDF seed 0",
@@ -746,7 +773,7 @@ def main_c5(args):
         "vae_ms": vae_ms, "wide_sdf_ms": wide_ms,
         "cpu_baseline": None,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not no_cpu:
         # the same per-instance work on the host: fp64 C encoder (oracle/vae.c) of the instance's image,
         # the wide network's preparation phase (oracle/oracle.c) and the structured C IPM, a bounded sample
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -774,10 +801,11 @@ def main_c5(args):
                                "sample": f"{S} instances: fp64 C encoder (oracle/vae.c, OpenMP) of one 270x480 image "
                                          f"each, the wide network's preparation phase at N={N} and the structured "
                                          "C IPM (oracle/oracle.c, oracle/qp_ipm.c)"}
-    if rank == 0:
-        print(json.dumps(out))
-    if world > 1:
-        dist.destroy_process_group()
+    ctx.synchronize()
+    vae.close()
+    net.close()
+    ctx.close()
+    return out
 
 
 if __name__ == "__main__":

@@ -104,3 +104,36 @@ def test_closed_loop_matches_oracle_pipeline(oracle_lib, shift, flag, margin):
         env = np.maximum(U0_ATOL, ENVELOPE * np.abs(up - uo).max(axis=(1, 2)))
         assert (d[:2] <= U0_ATOL).all() and (d <= env).all(), (d, env)
     n.ocp.close()
+
+
+@pytest.mark.parametrize("flag,margin", [(0.0, None), (1.0, -0.6)])
+def test_non_uniform_grid_closed_loop_matches_oracle(oracle_lib, flag, margin):
+    """mpc.uniform_dt = False (ocp.py:21-27): the first nb_short_nodes intervals are control_loop_time
+    (10 ms) and the rest share T - 20 ms, so dt_k feeds ERK4, the dt-scaled cost / slack weights and the
+    dt-scaled Levenberg-Marquardt term node by node.  N = 40: K closed-loop Nmpc.solve steps (the plant
+    advanced by u_0 over dt_0 = 10 ms) against the oracle pipeline on the same grid, u_0 within 2e-5 at
+    every step (contractive settings: flag off, or on with the SDF rows live and inactive)."""
+    O = oracle_lib
+    over = {} if margin is None else {"mpc__bound_margin": margin}
+    cfg = Config(mpc__N=40, mpc__uniform_dt=False, **over)
+    B = 4
+    n = Nmpc(cfg, batch=B)
+    dt = n.ocp.dt
+    assert dt.shape == (40,) and dt[0] == dt[1] == 0.01 and abs(dt.sum() - cfg.mpc.T) < 1e-12
+    assert np.ptp(dt[2:]) < 1e-15 and dt[2] > 0.03
+    x0 = scenario(n, np.random.default_rng(41))
+    n.set_sdf_flag(flag)
+    onet = O.Net(W.DEFAULT_SPEC, W.siren_weights(W.DEFAULT_SPEC, seed=0))
+    ug, xg = [], x0.copy()
+    for _ in range(K):
+        n.set_x0(xg)
+        assert n.solve() == 0 and (n.ocp.status == 0).all()
+        ug.append(n.get_u().copy())
+        xg = _plant(O, onet, cfg, xg, ug[-1], dt[0])
+    uo, xs, us = _oracle_loop(O, onet, n, cfg, x0, n.p, K)
+    d = np.abs(np.array(ug) - uo).max(axis=(1, 2))
+    print(f"\nnon-uniform grid, flag {flag}: max |u0 - u0_oracle| per step {d.max():.2e}")
+    assert d.max() <= U0_ATOL, d
+    xgpu, ugpu = n.get_matrices()
+    np.testing.assert_allclose(ugpu, us, rtol=0, atol=U0_ATOL)
+    n.ocp.close()
