@@ -1956,11 +1956,14 @@ extern "C" int sdfnmpc_vae_encode(sdfnmpc_ctx* ctx, sdfnmpc_vae* v, const sdfnmp
         n_x = std::max(n_x, nb);
         n_t = std::max(n_t, nb);
     }
-    // in floats per image: planes take 1.5 floats a value (n_x, n_t are multiples of 64: every plane 16-byte aligned)
+    // in floats per image: planes take 1.5 floats a value (n_x, n_t are multiples of 64: every plane 16-byte
+    // aligned once X is); the preprocessed images [B][H][W] are padded to a multiple of 64 floats, so X (and every
+    // plane after it, staged by 16-byte LDS-DMA) starts 256-byte aligned for any H, W, B
+    const size_t pre_pad = (n_pre * B + 63) & ~(size_t)63;
     const size_t per = n_pre + 2 * (3 * n_x / 2) + 3 * n_t / 2 + n_t + 2048;
-    HIPCHK(v->ws.ensure(per * B * sizeof(float)));
+    HIPCHK(v->ws.ensure((per * B + 64) * sizeof(float)));
     float* P = (float*)v->ws.p;
-    unsigned short* X = (unsigned short*)(P + n_pre * B);
+    unsigned short* X = (unsigned short*)(P + pre_pad);
     unsigned short* Y = X + 3 * n_x * B;
     unsigned short* T = Y + 3 * n_x * B;
     float* S = (float*)(T + 3 * n_t * B);

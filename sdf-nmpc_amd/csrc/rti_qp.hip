@@ -500,7 +500,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     // (C x)_{r-14}; kind 0 (initial iterate, u = 0): rows r < 10 of A x + c from the stage record.
     // Factor rows of nodes < PD come from fsave (written late in the backward sweeps).
     double chain = 0.0;  // p_{k+1} of the corrector sweep in lanes 0..9
-    auto fw_stage = [&](auto Kc, int k, const int lane) {
+    auto fw_stage = [&](auto Kc, int k, const int lane, auto&& hook) {
         const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 14 + NS;
         const int fcj = fc ? lane - 14 : 0;
         constexpr int K = decltype(Kc)::value;
@@ -535,6 +535,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         d2 xv[NX / 2];  // the chain input x_k, read after everything else
 #pragma unroll
         for (int l = 0; l < NX / 2; ++l) xv[l] = xp[l];
+        hook();  // every window read of the stage is issued: the next position's window may be committed
         __builtin_amdgcn_sched_barrier(0);
         double a0 = off, a1 = 0.0;
 #pragma unroll
@@ -575,7 +576,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
 
 #define FBST(v, off) bst(v, rsF, off, sko)
     d4 Pa = {0.0, 0.0, 0.0, 0.0};  // [P | p] of the node ahead, accumulator layout
-    auto bf_stage = [&](auto Fc, int q, const FConst& f) {
+    auto bf_stage = [&](auto Fc, int q, const FConst& f, auto&& hook) {
         constexpr bool FIRST = decltype(Fc)::value;  // q == 0: the terminal node
         const int g = f.g, c = f.c;
         const int og01 = f.og01, og2 = f.og2, cgi = f.cgi, gj = f.gj, gj4 = f.g, ab01 = f.ab01, ab2 = f.ab2;
@@ -614,6 +615,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
                 T[r] = win[(a < NX && c < NX) ? R_H + tri10(lo, hi) : (a < NX && c == 14) ? R_G + a : R_Z];
             }
             Pa = T;
+            hook();
             for (int t0 = 0; t0 < nhN; t0 += 4) {
                 const int jr = t0 + g;
                 const bool live = jr < nhN;
@@ -666,6 +668,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         const double bm = win[bmi];
         const double hxa = win[hxu_i];
         const double hua = win[huu_i] + huu_b * s.bd[k * NU + gj4];
+        hook();  // the last window read of the stage: the next position's window may be committed
         Hh = mfma(cg, fb, Hh);
         FSTAMP(9, Mu);
         // ---- L = chol(R^): R^[i][j] = M'[10+i][10+j] at lane 16 i + 10 + j
@@ -726,7 +729,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     // v = P c + p_{k+1};  lane r < 10: p_k[r] = g~_x[r] + (K^T g~_u)[r] + (A~^T v)[r]   (the chain)
     //                     lane 10 + i: z_u[i] = g~_u[i] + (B^T v)[i]
     // then w = L^-1 z_u, k_ff = -L^-T w, b~ = c + B k_ff (off the chain).  g~ = g + fold | box.
-    auto bc_stage = [&](auto Fc, int q, const int lane) {
+    auto bc_stage = [&](auto Fc, int q, const int lane, auto&& hook) {
         constexpr bool FIRST = decltype(Fc)::value;
         const bool fx = lane < NX, fu = lane >= NX && lane < 14;
         const ldsd* bc_row = fx ? win + F_AB + lane : fu ? win + WB_R + lane * 10 : win;
@@ -744,6 +747,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         FSTAMP(7, mfx);
         double off = *bc_g;
         if constexpr (FIRST) {  // p_N = g_N + sum_j gamma_j C_j^T over the terminal rows (C from LDS)
+            hook();
             const ldsd* ct = fx ? s.ctN + lane : s.zero;
             for (int j = 0; j < nhN; ++j) off += s.fg[NGS + j] * ct[fx ? 10 * j : 0];
             chain = off;
@@ -774,6 +778,7 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         }
         const double cb = win[WB_R + R_C + bx], B0 = win[WB_R + 100 + bx], B1 = win[WB_R + 110 + bx];
         const double B2 = win[WB_R + 120 + bx], B3 = win[WB_R + 130 + bx];
+        hook();  // the last window read of the stage: the next position's window may be committed
         // the chain input p_{k+1}: lanes 0..9 of the register chain, broadcast through scalar registers
         double pv[NX];
 #pragma unroll
@@ -1208,22 +1213,36 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
     };
 
     // ------------------------------------------------------------ IPM: sweeps over the record stream
-    auto stage = [&](auto Kc, auto Fc, int q, const auto& ln) {
+    auto stage = [&](auto Kc, auto Fc, int q, const auto& ln, auto&& hook) {
         constexpr int K = decltype(Kc)::value;
-        if constexpr (K == 1) bf_stage(Fc, q, ln);
-        else if constexpr (K == 3) bc_stage(Fc, q, ln);
-        else fw_stage(Kc, q, ln);
+        if constexpr (K == 1) bf_stage(Fc, q, ln, hook);
+        else if constexpr (K == 3) bc_stage(Fc, q, ln, hook);
+        else fw_stage(Kc, q, ln, hook);
     };
-    // one stream position: commit ring slot S (position q of this sweep), refill it with position qi
-    // of a sweep of kind KI, run the stage
-    auto position = [&](auto Kc, auto KIc, auto Sc, auto Fc, int q, int qi, bool live, const auto& ln) {
+#ifndef QP_LATE_COMMIT
+    // one stream position: its window was committed by the previous position's hook; refill its ring slot S
+    // with position qi of a sweep of kind KI, run the stage, whose hook -- after the stage's last window read
+    // -- commits the next position (ring slot S + 1, kind KN) into the window: the commit's wait for the
+    // record loads and its LDS writes run under the stage's arithmetic instead of heading the next stage
+    auto position = [&](auto Kc, auto KIc, auto KNc, auto Sc, auto Fc, int q, int qi, bool live, const auto& ln) {
+        constexpr int S = decltype(Sc)::value, S1 = (S + 1) % PD;
+        issue(KIc, ring[S], qi);
+        wave_sync();
+        auto hook = [&]() { commit(KNc, ring[S1]); };
+        if (live) stage(Kc, Fc, q, ln, hook);
+        else hook();
+        wave_sync();
+    };
+#else  // diagnostic: the round-5 schedule (commit at the head of each position)
+    auto position = [&](auto Kc, auto KIc, auto KNc, auto Sc, auto Fc, int q, int qi, bool live, const auto& ln) {
         constexpr int S = decltype(Sc)::value;
         commit(Kc, ring[S]);
         issue(KIc, ring[S], qi);
         wave_sync();
-        if (live) stage(Kc, Fc, q, ln);
+        if (live) stage(Kc, Fc, q, ln, [] {});
         wave_sync();
     };
+#endif
     auto sweep = [&](auto Kc) {
         constexpr int K = decltype(Kc)::value, KN = K == 4 ? 1 : K + 1;
         // the stages' lane constants derive from an opaque copy of the lane id, so they are hoisted
@@ -1237,32 +1256,41 @@ __global__ __launch_bounds__(64, QP_LB_WAVES) void rti_qp_kernel(QpArgs A) {
         using F_ = IC<0>;
         // slot S of a trip: position q0 + S (the first position of the sweep is its first node: the
         // terminal node of a backward sweep)
+        // KN of a position: the kind of the position after it (the next sweep's first one after the last slot
+        // of the last trip)
+        using KNL = IC<KN>;
         if (NP > PD) {
             // first trip
             each_slot([&](auto Sc) {
                 constexpr int S = decltype(Sc)::value;
-                position(Kc, Kc, Sc, std::conditional_t<S == 0, T_, F_>{}, S, S + PD, true, ln);
+                position(Kc, Kc, Kc, Sc, std::conditional_t<S == 0, T_, F_>{}, S, S + PD, true, ln);
             });
             int q0 = PD;
             for (; q0 < NP - PD; q0 += PD)  // every position of these trips is a node
                 each_slot([&](auto Sc) {
                     constexpr int S = decltype(Sc)::value;
-                    position(Kc, Kc, Sc, F_{}, q0 + S, q0 + S + PD, true, ln);
+                    position(Kc, Kc, Kc, Sc, F_{}, q0 + S, q0 + S + PD, true, ln);
                 });
             // last trip: refill with the next sweep's first positions; tail positions compute nothing
             each_slot([&](auto Sc) {
                 constexpr int S = decltype(Sc)::value;
-                position(Kc, IC<KN>{}, Sc, F_{}, q0 + S, S, q0 + S < N1, ln);
+                position(Kc, IC<KN>{}, std::conditional_t<S == PD - 1, KNL, decltype(Kc)>{}, Sc, F_{}, q0 + S, S,
+                         q0 + S < N1, ln);
             });
         } else {  // N + 1 <= PD: a single trip
             each_slot([&](auto Sc) {
                 constexpr int S = decltype(Sc)::value;
-                position(Kc, IC<KN>{}, Sc, std::conditional_t<S == 0, T_, F_>{}, S, S, S == 0 || S < N1, ln);
+                position(Kc, IC<KN>{}, std::conditional_t<S == PD - 1, KNL, decltype(Kc)>{}, Sc,
+                         std::conditional_t<S == 0, T_, F_>{}, S, S, S == 0 || S < N1, ln);
             });
         }
     };
 
     each_slot([&](auto Sc) { issue(IC<0>{}, ring[decltype(Sc)::value], decltype(Sc)::value); });
+#ifndef QP_LATE_COMMIT
+    commit(IC<0>{}, ring[0]);  // the stream's first position (later ones: the previous stage's hook)
+    wave_sync();
+#endif
     sweep(IC<0>{});
     term_cx(s.cxa, s.dx);
     STAMP(1);
