@@ -224,7 +224,7 @@ def test_scene_closed_loop_flag_sets_vs_oracle(oracle_lib, name):
                     gap = 0.5 * z @ H @ z + g @ z - (0.5 * zs @ H @ zs + g @ zs)
                     assert np.abs(E @ z - e).max() < 1e-8 and (G @ z + dd).min() > -1e-7, (b, (G @ z + dd).min())
                     assert gap <= qp_oracle.objective_bound(G.shape[0], 1e-8, ex["lam_l1"], rp), (b, gap, ex["lam_l1"], rp)
-                            xhist.append(xg[:, 0].copy())
+            xhist.append(xg[:, 0].copy())
             xg = S.plant(O, onet, cfg, xg, ug[-1], ocp.dt[0])
     finally:
         ocp.close()
