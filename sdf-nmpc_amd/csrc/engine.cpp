@@ -633,6 +633,8 @@ struct sdfnmpc_net {
     uint64_t fingerprint = 0;
     bool wide = false;
     WideDev wd;
+    WideRowArgs wrow{};    // the row evaluator's operands (sdf_row_wide.hip); per-call fields left zero
+    bool wrow_ok = false;  // the row evaluator and its server fit this network (LDS, weight bytes)
     // process-unique id: caches keyed on a network (the host path's hoist) never confuse a freed
     // network with a new one allocated at the same address
     uint64_t uid = next_uid();
@@ -669,6 +671,13 @@ static uint64_t net_fingerprint(HostNet& h) {  // FNV-1a over the parameters in 
         for (size_t q = 0; q < nb; ++q) fp = (fp ^ b[q]) * 1099511628211ULL;
     }
     return fp;
+}
+
+// weight bytes up to which a variant network takes the row evaluator on the host path
+// (SDFNMPC_WIDE_ROW_MAX_MB overrides; 0 sends every variant to the layer-by-layer schedule)
+static size_t wide_row_weight_cap() {
+    if (const char* e = getenv("SDFNMPC_WIDE_ROW_MAX_MB")) return (size_t)(atof(e) * 1048576.0);
+    return (size_t)64 << 20;
 }
 
 static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
@@ -750,6 +759,17 @@ static int upload_wide(sdfnmpc_ctx* ctx, HostNet&& h, sdfnmpc_net** out) {
     w.nb = h.nd * h.nf; w.e3 = e3; w.act = h.act; w.LH = Lh; w.LZ = LZ;
     net->args.b5 = h.b5[0];
     net->args.w0 = h.w0;
+    WideRowArgs& ra = net->wrow;
+    ra.F1 = w.F1; ra.F2 = w.F2; ra.F3 = w.F3; ra.F4 = w.F4;
+    ra.B4 = w.B4; ra.B3h = w.B3h; ra.B3e = w.B3e; ra.B2 = w.B2; ra.B1e = w.B1e;
+    ra.Bz = w.Bz; ra.Hz = w.Hz; ra.bz = w.bz; ra.b2 = w.b2; ra.b4 = w.b4; ra.w5 = w.w5; ra.emb_tab = w.emb_tab;
+    ra.b5 = h.b5[0]; ra.w0 = h.w0;
+    ra.P1 = P1; ra.P2 = P2; ra.P3 = P3; ra.P4 = P4; ra.NEK = NEK; ra.NEB = NEB; ra.nb = w.nb;
+    ra.LH = Lh; ra.LZ = LZ; ra.e3 = e3 ? 1 : 0; ra.act = h.act;
+    // one workgroup per row streams every weight once per row: worth it while the weights are L2 / MALL
+    // sized (a C5-sized network is faster on the layer-by-layer GEMMs)
+    const size_t srv_lds = wide_row_lds_bytes(ra) + 2 * SDF_MBOX_FLOATS * sizeof(float);
+    net->wrow_ok = srv_lds <= 160 * 1024 && blob.size() * sizeof(float) <= wide_row_weight_cap();
     net->fingerprint = net_fingerprint(h);
     net->host = std::move(h);
     *out = net;
@@ -1125,16 +1145,17 @@ static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const fl
             return fail(SDFNMPC_E_HIP, std::string("sdf server: ") + hipGetErrorString(q));
         }
     }
+    const int LH = net->host.L;  // the mailbox holds [rows][4] | [rows][LH] (SdfMbox)
     memcpy(S.mb->in, hp, (size_t)rows * 4 * sizeof(float));
-    memcpy(S.mb->in + (size_t)rows * 4, hl, (size_t)rows * L * sizeof(float));
+    memcpy(S.mb->in + (size_t)rows * 4, hl, (size_t)rows * LH * sizeof(float));
     S.mb->rows = rows;
     S.mb->grad = grad ? 1 : 0;
     const unsigned long long seq = ++S.seq;
     __atomic_store_n(&S.mb->seq_in, seq, __ATOMIC_RELEASE);
-    SdfRowArgs ra = net->row;
     auto relaunch = [&]() {
         ++S.epoch;
-        return launch_sdf_server(ra, S.mb_dev, S.idle_ticks, S.life_ticks, S.epoch, S.stream);
+        return net->wide ? launch_sdf_server_wide(net->wrow, S.mb_dev, S.idle_ticks, S.life_ticks, S.epoch, S.stream)
+                         : launch_sdf_server(net->row, S.mb_dev, S.idle_ticks, S.life_ticks, S.epoch, S.stream);
     };
     if (!S.live) {
         HIPCHK(relaunch());
@@ -1168,7 +1189,7 @@ static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const fl
         }
     }
     const volatile float* o = S.mb->out;
-    const size_t n = (size_t)rows * (grad ? 4 + L : 4);
+    const size_t n = (size_t)rows * (grad ? 4 + LH : 4);
     for (size_t i = 0; i < n; ++i) ho[i] = o[i];
     S.last = clk::now();
     const volatile SdfMbox* vm = S.mb;
@@ -1176,8 +1197,9 @@ static int srv_call(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, int rows, const fl
     S.acc[1] += (double)(vm->t_done - vm->t_staged) * 1e3 / S.khz;
     S.acc[2] += std::chrono::duration<double>(S.last - t0).count() * 1e6;
     S.acc[3] += 1.0;
-    for (int i = 0; i < 14; ++i)
-        S.ph[i] += (double)(vm->t_phase[i] - (i ? vm->t_phase[i - 1] : vm->t_staged)) * 1e3 / S.khz;
+    if (!net->wide)  // row_eval's phase stamps (the variant server keeps none)
+        for (int i = 0; i < 14; ++i)
+            S.ph[i] += (double)(vm->t_phase[i] - (i ? vm->t_phase[i - 1] : vm->t_staged)) * 1e3 / S.khz;
     return SDFNMPC_OK;
 }
 
@@ -1230,7 +1252,8 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         hp[r * 4 + 3] = 0.0f;
         for (int k = 0; k < L; ++k) hl[(size_t)r * L + k] = (float)in[(size_t)r * D + 3 + k];
     }
-    const bool use_row = !net->wide && rows <= SDF_ROW_MAX;
+    // the row evaluators: sdf_row.hip for the deployed network, sdf_row_wide.hip for a variant that fits it
+    const bool use_row = net->wide ? net->wrow_ok && rows <= wide_row_max_rows(L) : rows <= SDF_ROW_MAX;
     bool served = false;
     if (use_row && srv_enabled(ctx)) {  // the resident server: no launch, no copies, no synchronisation
         const int rc = srv_call(ctx, net, rows, hp, hl, grad != nullptr, ho);
@@ -1245,13 +1268,23 @@ extern "C" int sdfnmpc_sdf_eval_host(sdfnmpc_ctx* ctx, const sdfnmpc_net* net, i
         float* dpos = (float*)ctx->hin.p;
         float* dout = (float*)ctx->hout.p;
         HIPCHK(hipMemcpyAsync(dpos, hp, nin * sizeof(float), hipMemcpyHostToDevice, ctx->stream));
-        SdfRowArgs ra = net->row;
-        ra.pos = (const float4*)dpos;
-        ra.latent = dpos + (size_t)rows * 4;
-        ra.out = (float4*)dout;
-        ra.grad_latent = grad ? dout + (size_t)rows * 4 : nullptr;
-        ra.rows = rows;
-        HIPCHK(timed(ctx, "sdf_row", [&] { return launch_sdf_row(ra, ctx->stream); }));
+        if (net->wide) {
+            WideRowArgs ra = net->wrow;
+            ra.pos = (const float4*)dpos;
+            ra.latent = dpos + (size_t)rows * 4;
+            ra.out = (float4*)dout;
+            ra.grad_latent = grad ? dout + (size_t)rows * 4 : nullptr;
+            ra.rows = rows;
+            HIPCHK(timed(ctx, "sdf_row_wide", [&] { return launch_sdf_row_wide(ra, ctx->stream); }));
+        } else {
+            SdfRowArgs ra = net->row;
+            ra.pos = (const float4*)dpos;
+            ra.latent = dpos + (size_t)rows * 4;
+            ra.out = (float4*)dout;
+            ra.grad_latent = grad ? dout + (size_t)rows * 4 : nullptr;
+            ra.rows = rows;
+            HIPCHK(timed(ctx, "sdf_row", [&] { return launch_sdf_row(ra, ctx->stream); }));
+        }
         HIPCHK(hipMemcpyAsync(ho, dout, (grad ? nin : (size_t)rows * 4) * sizeof(float), hipMemcpyDeviceToHost,
                               ctx->stream));
         HIPCHK(host_wait(ctx));

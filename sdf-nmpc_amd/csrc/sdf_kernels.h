@@ -108,6 +108,7 @@ struct alignas(128) SdfMbox {
     float in[SDF_ROW_MAX * (4 + 128)];   // [rows][4] Co_p_B | [rows][L] latent
     float out[SDF_ROW_MAX * (4 + 128)];  // [rows][4] (df, d df / d pos) | [rows][L] d df / d latent
 };
+constexpr int SDF_MBOX_FLOATS = SDF_ROW_MAX * (4 + 128);  // in / out capacity (rows x (4 + size_latent))
 
 template <typename T>
 struct HoistArgs {
@@ -155,6 +156,30 @@ struct WideSdfArgs {
     float4* out;                      // [rows] (df, d df / d pos) or NULL
     double* h; double* Jh; double max_df;
 };
+
+// Single-row latency path for every network other than the deployed one (sdf_row_wide.hip): the wide
+// schedule's row-major [N][K] operands (engine.cpp upload_wide) as GEMVs inside one 512-thread workgroup per
+// row, value + full input gradient (d df / d pos and d df / d latent), served by the resident server or
+// launched per call.  Same semantics as wide_gemm's layers (activations, res modes, padding).
+struct WideRowArgs {
+    const float *F1, *F2, *F3, *F4;            // forward [P1][NEK], [P2][P1], [P3][P2 (+ NEK)], [P4][P3]
+    const float *B4, *B3h, *B3e, *B2, *B1e;    // backward [P3][P4], [P2][P3], [NEB][P3], [P1][P2], [NEB][P1]
+    const float *Bz, *Hz, *bz, *b2, *b4, *w5;  // [LZ][P1 + P3], [P1 + P3][LZ], [P1 + P3], [P2], [P4], [P4]
+    const float4* emb_tab;                     // [NEK]
+    float b5, w0;
+    int P1, P2, P3, P4, NEK, NEB, nb, LH, LZ, e3, act;
+    // per call
+    const float4* pos;      // [rows] (Co_p_B, pad)
+    const float* latent;    // [rows][LH]
+    float4* out;            // [rows] (df, d df / d pos)
+    float* grad_latent;     // [rows][LH] or NULL
+    int rows;
+};
+size_t wide_row_lds_bytes(const WideRowArgs& a);        // the evaluator's dynamic LDS
+int wide_row_max_rows(int LH);                           // rows per server request (the mailbox's capacity)
+hipError_t launch_sdf_row_wide(const WideRowArgs& a, hipStream_t s);
+hipError_t launch_sdf_server_wide(const WideRowArgs& a, SdfMbox* mb_dev, long long idle_ticks, long long life_ticks,
+                                  unsigned long long epoch, hipStream_t s);
 
 hipError_t launch_wide_gemm(const WideGemmArgs& a, int epi, hipStream_t s);
 template <typename T>  // double (stage parameters) or float
