@@ -16,7 +16,8 @@ import numpy as np
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_DIR = os.path.join(PKG_DIR, "lib")
-LIB_PATH = os.path.join(LIB_DIR, "libsdfnmpc.so")
+# SDFNMPC_LIB: a diagnostic build of the same library (tools/build_variant.sh, tools/exp/*.sh)
+LIB_PATH = os.environ.get("SDFNMPC_LIB") or os.path.join(LIB_DIR, "libsdfnmpc.so")
 L4C_PATH = os.path.join(LIB_DIR, "libsdf_l4c.so")
 
 # exported symbols declared in include/sdfnmpc.h (checked by tests/test_abi.py)

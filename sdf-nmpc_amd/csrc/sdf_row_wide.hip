@@ -66,10 +66,12 @@ __device__ __forceinline__ float dot4(float4 w, float4 x, float a) {
     return fmaf(w.w, x.w, a);
 }
 
-// out[j] = W[j][:K1 + K2] . [x1 | x2] for j < J; W row-major with row stride K1 + K2 (multiples of 4 floats),
-// x1 / x2 16-byte aligned in LDS.  Ends with a workgroup barrier.
+// epi(j, W[j][:K1 + K2] . [x1 | x2]) for j < J, the U rows of a group's batch through the epilogue at once (on
+// lanes 0..U-1 of the group); W row-major with row stride K1 + K2 (multiples of 4 floats), x1 / x2 16-byte
+// aligned in LDS.  Ends with a workgroup barrier.
+template <typename Epi>
 __device__ __forceinline__ void gemv(const float* W_, int J, const float* x1, int K1, const float* x2, int K2,
-                                     float* out) {
+                                     Epi&& epi) {
     const float* __restrict__ W = launder(W_);
     const int t = tix(), g = t / GRP, q = t % GRP;
     const int C1 = K1 / 4, C = (K1 + K2) / 4;
@@ -101,12 +103,15 @@ __device__ __forceinline__ void gemv(const float* W_, int J, const float* x1, in
                 for (int u = 0; u < U; ++u) a[u] = dot4(w[u][i], x, a[u]);
             }
         }
+        // every lane of a group gets the U sums; lane q < U takes row j0 + q RPP through the epilogue
+        float mine = 0.0f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const float v = row16_sum(a[u]);
-            const int j = j0 + u * RPP;
-            if (q == 0 && j < J) out[j] = v;
+            mine = q == u ? v : mine;
         }
+        const int j = j0 + q * RPP;
+        if (q < U && j < J) epi(j, mine);
     }
     __syncthreads();
 }
@@ -127,11 +132,11 @@ __device__ __forceinline__ void act_fd(int act, float w0, float t, float& h, flo
 
 // LDS layout of one row's evaluation (floats, every block a multiple of 4: 16-byte aligned)
 struct RowLds {
-    float *e, *gm, *z, *hz, *h1, *d1, *h2, *d2, *h3, *d3, *h4, *d4, *ge3, *ge1, *gz, *red;
+    float *e, *gm, *z, *hz, *h1, *d1, *h2, *d2, *h3, *d3, *h4, *d4, *ge3, *ge1, *red;
 };
 __host__ __device__ inline int r4(int n) { return (n + 3) & ~3; }
 __host__ __device__ inline size_t row_lds_floats(const WideRowArgs& a) {
-    return 2 * (size_t)r4(a.NEK) + 2 * (size_t)a.LZ + (a.P1 + a.P3) + 2 * (size_t)(a.P1 + a.P2 + a.P3 + a.P4) +
+    return 2 * (size_t)r4(a.NEK) + (size_t)a.LZ + (a.P1 + a.P3) + 2 * (size_t)(a.P1 + a.P2 + a.P3 + a.P4) +
            2 * (size_t)a.NEB + 8;
 }
 __device__ inline RowLds carve(float* q, const WideRowArgs& a) {
@@ -140,7 +145,7 @@ __device__ inline RowLds carve(float* q, const WideRowArgs& a) {
     s.e = take(a.NEK); s.gm = take(a.NEK); s.z = take(a.LZ); s.hz = take(a.P1 + a.P3);
     s.h1 = take(a.P1); s.d1 = take(a.P1); s.h2 = take(a.P2); s.d2 = take(a.P2);
     s.h3 = take(a.P3); s.d3 = take(a.P3); s.h4 = take(a.P4); s.d4 = take(a.P4);
-    s.ge3 = take(a.NEB); s.ge1 = take(a.NEB); s.gz = take(a.LZ); s.red = take(8);
+    s.ge3 = take(a.NEB); s.ge1 = take(a.NEB); s.red = take(8);
     return s;
 }
 
@@ -169,28 +174,23 @@ __device__ __forceinline__ void row_eval_wide(const WideRowArgs& A, const int r,
         s.gm[m] = g;
     }
     for (int k = tix(); k < A.LZ; k += WT) s.z[k] = k < A.LH ? A.latent[(size_t)r * A.LH + k] : 0.0f;
+    if (!A.e3)
+        for (int m = tix(); m < A.NEB; m += WT) s.ge3[m] = 0.0f;
     __syncthreads();
-    // ---- the latent's share of layers 1 and 3: hz = [W1z ; W3z] z + [b1 | b3] (the wide schedule's hoist)
-    gemv(A.Hz, A.P1 + A.P3, s.z, A.LZ, nullptr, 0, s.hz);
-    // ---- forward
-    gemv(A.F1, A.P1, s.e, A.NEK, nullptr, 0, s.h1);
-    for (int j = tix(); j < A.P1; j += WT) act_fd(act, w0, s.h1[j] + (s.hz[j] + A.bz[j]), s.h1[j], s.d1[j]);
-    __syncthreads();
-    gemv(A.F2, A.P2, s.h1, A.P1, nullptr, 0, s.h2);
-    for (int j = tix(); j < A.P2; j += WT) act_fd(act, w0, s.h2[j] + A.b2[j], s.h2[j], s.d2[j]);
-    __syncthreads();
-    gemv(A.F3, A.P3, s.h2, A.P2, A.e3 ? s.e : nullptr, A.e3 ? A.NEK : 0, s.h3);
-    for (int j = tix(); j < A.P3; j += WT)
-        act_fd(act, w0, s.h3[j] + (s.hz[A.P1 + j] + A.bz[A.P1 + j]), s.h3[j], s.d3[j]);
-    __syncthreads();
-    gemv(A.F4, A.P4, s.h3, A.P3, nullptr, 0, s.h4);
-    for (int j = tix(); j < A.P4; j += WT) {
+    // ---- the latent's share of layers 1 and 3: hz = [W1z ; W3z] z + [b1 | b3] (the wide schedule's hoist:
+    //      its STORE epilogue, acc + bias)
+    gemv(A.Hz, A.P1 + A.P3, s.z, A.LZ, nullptr, 0, [&](int j, float v) { s.hz[j] = v + A.bz[j]; });
+    // ---- forward, the activation (and its derivative factor) in each GEMV's epilogue
+    gemv(A.F1, A.P1, s.e, A.NEK, nullptr, 0, [&](int j, float v) { act_fd(act, w0, v + s.hz[j], s.h1[j], s.d1[j]); });
+    gemv(A.F2, A.P2, s.h1, A.P1, nullptr, 0, [&](int j, float v) { act_fd(act, w0, v + A.b2[j], s.h2[j], s.d2[j]); });
+    gemv(A.F3, A.P3, s.h2, A.P2, A.e3 ? s.e : nullptr, A.e3 ? A.NEK : 0,
+         [&](int j, float v) { act_fd(act, w0, v + s.hz[A.P1 + j], s.h3[j], s.d3[j]); });
+    gemv(A.F4, A.P4, s.h3, A.P3, nullptr, 0, [&](int j, float v) {
         float h, d;
-        act_fd(act, w0, s.h4[j] + A.b4[j], h, d);
+        act_fd(act, w0, v + A.b4[j], h, d);
         s.h4[j] = h;
         s.d4[j] = act == 0 ? (A.w5[j] * d) * w0 : A.w5[j] * d;  // delta4 (wide_gemm's SIN_L4 epilogue)
-    }
-    __syncthreads();
+    });
     if (wave == 0) {  // df = w5 . h4 + b5
         float v = 0.0f;
         for (int n = lane; n < A.P4; n += 64) v = fmaf(A.w5[n], s.h4[n], v);
@@ -200,29 +200,21 @@ __device__ __forceinline__ void row_eval_wide(const WideRowArgs& A, const int r,
     }
     // ---- backward: delta_{l-1} = (W_l^T delta_l) * act'(a_{l-1}) (* w0 for sin): torch's SinBackward then
     //      MulBackward, as wide_gemm's BWD epilogue; deltas overwrite the consumed activations
-    gemv(A.B4, A.P3, s.d4, A.P4, nullptr, 0, s.h3);
-    for (int j = tix(); j < A.P3; j += WT) {
-        const float dd = s.h3[j] * s.d3[j];
-        s.h3[j] = act == 0 ? dd * w0 : dd;
-    }
-    __syncthreads();
-    gemv(A.B3h, A.P2, s.h3, A.P3, nullptr, 0, s.h2);
-    gemv(A.B3e, A.NEB, s.h3, A.P3, nullptr, 0, s.ge3);  // zero rows unless layer 3 sees the embedding
-    for (int j = tix(); j < A.P2; j += WT) {
-        const float dd = s.h2[j] * s.d2[j];
-        s.h2[j] = act == 0 ? dd * w0 : dd;
-    }
-    __syncthreads();
-    gemv(A.B2, A.P1, s.h2, A.P2, nullptr, 0, s.h1);
-    for (int j = tix(); j < A.P1; j += WT) {
-        const float dd = s.h1[j] * s.d1[j];
-        s.h1[j] = act == 0 ? dd * w0 : dd;
-    }
-    __syncthreads();
-    gemv(A.B1e, A.NEB, s.h1, A.P1, nullptr, 0, s.ge1);
+    auto bwd = [&](float* dl, const float* dv) {
+        return [=](int j, float v) {
+            const float dd = v * dv[j];
+            dl[j] = act == 0 ? dd * w0 : dd;
+        };
+    };
+    gemv(A.B4, A.P3, s.d4, A.P4, nullptr, 0, bwd(s.h3, s.d3));
+    gemv(A.B3h, A.P2, s.h3, A.P3, nullptr, 0, bwd(s.h2, s.d2));
+    if (A.e3)  // res 'latent' / 'none': layer 3 does not see the embedding (ge3 zeroed with the embedding)
+        gemv(A.B3e, A.NEB, s.h3, A.P3, nullptr, 0, [&](int j, float v) { s.ge3[j] = v; });
+    gemv(A.B2, A.P1, s.h2, A.P2, nullptr, 0, bwd(s.h1, s.d1));
+    gemv(A.B1e, A.NEB, s.h1, A.P1, nullptr, 0, [&](int j, float v) { s.ge1[j] = v; });
     if (A.grad_latent) {  // d df / d z = [delta1 | delta3] . [W1z ; W3z]
-        gemv(A.Bz, A.LZ, s.h1, A.P1, s.h3, A.P3, s.gz);
-        for (int k = tix(); k < A.LH; k += WT) A.grad_latent[(size_t)r * A.LH + k] = s.gz[k];
+        float* gl = A.grad_latent + (size_t)r * A.LH;
+        gemv(A.Bz, A.LH, s.h1, A.P1, s.h3, A.P3, [&](int j, float v) { gl[j] = v; });
     }
     // ---- d df / d pos through the embedding (wide_final_kernel's sums, by one wave)
     if (wave == 0) {

@@ -7,7 +7,7 @@ R=$(cd "$(dirname "$0")/.." && pwd)
 O=$R/_build/$name
 mkdir -p $O
 cd $R/sdf-nmpc_amd/csrc
-for f in sdf_mlp sdf_wide linearize rti_qp rti_qp_seg ref_pack vae_enc sdf_row solver; do
+for f in sdf_mlp sdf_wide linearize rti_qp rti_qp_seg ref_pack vae_enc sdf_row sdf_row_wide solver; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wno-unused-function -mllvm -amdgpu-mfma-vgpr-form "$@" -c $f.hip -o $O/$f.o &
 done
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 "$@" -c engine.cpp -o $O/engine.o &

@@ -42,10 +42,13 @@ def main():
         os.environ["SDFNMPC_WIDE_ROW_MAX_MB"] = "0"
         net_l = _lib.Net.from_blob(ctx, blob)
         del os.environ["SDFNMPC_WIDE_ROW_MAX_MB"]
+        ctx.sdf_server_stats()
         srv = per_call(ctx, net, xs, True)
+        st = ctx.sdf_server_stats()
         launch = per_call(ctx, net, xs, False)
         layers = per_call(ctx, net_l, xs, False, n=500)
-        print(f"{name}: server {srv:.2f} us, row launch {launch:.2f} us, layer-by-layer {layers:.2f} us per call",
+        print(f"{name}: server {srv:.2f} us, row launch {launch:.2f} us, layer-by-layer {layers:.2f} us per call; "
+              f"server evaluation {st['eval_us']:.2f} us, staging {st['stage_us']:.2f} us, wait {st['wait_us']:.2f} us",
               flush=True)
         net.close()
         net_l.close()
