@@ -24,7 +24,7 @@ L4C_PATH = os.path.join(LIB_DIR, "libsdf_l4c.so")
 SYMBOLS = [
     "sdfnmpc_abi_version", "sdfnmpc_last_error", "sdfnmpc_ctx_create", "sdfnmpc_ctx_destroy",
     "sdfnmpc_ctx_set_stream", "sdfnmpc_ctx_use_null_stream", "sdfnmpc_ctx_stream", "sdfnmpc_ctx_synchronize", "sdfnmpc_ctx_set_tile_rows",
-    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_set_sdf_server", "sdfnmpc_ctx_sdf_server_stats", "sdfnmpc_ctx_qp_kernel", "sdfnmpc_qp_lds_bytes", "sdfnmpc_qp_capacity", "sdfnmpc_qp_capacity_for",
+    "sdfnmpc_ctx_set_qp_kernel", "sdfnmpc_ctx_set_sdf_server", "sdfnmpc_ctx_sdf_server_stats", "sdfnmpc_ctx_qp_kernel", "sdfnmpc_ctx_qp_kernel_for", "sdfnmpc_qp_lds_bytes", "sdfnmpc_qp_capacity", "sdfnmpc_qp_capacity_for",
     "sdfnmpc_ctx_enable_timing", "sdfnmpc_ctx_kernel_stats", "sdfnmpc_ctx_reset_stats", "sdfnmpc_net_load",
     "sdfnmpc_net_load_file", "sdfnmpc_net_siren", "sdfnmpc_net_free", "sdfnmpc_net_max_df",
     "sdfnmpc_net_size_latent", "sdfnmpc_net_fingerprint", "sdfnmpc_sdf_eval", "sdfnmpc_sdf_eval_host",
@@ -138,6 +138,7 @@ def load():
         "sdfnmpc_ctx_set_sdf_server": (i, [vp, i]),
         "sdfnmpc_ctx_sdf_server_stats": (i, [vp, P(d)]),
         "sdfnmpc_ctx_qp_kernel": (i, [vp, i, i]),
+        "sdfnmpc_ctx_qp_kernel_for": (i, [vp, i, i, P(QpOptsC)]),
         "sdfnmpc_qp_lds_bytes": (C.c_longlong, [i]),
         "sdfnmpc_qp_capacity": (C.c_longlong, [vp, i]),
         "sdfnmpc_qp_capacity_for": (C.c_longlong, [vp, i, P(QpOptsC)]),
@@ -257,9 +258,11 @@ class Context:
         return {"stage_us": o[0], "eval_us": o[1], "wait_us": o[2], "requests": int(o[3]),
                 "phases_us": [round(v, 2) for v in o[4:18]]}
 
-    def qp_kernel(self, N: int, B: int) -> str:
-        """The kernel a QP batch of B instances at horizon N runs ('serial' or 'segmented')."""
-        k = load().sdfnmpc_ctx_qp_kernel(self.h, N, B)
+    def qp_kernel(self, N: int, B: int, opts: "QpOptsC" = None) -> str:
+        """The kernel a QP batch of B instances at horizon N runs ('serial' or 'segmented'); with opts: for that
+        constraint set (sdfnmpc_ctx_qp_kernel_for)."""
+        lib = load()
+        k = lib.sdfnmpc_ctx_qp_kernel(self.h, N, B) if opts is None else lib.sdfnmpc_ctx_qp_kernel_for(self.h, N, B, C.byref(opts))
         return {1: "serial", 2: "segmented"}.get(k, "invalid")
 
     def qp_capacity(self, N: int, opts: "QpOptsC" = None) -> int:

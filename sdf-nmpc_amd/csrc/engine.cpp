@@ -333,25 +333,30 @@ extern "C" int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel) {
     return SDFNMPC_OK;
 }
 
+static int qp_cset_check(const sdfnmpc_qp_opts* o);
+static QpRows qp_rows_of(const sdfnmpc_qp_opts* o);
+
 // AUTO: the segmented kernel for latency-sized batches of long horizons (B <= SDFNMPC_QP_SEG_AUTO_MAX_B,
 // N >= SDFNMPC_QP_SEG_AUTO_MIN_N; one workgroup of four wavefronts per instance: 8-10 % lower latency than
 // the serial kernel at N = 40, 24 % at N = 60, equal at N = 30, 30 % slower at N = 20 where the three
 // couplings outweigh five-node segments), the serial one otherwise (one wavefront per instance: at
 // B = 1024 it fills every SIMD once and is 1.6x faster than four wavefronts per instance)
-// the segmented kernel covers the default row set only (h = [hfov, vfov, sdf] soft at every node, the
-// terminal rows the stage rows' copies: qp_is_default_set); any other constraint set runs on the serial kernel
-static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, bool default_set) {
-    if (!default_set) return (ctx && N >= 1 && B >= 0) ? SDFNMPC_QP_SERIAL : -1;
+// the segmented kernel covers the soft row sets whose terminal rows are the stage rows' copies (qp_is_seg_set:
+// the default h = [hfov, vfov, sdf], lidar, no_vfov, no_sdf_constraint, sdf_cost_only, no_sdf ...); any other
+// constraint set (hard rows, rec_feas / stability terminal rows) runs on the serial kernel
+static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, bool seg_set) {
+    if (!seg_set) return (ctx && N >= 1 && B >= 0) ? SDFNMPC_QP_SERIAL : -1;
     return sdfnmpc_ctx_qp_kernel(ctx, N, B);
 }
-// exactly the default row set (qp_default_rows): the segmented kernel reads the stage bounds / weights for
-// the terminal rows and h[N][0..2] as their values, so a set whose terminal rows differ in any
-// field -- columns, hE terms, bounds, weights -- is not it.  T: sdfnmpc_qp_opts or QpArgs (same field names)
+// a row set the segmented kernel serves: nh soft stage rows and, at the terminal node, the same rows -- it
+// reads the stage bounds / weights for the terminal rows and h[N][h_col[j]] as their values, so a
+// set whose terminal rows differ in any field (columns, hE terms, bounds, weights, hardness) is not one.
+// T: sdfnmpc_qp_opts or QpArgs (same field names)
 template <class T>
-static bool qp_is_default_set(const T& o) {
-    if (o.nh != 3 || o.nhs != 0 || o.nhN != 3 || o.nsN != 3) return false;
-    for (int j = 0; j < 3; ++j)
-        if (o.h_col[j] != j || o.hN_col[j] != j || o.hE_col[j] != -1 || o.lhN[j] != o.lh[j] || o.uhN[j] != o.uh[j] ||
+static bool qp_is_seg_set(const T& o) {
+    if (o.nh < 0 || o.nh > 3 || o.nhs != 0 || o.nhN != o.nh || o.nsN != o.nh) return false;
+    for (int j = 0; j < o.nh; ++j)
+        if (o.hN_col[j] != o.h_col[j] || o.hE_col[j] != -1 || o.lhN[j] != o.lh[j] || o.uhN[j] != o.uh[j] ||
             o.zlN[j] != o.zl[j] || o.ZlN[j] != o.Zl[j])
             return false;
     return true;
@@ -368,6 +373,11 @@ extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B) {
     return (B <= max_b && N >= SDFNMPC_QP_SEG_AUTO_MIN_N) ? SDFNMPC_QP_SEGMENTED : SDFNMPC_QP_SERIAL;
 }
 
+extern "C" int sdfnmpc_ctx_qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, const sdfnmpc_qp_opts* o) {
+    if (o && qp_cset_check(o)) return -1;
+    return qp_kernel_for(ctx, N, B, o ? qp_is_seg_set(*o) : true);
+}
+
 extern "C" long long sdfnmpc_qp_lds_bytes(int N) {
     return N < 1 ? -1 : (long long)qp_lds_bytes(N);
 }
@@ -375,8 +385,6 @@ extern "C" long long sdfnmpc_qp_lds_bytes(int N) {
 // Instances the context's device solves in one wave of QP workgroups: every CU holds as many
 // instances as its LDS fits (the QP keeps each instance's iterate, duals and record window in LDS;
 // rti_qp.hip: one 64-lane workgroup per instance, rti_qp_seg.hip: one workgroup of NSEG waves).
-static int qp_cset_check(const sdfnmpc_qp_opts* o);
-static QpRows qp_rows_of(const sdfnmpc_qp_opts* o);
 
 extern "C" long long sdfnmpc_qp_capacity(const sdfnmpc_ctx* ctx, int N) { return sdfnmpc_qp_capacity_for(ctx, N, nullptr); }
 
@@ -386,7 +394,7 @@ extern "C" long long sdfnmpc_qp_capacity_for(const sdfnmpc_ctx* ctx, int N, cons
     if (o && qp_cset_check(o)) return -1;
     const QpRows rows = o ? qp_rows_of(o) : qp_rows_default();
     // a batch that fills the device: the kernel AUTO picks above SDFNMPC_QP_SEG_AUTO_MAX_B
-    const bool seg = qp_kernel_for(ctx, N, 1 << 30, o ? qp_is_default_set(*o) : true) == SDFNMPC_QP_SEGMENTED;
+    const bool seg = qp_kernel_for(ctx, N, 1 << 30, o ? qp_is_seg_set(*o) : true) == SDFNMPC_QP_SEGMENTED;
     const size_t per = seg ? qp_seg_lds_bytes(N) : qp_lds_bytes(N, rows);
     if (per == 0 || per > ctx->lds_per_cu) return 0;  // the horizon does not fit one CU's LDS
     // the runtime's occupancy of the kernel (LDS, registers and waves at once): the serial kernel's 375
@@ -1551,7 +1559,7 @@ static int qp_build(sdfnmpc_ctx* ctx, const sdfnmpc_qp_opts* o, const sdfnmpc_qp
     q.lm_scaling = o->lm_scaling;
     q.warm_start = o->warm_start ? 1 : 0;
     q.nh = o->nh; q.nhN = o->nhN; q.nsN = o->nsN; q.nyN = o->nyN; q.nhs = o->nhs;
-    q.default_rows = qp_is_default_set(*o) ? 1 : 0;
+    q.seg_rows = qp_is_seg_set(*o) ? 1 : 0;
     q.sdf_row = -1;
     for (int j = 0; j < 3; ++j) {
         q.h_col[j] = j < o->nh ? o->h_col[j] : 0;
@@ -1580,7 +1588,7 @@ static long long cset_key(const QpArgs& q) {
 // the IPM kernel of this context and horizon: the segmented one (four wavefronts per instance,
 // rti_qp_seg.hip) where it supports N, unless the context asks for the serial one (rti_qp.hip)
 static hipError_t qp_launch(sdfnmpc_ctx* ctx, const QpArgs& q) {
-    if (qp_kernel_for(ctx, q.N, q.B, q.default_rows != 0) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
+    if (qp_kernel_for(ctx, q.N, q.B, q.seg_rows != 0) == SDFNMPC_QP_SEGMENTED) return launch_rti_qp_seg(q, ctx->stream);
     return launch_rti_qp(q, ctx->stream);
 }
 

@@ -38,12 +38,12 @@ struct QpArgs {
     int sdf_row_patch;  // rti_qp_kernel: copy J_h[.][2] into the records' C^T row 2 before the sweeps
     int warm_start;     // 1: the IPM starts from the du found in du on entry (qp_solver_warm_start, ocp.py:116)
     int nhs;            // hard stage rows: the last nhs of the nh (slack weight None, base_model.py:142-155)
-    int default_rows;   // 1: exactly qp_default_rows' set (the segmented kernel's only one)
+    int seg_rows;       // 1: a row set the segmented kernel serves (soft rows only, terminal = stage rows)
 };
 
 // the default constraint set (h = [hfov, vfov, sdf] at every node, soft) from lh .. Zl (diagnostic drivers)
 inline void qp_default_rows(QpArgs& q) {
-    q.nh = 3; q.nhN = 3; q.nsN = 3; q.nyN = 4; q.sdf_row = 2; q.nhs = 0; q.default_rows = 1;
+    q.nh = 3; q.nhN = 3; q.nsN = 3; q.nyN = 4; q.sdf_row = 2; q.nhs = 0; q.seg_rows = 1;
     for (int j = 0; j < 3; ++j) {
         q.h_col[j] = j; q.zlN[j] = q.zl[j]; q.ZlN[j] = q.Zl[j];
     }

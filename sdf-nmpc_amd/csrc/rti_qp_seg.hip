@@ -244,7 +244,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     // where each one held a 64-bit SGPR mask for the whole kernel and the masks spilled to VGPR lanes.
     const int lane_k = lane;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int N = A.N, N1 = N + 1, m = 8 * N + 12 * N1;
+    // soft row sets only: nh (0..3) stage rows at every node, the terminal rows the stage rows' copies
+    // (engine.cpp qp_is_seg_set); group j < nh of a node reads column h_col[j] of h / J_h
+    const int nh = A.nh;
+    const int N = A.N, N1 = N + 1, m = 8 * N + 4 * nh * N1;
     const SegSmem s = seg_carve<NSEG, NMAX>((ldsd*)lds_q, w);
     ldsd* const win = s.win;                                  // two windows; the coupling's scratch
     const int sa = w * N1 / NSEG, sb = (w + 1) * N1 / NSEG;  // this wave's nodes [sa, sb)
@@ -279,10 +282,15 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         s.cst[tid] = v;
     }
     if (tid < 48) s.zero[tid] = 0.0;
+    // folds of every group: the groups past nh keep (0, 0) (their C^T rows are zero rows of the record)
+    for (int e = tid; e < N1 * NS; e += 64 * NSEG) {
+        s.fw[e] = 0.0;
+        s.fg[e] = 0.0;
+    }
     if (A.sdf_row_patch) {  // records packed beside the SDF kernel (pack_part 1): their sdf row of C^T
         for (int e = lane; e < (sb - sa) * NX; e += 64) {
             const int k = sa + e / NX, l = e % NX;
-            Rw[(size_t)k * REC + R_CT + 20 + l] = A.Jh[((size_t)b * N1 + k) * 30 + l * 3 + 2];
+            Rw[(size_t)k * REC + R_CT + 10 * A.sdf_row + l] = A.Jh[((size_t)b * N1 + k) * 30 + l * 3 + 2];
         }
     }
     // [c | g | B | C^T] of the stage record into the factor record (R[100, 194) is [B | c | g | C^T])
@@ -294,10 +302,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     // lane-owned rows: box pair (kb, ib) (rows 8 kb + ib, 8 kb + 4 + ib), soft group (ks, js) (rows
     // 8 N + 12 ks + 4 js + q) of this wave's nodes
     const int kb = sa + (lane >> 2), ib = lane & 3, ks = sa + lane / 3, js = lane % 3;
-    const bool ownb = kb < (sb < N ? sb : N), owns = ks < sb;
+    const bool ownb = kb < (sb < N ? sb : N), owns = ks < sb && js < nh;
     const int kbc = ownb ? kb : sa, ksc = owns ? ks : sa;
     const double ubv = ownb ? A.u[((size_t)b * N + kbc) * NU + ib] : 0.0;
-    const double hsv = owns ? A.h[((size_t)b * N1 + ksc) * NS + js] : 0.0;
+    const double hsv = owns ? A.h[((size_t)b * N1 + ksc) * NS + A.h_col[js]] : 0.0;
     if (tid < NX) s.dxc[tid] = A.x0[(size_t)b * 10 + tid] - A.x[(size_t)b * N1 * 10 + tid];
     // du of the start iterate into dua (free until the first forward sweep): 0, or on a primal warm start
     // the previous QP's du as found in A.du (qp_solver_warm_start, ocp.py:116)
@@ -1384,9 +1392,9 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     }
     SSTAMP_OUT
     // ------------------------------------------------------------ outputs
-    if (A.slack && owns) {
-        A.slack[((size_t)b * N1 * NS + ksc * NS + js) * 2] = ts[2];
-        A.slack[((size_t)b * N1 * NS + ksc * NS + js) * 2 + 1] = ts[3];
+    if (A.slack && ks < sb) {  // [N+1][3][2], zero past the nh rows (rti_qp.hip's layout)
+        A.slack[((size_t)b * N1 * NS + ks * NS + js) * 2] = owns ? ts[2] : 0.0;
+        A.slack[((size_t)b * N1 * NS + ks * NS + js) * 2 + 1] = owns ? ts[3] : 0.0;
     }
     if (tid == 0) {
         A.iters[b] = it;

