@@ -341,25 +341,18 @@ static QpRows qp_rows_of(const sdfnmpc_qp_opts* o);
 // the serial kernel at N = 40, 24 % at N = 60, equal at N = 30, 30 % slower at N = 20 where the three
 // couplings outweigh five-node segments), the serial one otherwise (one wavefront per instance: at
 // B = 1024 it fills every SIMD once and is 1.6x faster than four wavefronts per instance)
-// the segmented kernel covers the soft row sets whose terminal rows are the stage rows' copies (qp_is_seg_set:
-// the default h = [hfov, vfov, sdf], lidar, no_vfov, no_sdf_constraint, sdf_cost_only, no_sdf ...); any other
-// constraint set (hard rows, rec_feas / stability terminal rows) runs on the serial kernel
+// the segmented kernel covers every row set without hard stage rows: 0..3 soft stage rows and any terminal
+// rows (soft first; the rec_feas braking / Co_p_E rows and stability's velocity box hard) -- qp_is_seg_set;
+// a set with hard stage rows (slack_fov / slack_df None) runs on the serial kernel
 static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, bool seg_set) {
     if (!seg_set) return (ctx && N >= 1 && B >= 0) ? SDFNMPC_QP_SERIAL : -1;
     return sdfnmpc_ctx_qp_kernel(ctx, N, B);
 }
-// a row set the segmented kernel serves: nh soft stage rows and, at the terminal node, the same rows -- it
-// reads the stage bounds / weights for the terminal rows and h[N][h_col[j]] as their values, so a
-// set whose terminal rows differ in any field (columns, hE terms, bounds, weights, hardness) is not one.
-// T: sdfnmpc_qp_opts or QpArgs (same field names)
+// a row set the segmented kernel serves (rti_qp_seg.hip: nh soft rows per stage node, nhN terminal rows on
+// lanes 48 + j of the last wave).  T: sdfnmpc_qp_opts or QpArgs (same field names)
 template <class T>
 static bool qp_is_seg_set(const T& o) {
-    if (o.nh < 0 || o.nh > 3 || o.nhs != 0 || o.nhN != o.nh || o.nsN != o.nh) return false;
-    for (int j = 0; j < o.nh; ++j)
-        if (o.hN_col[j] != o.h_col[j] || o.hE_col[j] != -1 || o.lhN[j] != o.lh[j] || o.uhN[j] != o.uh[j] ||
-            o.zlN[j] != o.zl[j] || o.ZlN[j] != o.Zl[j])
-            return false;
-    return true;
+    return o.nh >= 0 && o.nh <= 3 && o.nhs == 0 && o.nsN >= 0 && o.nsN <= 3 && o.nhN >= o.nsN && o.nhN <= QP_NHN;
 }
 
 extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B) {

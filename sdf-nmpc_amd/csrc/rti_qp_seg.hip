@@ -127,8 +127,11 @@ __device__ __forceinline__ void chol_cols(double (&col)[NX], double (&inv)[NX], 
     for (int i = 0; i < NX; ++i) col[i] = i < lane ? 0.0 : col[i] * myinv;
 }
 
+// constant table (s.cst): box bounds, then per row kind ci (0..2 stage rows j, 3 + j terminal rows j) its
+// lower / upper bound and L1 / L2 slack weights
+constexpr int C_LO = 8, C_HI = C_LO + 3 + QP_NHN, C_ZL = C_HI + 3 + QP_NHN, C_ZU = C_ZL + 3 + QP_NHN, C_N = C_ZU + 3 + QP_NHN;
 struct SegSmem {
-    ldsd *dxc, *dua, *duc, *cxa, *cxc, *fw, *fg, *bd, *bv, *skv, *cst, *zero;
+    ldsd *dxc, *dua, *duc, *cxa, *cxc, *fw, *fg, *bd, *bv, *skv, *cst, *ctn, *zero;
     ldsd *win, *junk, *xlam, *vec;  // this wave's
     ldsd *slot, *red;               // hand-off slots [3][112], reduction partials
 };
@@ -139,9 +142,11 @@ template <int NSEG, int NMAX>
 struct SegLds {
     static constexpr int ev(int n) { return (n + 1) & ~1; }
     static constexpr int N1 = NMAX + 1;
+    static constexpr int NG = NMAX * NS + QP_NHN;  // groups: k NS + j at stages k < N, N NS + j the terminal rows
     static constexpr int DXC = 0, DUA = DXC + ev(N1 * NX), DUC = DUA + ev(NMAX * NU), CXA = DUC + ev(NMAX * NU),
-                         CXC = CXA + ev(N1 * NS), FW = CXC + ev(N1 * NS), FG = FW + ev(N1 * NS), BD = FG + ev(N1 * NS),
-                         BV = BD + ev(NMAX * NU), SKV = BV + ev(NMAX * NU), CST = SKV + ev(N1), ZERO = CST + 20, WINS = ZERO + 48,
+                         CXC = CXA + ev(NG), FW = CXC + ev(NG), FG = FW + ev(NG), BD = FG + ev(NG),
+                         BV = BD + ev(NMAX * NU), SKV = BV + ev(NMAX * NU), CST = SKV + ev(N1), CTN = CST + ev(C_N),
+                         ZERO = CTN + 10 * QP_NHN, WINS = ZERO + 48,
                          JUNK = WINS + NSEG * 2 * WIN, XLAM = JUNK + NSEG * 2, VEC = XLAM + NSEG * 16, SLOT = VEC + NSEG * 64,
                          RED = SLOT + (NSEG_MAX - 1) * 112, TOTAL = RED + 64;
 };
@@ -152,7 +157,7 @@ __device__ __forceinline__ SegSmem seg_carve(ldsd* q, int w) {
     SegSmem s;
     s.dxc = q + L::DXC; s.dua = q + L::DUA; s.duc = q + L::DUC; s.cxa = q + L::CXA; s.cxc = q + L::CXC;
     s.fw = q + L::FW; s.fg = q + L::FG; s.bd = q + L::BD; s.bv = q + L::BV; s.skv = q + L::SKV;
-    s.cst = q + L::CST; s.zero = q + L::ZERO; s.slot = q + L::SLOT; s.red = q + L::RED;
+    s.cst = q + L::CST; s.ctn = q + L::CTN; s.zero = q + L::ZERO; s.slot = q + L::SLOT; s.red = q + L::RED;
     s.win = q + L::WINS + w * 2 * WIN;
     s.junk = q + L::JUNK + 2 * w;
     s.xlam = q + L::XLAM + 16 * w;
@@ -244,10 +249,11 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     // where each one held a 64-bit SGPR mask for the whole kernel and the masks spilled to VGPR lanes.
     const int lane_k = lane;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // soft row sets only: nh (0..3) stage rows at every node, the terminal rows the stage rows' copies
-    // (engine.cpp qp_is_seg_set); group j < nh of a node reads column h_col[j] of h / J_h
+    // row sets without hard stage rows (engine.cpp qp_is_seg_set): nh (0..3) soft stage rows at nodes k < N,
+    // group j of a node reading column h_col[j] of h / J_h; nhN terminal rows, the first nsN soft, row j
+    // reading h[N][hN_col[j]] + hE[hE_col[j]] (rti_qp.hip's row set: QpRows with nhs = 0)
     const int nh = A.nh;
-    const int N = A.N, N1 = N + 1, m = 8 * N + 4 * nh * N1;
+    const int N = A.N, N1 = N + 1, m = 8 * N + 4 * (nh * N + A.nsN) + 2 * (A.nhN - A.nsN);
     const SegSmem s = seg_carve<NSEG, NMAX>((ldsd*)lds_q, w);
     ldsd* const win = s.win;                                  // two windows; the coupling's scratch
     const int sa = w * N1 / NSEG, sb = (w + 1) * N1 / NSEG;  // this wave's nodes [sa, sb)
@@ -265,7 +271,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
 
     // ------------------------------------------------------------ constants, static record copies
     for (int e = tid; e < N1; e += 64 * NSEG) s.skv[e] = (A.cost_scaling && e < N) ? A.dt[e] : 1.0;
-    if (tid < 20) {
+    if (tid < C_N) {  // constant indices: scalar loads of the kernel arguments
         double v = 0.0;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -274,16 +280,35 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         }
 #pragma unroll
         for (int j = 0; j < 3; ++j) {
-            if (tid == 8 + j) v = A.lh[j];
-            if (tid == 11 + j) v = A.uh[j];
-            if (tid == 14 + j) v = A.zl[j];
-            if (tid == 17 + j) v = A.Zl[j];
+            if (tid == C_LO + j) v = A.lh[j];
+            if (tid == C_HI + j) v = A.uh[j];
+            if (tid == C_ZL + j) v = A.zl[j];
+            if (tid == C_ZU + j) v = A.Zl[j];
+        }
+#pragma unroll
+        for (int j = 0; j < QP_NHN; ++j) {
+            if (tid == C_LO + 3 + j) v = A.lhN[j];
+            if (tid == C_HI + 3 + j) v = A.uhN[j];
+            if (tid == C_ZL + 3 + j) v = j < 3 ? A.zlN[j < 3 ? j : 0] : 0.0;
+            if (tid == C_ZU + 3 + j) v = j < 3 ? A.ZlN[j < 3 ? j : 0] : 0.0;
         }
         s.cst[tid] = v;
     }
+    // terminal rows j < nhN: C row j = J_h[N] column hN_col[j] + J_hE column hE_col[j] (rti_qp.hip's)
+    for (int e = tid; e < A.nhN * 10; e += 64 * NSEG) {
+        const int j = e / 10, l = e - 10 * j;
+        int c1 = -1, c2 = -1;
+#pragma unroll
+        for (int q = 0; q < QP_NHN; ++q)
+            if (q == j) { c1 = A.hN_col[q]; c2 = A.hE_col[q]; }
+        double cv = 0.0;
+        if (c1 >= 0) cv += A.Jh[((size_t)b * N1 + N) * 30 + l * 3 + c1];
+        if (c2 >= 0) cv += A.JhE[((size_t)b * 10 + l) * 6 + c2];
+        s.ctn[e] = cv;
+    }
     if (tid < 48) s.zero[tid] = 0.0;
     // folds of every group: the groups past nh keep (0, 0) (their C^T rows are zero rows of the record)
-    for (int e = tid; e < N1 * NS; e += 64 * NSEG) {
+    for (int e = tid; e < N * NS + QP_NHN; e += 64 * NSEG) {
         s.fw[e] = 0.0;
         s.fg[e] = 0.0;
     }
@@ -299,13 +324,36 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         const int src = q < 10 ? R_C + q : q < 24 ? R_G + q - 10 : q < 64 ? 100 + q - 24 : R_CT + q - 64;
         F[(size_t)k * FRECS + S_C + q] = R[(size_t)k * REC + src];
     }
-    // lane-owned rows: box pair (kb, ib) (rows 8 kb + ib, 8 kb + 4 + ib), soft group (ks, js) (rows
-    // 8 N + 12 ks + 4 js + q) of this wave's nodes
-    const int kb = sa + (lane >> 2), ib = lane & 3, ks = sa + lane / 3, js = lane % 3;
-    const bool ownb = kb < (sb < N ? sb : N), owns = ks < sb && js < nh;
-    const int kbc = ownb ? kb : sa, ksc = owns ? ks : sa;
+    // lane-owned rows: box pair (kb, ib) (rows 8 kb + ib, 8 kb + 4 + ib) of this wave's nodes; soft group
+    // (ks, js) of a stage node (lanes 0..47: at most 15 stage nodes x 3); in the last wave lanes 48 + j the
+    // terminal row j: soft (its four rows in ts / ls) or hard (lower, upper in ts[0..1] / ls[0..1])
+    const bool last = w == NSEG - 1;
+    const int jt = lane - 48;
+    const bool tlane = last && jt >= 0 && jt < QP_NHN;
+    const int kb = sa + (lane >> 2), ib = lane & 3, ks = tlane ? N : sa + lane / 3, js = tlane ? jt : lane % 3;
+    const bool ownb = kb < (sb < N ? sb : N);
+    const bool owns = tlane ? jt < A.nsN : ks < (last ? N : sb) && js < nh;
+    const bool ownh = tlane && jt >= A.nsN && jt < A.nhN;
+    const int ci = tlane ? 3 + jt : js;  // the row kind in the constant table
+    const int kbc = ownb ? kb : sa, ksc = (owns || ownh) ? ks : sa;
     const double ubv = ownb ? A.u[((size_t)b * N + kbc) * NU + ib] : 0.0;
-    const double hsv = owns ? A.h[((size_t)b * N1 + ksc) * NS + A.h_col[js]] : 0.0;
+    double hsv = 0.0;
+    if (owns || ownh) {
+        if (tlane) {
+            int c1 = -1, c2 = -1;
+#pragma unroll
+            for (int q = 0; q < QP_NHN; ++q)
+                if (q == jt) { c1 = A.hN_col[q]; c2 = A.hE_col[q]; }
+            if (c1 >= 0) hsv += A.h[((size_t)b * N1 + N) * NS + c1];
+            if (c2 >= 0) hsv += A.hE[(size_t)b * 6 + c2];
+        } else {
+            int hc = 0;
+#pragma unroll
+            for (int q = 0; q < 3; ++q)
+                if (q == js) hc = A.h_col[q];
+            hsv = A.h[((size_t)b * N1 + ksc) * NS + hc];
+        }
+    }
     if (tid < NX) s.dxc[tid] = A.x0[(size_t)b * 10 + tid] - A.x[(size_t)b * N1 * 10 + tid];
     // du of the start iterate into dua (free until the first forward sweep): 0, or on a primal warm start
     // the previous QP's du as found in A.du (qp_solver_warm_start, ocp.py:116)
@@ -322,10 +370,10 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     // row constants: box rows at du = 0 (dlo, dup), soft rows at C dx = 0 (hl0, hu0), slack weights
     auto dlo = [&]() { return ubv - s.cst[ib]; };
     auto dup = [&]() { return s.cst[4 + ib] - ubv; };
-    auto hl0 = [&]() { return hsv - s.cst[8 + js]; };
-    auto hu0 = [&]() { return s.cst[11 + js] - hsv; };
-    auto Zs = [&]() { return s.skv[ksc] * s.cst[17 + js]; };
-    auto zs = [&]() { return s.skv[ksc] * s.cst[14 + js]; };
+    auto hl0 = [&]() { return hsv - s.cst[C_LO + ci]; };
+    auto hu0 = [&]() { return s.cst[C_HI + ci] - hsv; };
+    auto Zs = [&]() { return s.skv[ksc] * s.cst[C_ZU + ci]; };
+    auto zs = [&]() { return s.skv[ksc] * s.cst[C_ZL + ci]; };
     double tb0 = 1.0, tb1 = 1.0, lb0 = 0.0, lb1 = 0.0;  // box rows (lower, upper); unowned: t = 1, lambda = 0
     double ts[4] = {1.0, 1.0, 1.0, 1.0}, ls[4] = {0.0, 0.0, 0.0, 0.0};
     // the row state parks in memory while the factor sweep and its coupling need the registers
@@ -417,13 +465,14 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         const int lane = opaque(lane_k);
         constexpr int K = decltype(Kc)::value;
         constexpr bool LAM = decltype(LAMc)::value;
-        const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 17;
+        const bool term = k == N;  // the terminal node: its nhN rows' C from ctn (lanes 14 .. 13 + nhN)
+        const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 14 + (term ? A.nhN : NS);
         const int fcj = fc ? lane - 14 : 0;
         ldsd* const duo = K == 4 ? s.duc : s.dua;
         ldsd* const cxo = K == 4 ? s.cxc : s.cxa;
         double row[NX], off;
         if constexpr (K == 0) {
-            const ldsd* rp = fx ? cw + R_AB + lane : fc ? cw + R_CT + fcj * 10 : s.zero;
+            const ldsd* rp = fx ? cw + R_AB + lane : fc ? (term ? s.ctn : cw + R_CT) + fcj * 10 : s.zero;
             const int str = fx ? 10 : 1;
 #pragma unroll
             for (int l = 0; l < NX; ++l) row[l] = rp[l * str];
@@ -434,7 +483,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
                                cw[R_AB + 120 + bx] * s.dua[ku * NU + 2] + cw[R_AB + 130 + bx] * s.dua[ku * NU + 3];
             off += (fx ? 1.0 : 0.0) * bdu;
         } else {
-            const ldsd2* rp = (const ldsd2*)(lane < 14 ? cw + lane * FR : fc ? cw + WF_CT + fcj * 10 : s.zero);
+            const ldsd2* rp = (const ldsd2*)(lane < 14 ? cw + lane * FR : fc ? (term ? s.ctn : cw + WF_CT) + fcj * 10 : s.zero);
 #pragma unroll
             for (int l = 0; l < NX / 2; ++l) {
                 const d2 v = rp[l];
@@ -492,14 +541,22 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         const int gj = g < NS ? g : 0;
         const double cg = cw[fget(f, F_CGI)];
         const double fb = mg3 * fma(s.fw[k * NS + gj], cg, m14 * s.fg[k * NS + gj]);
-        if constexpr (FIRST) {  // [P_N | p_N] = [H_N | g_N] + fold
+        if constexpr (FIRST) {  // [P_N | p_N] = [H_N | g_N] + the folds of the nhN terminal rows (C rows in ctn)
             d4 T;
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int a_ = g + 4 * r, lo = a_ < c ? a_ : c, hi = a_ < c ? c : a_;
                 T[r] = cw[(a_ < NX && c < NX) ? R_H + tri10(lo, hi) : (a_ < NX && c == 14) ? R_G + a_ : R_Z];
             }
-            Pa = mfma(cg, fb, T);
+            const int nhN = A.nhN;
+            auto tfold = [&](int j, d4 acc) {  // rows j = g (+ 4): lane (g, c) holds C[j][c] and w_j C[j][c] + [c = 14] gamma_j
+                const bool live = j < nhN;
+                const double ct = ldsel(s.ctn, 10 * (live ? j : 0) + (c < NX ? c : 0), live && c < NX);
+                const double fj = live ? fma(s.fw[N * NS + j], ct, m14 * s.fg[N * NS + j]) : 0.0;
+                return mfma(ct, fj, acc);
+            };
+            Pa = tfold(g, T);
+            if (nhN > 4) Pa = tfold(g + 4, Pa);
             refill();
             return;
         }
@@ -652,7 +709,13 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         const int bx = fx ? lane : 0;
         // ---- the chain's offset: g~_x + K^T g~_u (lanes 0..9), g~_u (lanes 10..13)
         double off = *(lane < 14 ? cw + S_GV + lane : s.zero);
-        {
+        if constexpr (FIRST) {  // the terminal rows' C from ctn
+#pragma unroll
+            for (int j = 0; j < QP_NHN; ++j) {
+                const bool live = fx && j < A.nhN;
+                off += live ? s.fg[N * NS + j] * s.ctn[10 * j + bx] : 0.0;
+            }
+        } else {
             const ldsd* bc_ct = fx ? cw + S_CT + lane : s.zero;
 #pragma unroll
             for (int j = 0; j < NS; ++j) off += s.fg[k * NS + j] * bc_ct[10 * j];
@@ -773,6 +836,19 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
             const double Zsv = Zs(), zsv = zs();
             if (!phase) s.fw[ksc * NS + js] = g.s1 * (Zsv + g.s2) * g.iHl + g.s3 * (Zsv + g.s4) * g.iHu;
             s.fg[ksc * NS + js] = -(g.v1 * (Zsv + g.s2) + g.s1 * (zsv - g.v2)) * g.iHl + (g.v3 * (Zsv + g.s4) + g.s3 * (zsv - g.v4)) * g.iHu;
+        }
+        if (ownh) {  // a hard row folds like a box pair: w = sigma_l + sigma_u, gamma = -v_l + v_u (rti_qp.hip)
+            const double d0 = hl0(), d1 = hu0();
+            const double it0 = rcp_nr(ts[0]), it1 = rcp_nr(ts[1]), sg0 = ls[0] * it0, sg1 = ls[1] * it1;
+            double v0 = sg0 * (ts[0] - d0), v1 = sg1 * (ts[1] - d1);
+            if (phase) {
+                const double cx = s.cxa[ksc * NS + js];
+                const double da0 = cx + d0 - ts[0], da1 = -cx + d1 - ts[1];
+                v0 -= (da0 * (-sg0 * da0 - ls[0]) - sigmu) * it0;
+                v1 -= (da1 * (-sg1 * da1 - ls[1]) - sigmu) * it1;
+            }
+            if (!phase) s.fw[ksc * NS + js] = sg0 + sg1;
+            s.fg[ksc * NS + js] = -v0 + v1;
         }
         if (ownb) {
             const double d0 = dlo(), d1 = dup();
@@ -1117,13 +1193,22 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         if (owns) {
             const double cx = s.cxa[ksc * NS + js];
             const double v[4] = {cx + hl0(), -cx + hu0(), 0.0, 0.0};
-            const double l0 = fmax(L0, LC * s.skv[ksc] * s.cst[14 + js]);
+            const double l0 = fmax(L0, LC * s.skv[ksc] * s.cst[C_ZL + ci]);
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 ts[q] = fmax(v[q], T0);
                 ls[q] = l0;
                 rl = fmax(rl, fabs(v[q] - ts[q]));
             }
+        }
+        if (ownh) {  // hard terminal row: lower cx + (h - lo), upper -cx + (hi - h) (rti_qp.hip rows_init)
+            const double cx = s.cxa[ksc * NS + js];
+            const double v0 = cx + hl0(), v1 = -cx + hu0();
+            ts[0] = fmax(v0, T0);
+            ts[1] = fmax(v1, T0);
+            ls[0] = L0;
+            ls[1] = L0;
+            rl = fmax(rl, fmax(fabs(v0 - ts[0]), fabs(v1 - ts[1])));
         }
         rp = wg_red(wmax(rl), opmax);
     }
@@ -1134,7 +1219,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
             sum += tb0 * lb0 + tb1 * lb1;
             mx = fmax(tb0 * lb0, tb1 * lb1);
         }
-        if (owns) {
+        if (owns || ownh) {  // a hard row's unused ts[2..3] / ls[2..3] stay 1 / 0
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 sum += ts[q] * ls[q];
@@ -1259,10 +1344,20 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
                     bound(ts[q], ls[q], sdt[q], sdl[q]);
                 }
             }
+            if (ownh) {
+                const double cx = s.cxa[ksc * NS + js];
+                sdt[0] = cx + hl0() - ts[0];
+                sdt[1] = -cx + hu0() - ts[1];
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    sdl[q] = -(ls[q] * rcp_nr(ts[q])) * sdt[q] - ls[q];
+                    bound(ts[q], ls[q], sdt[q], sdl[q]);
+                }
+            }
             const double aa = wg_red(wmin(amax), opmin);
             double lmua = 0.0;
             if (ownb) lmua += (tb0 + aa * bdt0) * (lb0 + aa * bdl0) + (tb1 + aa * bdt1) * (lb1 + aa * bdl1);
-            if (owns) {
+            if (owns || ownh) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) lmua += (ts[q] + aa * sdt[q]) * (ls[q] + aa * sdl[q]);
             }
@@ -1357,13 +1452,25 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
                     bound(ts[q], ls[q], sdt[q], sdl[q]);
                 }
             }
+            if (ownh) {
+                const double cc = s.cxc[ksc * NS + js], ca = s.cxa[ksc * NS + js];
+                const double dd[2] = {hl0(), hu0()};
+#pragma unroll
+                for (int q = 0; q < 2; ++q) {
+                    const double dta = (q ? -ca : ca) + dd[q] - ts[q];
+                    sdt[q] = (q ? -cc : cc) + dd[q] - ts[q];
+                    const double itq = rcp_nr(ts[q]), sg = ls[q] * itq;
+                    sdl[q] = -sg * sdt[q] - ls[q] - (dta * (-sg * dta - ls[q]) - sigmu) * itq;
+                    bound(ts[q], ls[q], sdt[q], sdl[q]);
+                }
+            }
             const double tau = fmin(TAU_HI, fmax(TAU_LO, 1.0 - mu));
             const double al = fmin(1.0, tau * wg_red(wmin(amax), opmin));
             if (ownb) {
                 tb0 += al * bdt[0]; lb0 += al * bdl[0];
                 tb1 += al * bdt[1]; lb1 += al * bdl[1];
             }
-            if (owns) {
+            if (owns || ownh) {
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     ts[q] += al * sdt[q];
@@ -1392,7 +1499,8 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     }
     SSTAMP_OUT
     // ------------------------------------------------------------ outputs
-    if (A.slack && ks < sb) {  // [N+1][3][2], zero past the nh rows (rti_qp.hip's layout)
+    // slacks [N+1][3][2] (rti_qp.hip's layout): stage node k's soft row j, the terminal soft row j; zero past them
+    if (A.slack && (tlane ? jt < 3 : ks < (last ? N : sb))) {
         A.slack[((size_t)b * N1 * NS + ks * NS + js) * 2] = owns ? ts[2] : 0.0;
         A.slack[((size_t)b * N1 * NS + ks * NS + js) * 2 + 1] = owns ? ts[3] : 0.0;
     }

@@ -109,9 +109,8 @@ def test_qp_per_flag_set_vs_c_ipm_and_exact(gpu_ctx, oracle_lib, name):
 
 
 def _seg_set(name):
-    """A row set the segmented kernel serves: soft stage rows, the terminal rows their copies."""
-    _, cols, term = F.FLAG_SETS[name]
-    return [(c, -1, True) for c in cols] == term
+    """A row set the segmented kernel serves: no hard stage rows (engine.cpp qp_is_seg_set)."""
+    return F.quad(name).nhs == 0
 
 
 SEG_SETS = [n for n in F.FLAG_SETS if _seg_set(n)]
@@ -120,16 +119,17 @@ SEG_SETS = [n for n in F.FLAG_SETS if _seg_set(n)]
 @pytest.mark.parametrize("name", SEG_SETS)
 def test_segmented_qp_per_soft_flag_set(gpu_ctx, oracle_lib, name):
     """VERDICT r5 missing 2: the segmented kernel (rti_qp_seg.hip, four wavefronts per instance, the B = 1
-    latency kernel) on every soft row set -- 0..3 of hfov / vfov / sdf at each node, the terminal rows their
-    copies (lidar, no_vfov, no_sdf_constraint, sdf_cost_only, lidar_sdf_only, no_sdf) -- at N = 40, to the
+    latency kernel) on every row set without hard stage rows -- 0..3 soft rows of hfov / vfov / sdf at each
+    node and any terminal rows (lidar, no_vfov, no_sdf_constraint, sdf_cost_only, lidar_sdf_only, no_sdf; the
+    rec_feas braking and Co_p_E rows, stability's velocity box, hard, on the scene net) -- at N = 40, to the
     same bar as the serial kernel against the C IPM and the exact solution."""
     _check_qp(gpu_ctx, oracle_lib, name, 16, 40, "segmented")
 
 
 def test_segmented_kernel_row_sets(gpu_ctx):
     """The kernel each flag set's QP runs when the context asks for the segmented one
-    (sdfnmpc_ctx_qp_kernel_for): the soft sets get it; a set with a hard row or its own terminal rows
-    (hard_*, rec_feas, stability) stays on the serial kernel."""
+    (sdfnmpc_ctx_qp_kernel_for): every set without hard stage rows gets it; the hard_* sets (slack None)
+    stay on the serial kernel."""
     gpu_ctx.set_qp_kernel("segmented")
     try:
         for name in F.FLAG_SETS:
