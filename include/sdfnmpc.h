@@ -245,11 +245,10 @@ int sdfnmpc_ctx_set_qp_kernel(sdfnmpc_ctx* ctx, int kernel);
 /* the kernel a QP batch of B instances at horizon N runs on this context (SDFNMPC_QP_SERIAL or
  * _SEGMENTED; -1 on bad arguments) */
 int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B);
-/* the same for the constraint set of opts (NULL: the default set).  The segmented kernel serves every set
- * without hard stage rows (any 0..3 soft stage rows of hfov / vfov / sdf and any terminal rows: default,
- * lidar, no_vfov, no_sdf_constraint, sdf_cost_only, no_sdf, rec_feas, stability ...); a set with hard stage
- * rows (slack_fov / slack_df None, nhs > 0) runs on the serial kernel whatever the context asks for.
- * Replaces acados' one HPIPM instance per solver (ocp.py:113-120). */
+/* the same for the constraint set of opts (NULL: the default set; -1 on a malformed set).  Both kernels serve
+ * every constraint set sdfnmpc_qp_opts describes (soft / hard stage rows, rec_feas and stability terminal
+ * rows), so the choice is the batch / horizon policy above.  Replaces acados' one HPIPM instance per solver
+ * (ocp.py:113-120). */
 int sdfnmpc_ctx_qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, const sdfnmpc_qp_opts* opts);
 /* LDS bytes one instance of the serial QP kernel holds at horizon N (-1: N < 1) */
 long long sdfnmpc_qp_lds_bytes(int N);

@@ -341,18 +341,18 @@ static QpRows qp_rows_of(const sdfnmpc_qp_opts* o);
 // the serial kernel at N = 40, 24 % at N = 60, equal at N = 30, 30 % slower at N = 20 where the three
 // couplings outweigh five-node segments), the serial one otherwise (one wavefront per instance: at
 // B = 1024 it fills every SIMD once and is 1.6x faster than four wavefronts per instance)
-// the segmented kernel covers every row set without hard stage rows: 0..3 soft stage rows and any terminal
-// rows (soft first; the rec_feas braking / Co_p_E rows and stability's velocity box hard) -- qp_is_seg_set;
-// a set with hard stage rows (slack_fov / slack_df None) runs on the serial kernel
+// the segmented kernel covers every row set the serial one does (qp_is_seg_set: 0..3 stage rows, soft or
+// hard, and up to QP_NHN terminal rows); the choice between them is the batch / horizon policy below
 static int qp_kernel_for(const sdfnmpc_ctx* ctx, int N, int B, bool seg_set) {
     if (!seg_set) return (ctx && N >= 1 && B >= 0) ? SDFNMPC_QP_SERIAL : -1;
     return sdfnmpc_ctx_qp_kernel(ctx, N, B);
 }
-// a row set the segmented kernel serves (rti_qp_seg.hip: nh soft rows per stage node, nhN terminal rows on
-// lanes 48 + j of the last wave).  T: sdfnmpc_qp_opts or QpArgs (same field names)
+// a row set the segmented kernel serves (rti_qp_seg.hip: the stage groups of a node on three lanes, the
+// nhN terminal rows on lanes 48 + j of the last wave).  T: sdfnmpc_qp_opts or QpArgs (same field names)
 template <class T>
 static bool qp_is_seg_set(const T& o) {
-    return o.nh >= 0 && o.nh <= 3 && o.nhs == 0 && o.nsN >= 0 && o.nsN <= 3 && o.nhN >= o.nsN && o.nhN <= QP_NHN;
+    return o.nh >= 0 && o.nh <= 3 && o.nhs >= 0 && o.nhs <= o.nh && o.nsN >= 0 && o.nsN <= 3 && o.nhN >= o.nsN &&
+           o.nhN <= QP_NHN;
 }
 
 extern "C" int sdfnmpc_ctx_qp_kernel(const sdfnmpc_ctx* ctx, int N, int B) {

@@ -38,7 +38,7 @@ struct QpArgs {
     int sdf_row_patch;  // rti_qp_kernel: copy J_h[.][2] into the records' C^T row 2 before the sweeps
     int warm_start;     // 1: the IPM starts from the du found in du on entry (qp_solver_warm_start, ocp.py:116)
     int nhs;            // hard stage rows: the last nhs of the nh (slack weight None, base_model.py:142-155)
-    int seg_rows;       // 1: a row set the segmented kernel serves (no hard stage rows: engine.cpp qp_is_seg_set)
+    int seg_rows;       // 1: a row set the segmented kernel serves (engine.cpp qp_is_seg_set)
 };
 
 // the default constraint set (h = [hfov, vfov, sdf] at every node, soft) from lh .. Zl (diagnostic drivers)

@@ -249,11 +249,12 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     // where each one held a 64-bit SGPR mask for the whole kernel and the masks spilled to VGPR lanes.
     const int lane_k = lane;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // row sets without hard stage rows (engine.cpp qp_is_seg_set): nh (0..3) soft stage rows at nodes k < N,
-    // group j of a node reading column h_col[j] of h / J_h; nhN terminal rows, the first nsN soft, row j
-    // reading h[N][hN_col[j]] + hE[hE_col[j]] (rti_qp.hip's row set: QpRows with nhs = 0)
-    const int nh = A.nh;
-    const int N = A.N, N1 = N + 1, m = 8 * N + 4 * (nh * N + A.nsN) + 2 * (A.nhN - A.nsN);
+    // the row set (rti_qp.hip's, QpRows): nh (0..3) stage rows at nodes k < N, group j of a node reading column
+    // h_col[j] of h / J_h, the last nhs of them hard (none at node 0); nhN terminal rows, the first nsN soft,
+    // row j reading h[N][hN_col[j]] + hE[hE_col[j]]
+    const int nh = A.nh, nss = nh - A.nhs;
+    const int N = A.N, N1 = N + 1,
+              m = 8 * N + 4 * (nss * N + A.nsN) + 2 * ((N - 1) * A.nhs + A.nhN - A.nsN);
     const SegSmem s = seg_carve<NSEG, NMAX>((ldsd*)lds_q, w);
     ldsd* const win = s.win;                                  // two windows; the coupling's scratch
     const int sa = w * N1 / NSEG, sb = (w + 1) * N1 / NSEG;  // this wave's nodes [sa, sb)
@@ -324,16 +325,17 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         const int src = q < 10 ? R_C + q : q < 24 ? R_G + q - 10 : q < 64 ? 100 + q - 24 : R_CT + q - 64;
         F[(size_t)k * FRECS + S_C + q] = R[(size_t)k * REC + src];
     }
-    // lane-owned rows: box pair (kb, ib) (rows 8 kb + ib, 8 kb + 4 + ib) of this wave's nodes; soft group
-    // (ks, js) of a stage node (lanes 0..47: at most 15 stage nodes x 3); in the last wave lanes 48 + j the
-    // terminal row j: soft (its four rows in ts / ls) or hard (lower, upper in ts[0..1] / ls[0..1])
+    // lane-owned rows: box pair (kb, ib) (rows 8 kb + ib, 8 kb + 4 + ib) of this wave's nodes; group (ks, js)
+    // of a stage node (lanes 0..47: at most 15 stage nodes x 3), soft (its four rows in ts / ls) or hard
+    // (lower, upper in ts[0..1] / ls[0..1]); in the last wave lanes 48 + j the terminal row j, soft or hard
     const bool last = w == NSEG - 1;
     const int jt = lane - 48;
     const bool tlane = last && jt >= 0 && jt < QP_NHN;
     const int kb = sa + (lane >> 2), ib = lane & 3, ks = tlane ? N : sa + lane / 3, js = tlane ? jt : lane % 3;
     const bool ownb = kb < (sb < N ? sb : N);
-    const bool owns = tlane ? jt < A.nsN : ks < (last ? N : sb) && js < nh;
-    const bool ownh = tlane && jt >= A.nsN && jt < A.nhN;
+    const bool stg = !tlane && ks < (last ? N : sb) && js < nh;
+    const bool owns = tlane ? jt < A.nsN : stg && js < nss;
+    const bool ownh = tlane ? jt >= A.nsN && jt < A.nhN : stg && js >= nss && ks > 0;
     const int ci = tlane ? 3 + jt : js;  // the row kind in the constant table
     const int kbc = ownb ? kb : sa, ksc = (owns || ownh) ? ks : sa;
     const double ubv = ownb ? A.u[((size_t)b * N + kbc) * NU + ib] : 0.0;
@@ -1201,7 +1203,7 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
                 rl = fmax(rl, fabs(v[q] - ts[q]));
             }
         }
-        if (ownh) {  // hard terminal row: lower cx + (h - lo), upper -cx + (hi - h) (rti_qp.hip rows_init)
+        if (ownh) {  // hard row: lower cx + (h - lo), upper -cx + (hi - h) (rti_qp.hip rows_init)
             const double cx = s.cxa[ksc * NS + js];
             const double v0 = cx + hl0(), v1 = -cx + hu0();
             ts[0] = fmax(v0, T0);
