@@ -240,7 +240,7 @@ def main():
     lin_gbs = lin_b / (kms["linearize"] * 1e-3) / 1e9  # beside sdf_mlp, as the step runs it
     # linearize alone: a second context with the serial preparation (SDFNMPC_SERIAL_PREP is read at context
     # creation), the same buffers, HIP events around the kernel (untimed diagnostic pass)
-    lin_alone_ms = None
+    lin_alone_ms = lin_events_ms = None
     if rank == 0:
         prev_sp = os.environ.get("SDFNMPC_SERIAL_PREP")
         os.environ["SDFNMPC_SERIAL_PREP"] = "1"
@@ -258,7 +258,21 @@ def main():
             _lib.linearize(ctx_s, net, model, B, N, np_, bufs)
         v = ctx_s.kernel_stats("linearize")
         ctx_s.synchronize()
-        lin_alone_ms = v[0] / v[1] if v[1] else None
+        lin_events_ms = v[0] / v[1] if v[1] else None  # an event pair around each launch (adds its own gap)
+        # the kernel alone: 20 back-to-back launches without the SDF kernels (no_sdf: the sdf row is not
+        # written; linearize's work does not depend on it) between one event pair -- rocprofv3's per-launch
+        # mean is the same figure (profiles/r06/kernel_stats_bench.csv)
+        ctx_s.enable_timing(False)
+        reps = 20
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            _lib.linearize(ctx_s, None, model, B, N, np_, bufs, no_sdf=True)
+        e1.record()
+        e1.synchronize()
+        lin_alone_ms = e0.elapsed_time(e1) / reps
+        _lib.linearize(ctx_s, net, model, B, N, np_, bufs)  # the sdf rows back for the steps after
+        ctx_s.synchronize()
         del ctx_s
     qp_flop = float(it.sum()) * (N + 1) * QP_FLOP_PER_NODE_ITER
     qp_tf = qp_flop / (kms["rti_qp"] * 1e-3) / 1e12
@@ -406,7 +420,9 @@ def main():
                                "note": "achieved over the kernel's duration beside sdf_mlp (the step's schedule)",
                                "alone": None if lin_alone_ms is None else {
                                    "ms": lin_alone_ms, "achieved": lin_b / (lin_alone_ms * 1e-3) / 1e9,
-                                   "frac": lin_b / (lin_alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS}},
+                                   "frac": lin_b / (lin_alone_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                   "timing": "20 back-to-back launches between one event pair",
+                                   "ms_event_pair_per_launch": lin_events_ms}},
         "cpu_baseline": cpu,
         "prep": prep_out,
         "c2": c2,

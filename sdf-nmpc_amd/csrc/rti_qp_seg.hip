@@ -295,16 +295,22 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         }
         s.cst[tid] = v;
     }
-    // terminal rows j < nhN: C row j = J_h[N] column hN_col[j] + J_hE column hE_col[j] (rti_qp.hip's)
-    for (int e = tid; e < A.nhN * 10; e += 64 * NSEG) {
-        const int j = e / 10, l = e - 10 * j;
+    // terminal rows j < nhN: C row j = J_h[N] column hN_col[j] + J_hE column hE_col[j] (rti_qp.hip's); rows
+    // nhN .. QP_NHN - 1 zero, so the terminal stages run over all QP_NHN rows without a count (their folds
+    // stay zero: no lane owns them)
+    if (tid < 10 * QP_NHN) {
+        const int e = tid, j = e / 10, l = e - 10 * j;
+        const double* jr = A.Jh + ((size_t)b * N1 + N) * 30 + l * 3;
+        const double j0 = jr[0], j1 = jr[1], j2 = jr[2];  // in flight while the columns are looked up
         int c1 = -1, c2 = -1;
 #pragma unroll
         for (int q = 0; q < QP_NHN; ++q)
             if (q == j) { c1 = A.hN_col[q]; c2 = A.hE_col[q]; }
         double cv = 0.0;
-        if (c1 >= 0) cv += A.Jh[((size_t)b * N1 + N) * 30 + l * 3 + c1];
-        if (c2 >= 0) cv += A.JhE[((size_t)b * 10 + l) * 6 + c2];
+        if (j < A.nhN) {
+            if (c1 >= 0) cv += c1 == 0 ? j0 : c1 == 1 ? j1 : j2;
+            if (c2 >= 0) cv += A.JhE[((size_t)b * 10 + l) * 6 + c2];  // rec_feas / stability rows only
+        }
         s.ctn[e] = cv;
     }
     if (tid < 48) s.zero[tid] = 0.0;
@@ -463,12 +469,14 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
     // ------------------------------------------------------------ forward stage
     // lane r < 10: x_{k+1}[r]; 10..13: u_k; 14..16: (C x_k)_{r-14}.  K == 0: the initial iterate
     // (rows of A x + c from the stage record).  LAM: the costate term -[B G; G] lam_b of segments 0..2.
-    auto fw_stage = [&](auto Kc, auto LAMc, int k, bool seg_end, const ldsd* cw, auto refill) {
+    // TERM: the terminal node (its rows' C from ctn, lanes 14 .. 13 + QP_NHN), a separate instantiation so the
+    // other stages keep their lane constants
+    auto fw_stage = [&](auto Kc, auto LAMc, auto TERMc, int k, bool seg_end, const ldsd* cw, auto refill) {
         const int lane = opaque(lane_k);
         constexpr int K = decltype(Kc)::value;
         constexpr bool LAM = decltype(LAMc)::value;
-        const bool term = k == N;  // the terminal node: its nhN rows' C from ctn (lanes 14 .. 13 + nhN)
-        const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < 14 + (term ? A.nhN : NS);
+        constexpr bool term = decltype(TERMc)::value;
+        const bool fx = lane < NX, fu = lane >= NX && lane < 14, fc = lane >= 14 && lane < (term ? 14 + QP_NHN : 14 + NS);
         const int fcj = fc ? lane - 14 : 0;
         ldsd* const duo = K == 4 ? s.duc : s.dua;
         ldsd* const cxo = K == 4 ? s.cxc : s.cxa;
@@ -550,15 +558,14 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
                 const int a_ = g + 4 * r, lo = a_ < c ? a_ : c, hi = a_ < c ? c : a_;
                 T[r] = cw[(a_ < NX && c < NX) ? R_H + tri10(lo, hi) : (a_ < NX && c == 14) ? R_G + a_ : R_Z];
             }
-            const int nhN = A.nhN;
-            auto tfold = [&](int j, d4 acc) {  // rows j = g (+ 4): lane (g, c) holds C[j][c] and w_j C[j][c] + [c = 14] gamma_j
-                const bool live = j < nhN;
-                const double ct = ldsel(s.ctn, 10 * (live ? j : 0) + (c < NX ? c : 0), live && c < NX);
-                const double fj = live ? fma(s.fw[N * NS + j], ct, m14 * s.fg[N * NS + j]) : 0.0;
-                return mfma(ct, fj, acc);
+            // rows j = g and g + 4 (rows past nhN are zero rows with zero folds): lane (g, c) holds C[j][c] and
+            // w_j C[j][c] + [c = 14] gamma_j
+            auto tfold = [&](int j, d4 acc) {
+                const double ct = ldsel(s.ctn, 10 * j + (c < NX ? c : 0), c < NX);
+                return mfma(ct, fma(s.fw[N * NS + j], ct, m14 * s.fg[N * NS + j]), acc);
             };
             Pa = tfold(g, T);
-            if (nhN > 4) Pa = tfold(g + 4, Pa);
+            Pa = tfold(g + 4, Pa);
             refill();
             return;
         }
@@ -711,11 +718,11 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         const int bx = fx ? lane : 0;
         // ---- the chain's offset: g~_x + K^T g~_u (lanes 0..9), g~_u (lanes 10..13)
         double off = *(lane < 14 ? cw + S_GV + lane : s.zero);
-        if constexpr (FIRST) {  // the terminal rows' C from ctn
+        if constexpr (FIRST) {  // the terminal rows' C from ctn (rows past nhN: zero rows, zero gamma)
 #pragma unroll
             for (int j = 0; j < QP_NHN; ++j) {
-                const bool live = fx && j < A.nhN;
-                off += live ? s.fg[N * NS + j] * s.ctn[10 * j + bx] : 0.0;
+                const double t = s.fg[N * NS + j] * s.ctn[10 * j + bx];
+                off += fx ? t : 0.0;
             }
         } else {
             const ldsd* bc_ct = fx ? cw + S_CT + lane : s.zero;
@@ -1166,16 +1173,24 @@ __global__ __launch_bounds__(64 * NSEG, NSEG == 4 ? 2 : NSEG) void rti_qp_seg_ke
         SSTAMP(decltype(Kc)::value == 2 ? 4 : 9);
         SSTAMP_PHASE(decltype(Kc)::value == 2 ? 12 : 14);
         if (aug) {
-            sweep(Kc, nn, node_fw, [&](int q, int k, const ldsd* cw, auto rf) { fw_stage(Kc, IC<1>{}, k, k == sb - 1, cw, rf); (void)q; });
+            sweep(Kc, nn, node_fw, [&](int q, int k, const ldsd* cw, auto rf) { fw_stage(Kc, IC<1>{}, IC<0>{}, k, k == sb - 1, cw, rf); (void)q; });
         } else {
-            sweep(Kc, nn, node_fw, [&](int q, int k, const ldsd* cw, auto rf) { fw_stage(Kc, IC<0>{}, k, false, cw, rf); (void)q; });
+            sweep(Kc, nn, node_fw, [&](int q, int k, const ldsd* cw, auto rf) {
+                if (k == N) fw_stage(Kc, IC<0>{}, IC<1>{}, k, false, cw, rf);
+                else fw_stage(Kc, IC<0>{}, IC<0>{}, k, false, cw, rf);
+                (void)q;
+            });
         }
     };
 
     // ------------------------------------------------------------ initial iterate (wave 0, all nodes)
 #ifndef SEGX_NO_INIT
     if (w == 0)
-        sweep(IC<0>{}, N1, node_fw, [&](int q, int k, const ldsd* cw, auto rf) { fw_stage(IC<0>{}, IC<0>{}, k, false, cw, rf); (void)q; });
+        sweep(IC<0>{}, N1, node_fw, [&](int q, int k, const ldsd* cw, auto rf) {
+            if (k == N) fw_stage(IC<0>{}, IC<0>{}, IC<1>{}, k, false, cw, rf);
+            else fw_stage(IC<0>{}, IC<0>{}, IC<0>{}, k, false, cw, rf);
+            (void)q;
+        });
 #endif
     wg_sync();
     for (int e = lane; e < nn * NX; e += 64) A.dx[((size_t)b * N1 + sa) * NX + e] = s.dxc[sa * NX + e];
