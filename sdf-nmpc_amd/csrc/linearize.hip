@@ -135,7 +135,7 @@ __global__ __launch_bounds__(256, LIN_WAVES) void linearize_kernel(LinArgs A) {
         const int t = sl < 4 ? 3 + sl : 6 + sl;  // the tangent direction of this lane: q0..q3, u0..u3
         dd X[10];
 #pragma unroll
-        for (int i = 0; i < 10; ++i) X[i] = {xv[i], (i == t) ? 1.0 : 0.0};
+        for (int i = 0; i < 10; ++i) X[i] = {xv[i], (i >= 3 && i < 7 && i == t) ? 1.0 : 0.0};  // t: q0..q3 or u
         const long long s = b * N + k;
         const double* ur = A.u + s * 4;
         dd U[4];
