@@ -785,7 +785,9 @@ def c5_leg(local, dev, world, rank, B, N, steps, warm, no_cpu, global_batch=0):
                      "traffic": None, "flop_per_step": conv_flop, "fp32_equivalent_tflops": conv_tf,
                      "fp32_equivalent_frac_of_f32_mfma_peak": conv_tf / FP32_MFMA_PEAK_TFLOPS},
         "roofline_wide_sdf": {"bound": "mfma", "kernel": "sdf_wide_gemm (9 launches)", "achieved": wide_tf,
-                              "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": wide_tf / FP32_MFMA_PEAK_TFLOPS},
+                              "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": wide_tf / FP32_MFMA_PEAK_TFLOPS,
+                              "note": "fp32 GEMM FLOPs over the f32 MFMA peak; the products run fp32-exact as three-way "
+                                      "bf16 splits on the bf16 pipe (sdf_wide.hip SPLIT; SDFNMPC_WIDE_F32=1: f32 MFMA)"},
         "vae_ms": vae_ms, "wide_sdf_ms": wide_ms,
         "cpu_baseline": None,
     }

@@ -21,21 +21,55 @@
 // the 8 XCDs each keep one row tile while the weight columns stream through their L2.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+#include <type_traits>
+
 #include "sdf_kernels.h"
 #include "sincos.h"
 
 namespace sdfn {
 
 typedef float wf32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 wbf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int WG_BM = 128, WG_BN = 128, WG_BK = 16, WG_LD = 20, WG_GROUP = 8;
 
 #ifndef WIDE_WGS
 #define WIDE_WGS 4  // 119 VGPRs, 40 KB LDS: four 256-thread workgroups per CU (three: 2.88 vs 2.59 ms at C5)
 #endif
-template <int EPI>
-__global__ __launch_bounds__(256, WIDE_WGS) void wide_gemm_kernel(WideGemmArgs a) {
-    __shared__ float smem[2 * (WG_BM + WG_BN) * WG_LD];
+// fp32 products on the bf16 matrix pipe (SPLIT, round 6; vae_enc.hip's scheme): each fp32 operand is split
+// exactly into three bf16 x = hi + mid + lo (round-to-nearest of the remainders) as it is staged into LDS (three
+// planes per operand, 32-byte rows with the halves of rows 8..15 of every 16 swapped: conflict-free
+// ds_read_b128), and a 32 x 32 block takes six v_mfma_f32_32x32x16_bf16 per K-tile of 16 -- al.bh, ah.bl,
+// am.bm, am.bh, ah.bm, ah.bh, smallest first, accumulated in fp32; the dropped products (am.bl, al.bm,
+// al.bl) are <= 2^-27 relative, under the fp32 rounding level.  6 x 32 matrix-pipe cycles per block and K-tile
+// against 8 x 64 for v_mfma_f32_32x32x2_f32.  48 KB of LDS: three workgroups per CU.
+// Two values at a time, each rounded to nearest bf16 (v_cvt_pk_bf16_f32, the first value in the low half):
+// x = hi + mid + lo exactly (the remainders of a round-to-nearest are exact fp32 and keep <= 16, then <= 8
+// significant bits), and each remainder is at most half a bf16 ulp of the one before, so the three dropped
+// products are <= 2^-27 relative (2^-24 with truncation, vae_enc.hip's split: too coarse for the deep
+// ReLU variants' scale-free bar)
+typedef __bf16 wbf16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ unsigned wpk(float a, float b) {
+    const wbf16x2 t = {(__bf16)a, (__bf16)b};
+    return __builtin_bit_cast(unsigned, t);
+}
+__device__ __forceinline__ void wsplit2(float a, float b, unsigned& h, unsigned& m, unsigned& l) {
+    h = wpk(a, b);
+    const float ra = a - __uint_as_float(h << 16), rb = b - __uint_as_float(h & 0xffff0000u);
+    m = wpk(ra, rb);
+    const float sa = ra - __uint_as_float(m << 16), sb = rb - __uint_as_float(m & 0xffff0000u);
+    l = wpk(sa, sb);
+}
+__device__ __forceinline__ int wsw(int row, int half) { return row * 16 + 8 * (half ^ ((row >> 3) & 1)); }
+constexpr int WS_PLANE = WG_BM * 16;  // bf16 per plane and operand (WG_BM == WG_BN)
+constexpr int WS_LDS_FLOATS = 2 * 6 * WS_PLANE / 2;
+static_assert(WG_BM == WG_BN && WS_LDS_FLOATS >= 4 * 64 * 33, "split staging / epilogue LDS");
+
+template <int EPI, bool SPLIT>
+__global__ __launch_bounds__(256, SPLIT ? 3 : WIDE_WGS) void wide_gemm_kernel(WideGemmArgs a) {
+    constexpr int SMEM = SPLIT ? WS_LDS_FLOATS : 2 * (WG_BM + WG_BN) * WG_LD;
+    __shared__ __align__(16) float smem[SMEM];
     float(*As)[WG_BM * WG_LD] = (float(*)[WG_BM * WG_LD])smem;
     float(*Bs)[WG_BN * WG_LD] = (float(*)[WG_BN * WG_LD])(smem + 2 * WG_BM * WG_LD);
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -69,12 +103,30 @@ __global__ __launch_bounds__(256, WIDE_WGS) void wide_gemm_kernel(WideGemmArgs a
         rb0 = *(const float4*)(pb0 + (size_t)(kt) * WG_BK);                                             \
         rb1 = *(const float4*)(pb1 + (size_t)(kt) * WG_BK);                                             \
     } while (0)
-#define WIDE_STASH(buf)                           \
-    do {                                          \
-        *(float4*)(&As[buf][srow0]) = ra0;        \
-        *(float4*)(&As[buf][srow1]) = ra1;        \
-        *(float4*)(&Bs[buf][srow0]) = rb0;        \
-        *(float4*)(&Bs[buf][srow1]) = rb1;        \
+    unsigned short* const L16 = (unsigned short*)smem;  // SPLIT: [buf][A hi, mid, lo, B hi, mid, lo][row * 16]
+    // SPLIT: a float4 (4 k of one row) into the three planes of operand `op` of buffer `buf`, row `row`
+    auto split_stash = [&](int buf, int op, int row, float4 v) {
+        unsigned h0, m0, l0, h1, m1, l1;
+        wsplit2(v.x, v.y, h0, m0, l0);
+        wsplit2(v.z, v.w, h1, m1, l1);
+        unsigned short* base = L16 + (size_t)(buf * 6 + 3 * op) * WS_PLANE + wsw(row, kq >> 1) + 4 * (kq & 1);
+        *(uint2*)base = make_uint2(h0, h1);
+        *(uint2*)(base + WS_PLANE) = make_uint2(m0, m1);
+        *(uint2*)(base + 2 * WS_PLANE) = make_uint2(l0, l1);
+    };
+#define WIDE_STASH(buf)                                    \
+    do {                                                   \
+        if constexpr (SPLIT) {                             \
+            split_stash(buf, 0, tid >> 2, ra0);            \
+            split_stash(buf, 0, (tid >> 2) + 64, ra1);     \
+            split_stash(buf, 1, tid >> 2, rb0);            \
+            split_stash(buf, 1, (tid >> 2) + 64, rb1);     \
+        } else {                                           \
+            *(float4*)(&As[buf][srow0]) = ra0;             \
+            *(float4*)(&As[buf][srow1]) = ra1;             \
+            *(float4*)(&Bs[buf][srow0]) = rb0;             \
+            *(float4*)(&Bs[buf][srow1]) = rb1;             \
+        }                                                  \
     } while (0)
 
     wf32x16 acc[2][2];
@@ -91,6 +143,34 @@ __global__ __launch_bounds__(256, WIDE_WGS) void wide_gemm_kernel(WideGemmArgs a
     for (int kt = 0; kt < KT; ++kt) {
         const int buf = kt & 1;
         if (kt + 1 < KT) WIDE_LOAD(kt + 1);
+        if constexpr (SPLIT) {
+            const unsigned short* pa_ = L16 + (size_t)(buf * 6) * WS_PLANE;
+            const unsigned short* pb_ = pa_ + 3 * WS_PLANE;
+            wbf16x8 ah[2], am[2], al[2], bh[2], bm[2], bl[2];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) {
+                const int oa = wsw(wm * 64 + 32 * i + lr, lh), ob = wsw(wn * 64 + 32 * i + lr, lh);
+                ah[i] = *(const wbf16x8*)(pa_ + oa);
+                am[i] = *(const wbf16x8*)(pa_ + WS_PLANE + oa);
+                al[i] = *(const wbf16x8*)(pa_ + 2 * WS_PLANE + oa);
+                bh[i] = *(const wbf16x8*)(pb_ + ob);
+                bm[i] = *(const wbf16x8*)(pb_ + WS_PLANE + ob);
+                bl[i] = *(const wbf16x8*)(pb_ + 2 * WS_PLANE + ob);
+            }
+#define WIDE_MM(X, Y)                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < 2; ++i) _Pragma("unroll") for (int j = 0; j < 2; ++j)         \
+        acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(X[i], Y[j], acc[i][j], 0, 0, 0);
+            WIDE_MM(al, bh)
+            WIDE_MM(ah, bl)
+            WIDE_MM(am, bm)
+            WIDE_MM(am, bh)
+            WIDE_MM(ah, bm)
+            WIDE_MM(ah, bh)
+#undef WIDE_MM
+            if (kt + 1 < KT) WIDE_STASH(buf ^ 1);
+            __syncthreads();
+            continue;
+        }
         float av[2][8], bv[2][8];
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -174,11 +254,21 @@ hipError_t launch_wide_gemm(const WideGemmArgs& a, int epi, hipStream_t s) {
         return hipErrorInvalidValue;
     const long long MT = (a.M + WG_BM - 1) / WG_BM, grid = MT * (a.N / WG_BN);
     if (grid > 0x7fffffffLL) return hipErrorInvalidValue;
+    // SDFNMPC_WIDE_F32=1: the exact-fp32 MFMA main loop (comparison builds of the same library)
+    static const bool f32 = [] { const char* e = getenv("SDFNMPC_WIDE_F32"); return e && *e == '1'; }();
+    auto go = [&](auto ec, auto sc) {
+        hipLaunchKernelGGL((wide_gemm_kernel<decltype(ec)::value, decltype(sc)::value>), dim3((unsigned)grid), dim3(256),
+                           0, s, a);
+    };
+    auto by_split = [&](auto ec) {
+        if (f32) go(ec, std::false_type{});
+        else go(ec, std::true_type{});
+    };
     switch (epi) {
-        case WIDE_EPI_SIN: hipLaunchKernelGGL((wide_gemm_kernel<WIDE_EPI_SIN>), dim3((unsigned)grid), dim3(256), 0, s, a); break;
-        case WIDE_EPI_SIN_L4: hipLaunchKernelGGL((wide_gemm_kernel<WIDE_EPI_SIN_L4>), dim3((unsigned)grid), dim3(256), 0, s, a); break;
-        case WIDE_EPI_BWD: hipLaunchKernelGGL((wide_gemm_kernel<WIDE_EPI_BWD>), dim3((unsigned)grid), dim3(256), 0, s, a); break;
-        case WIDE_EPI_STORE: hipLaunchKernelGGL((wide_gemm_kernel<WIDE_EPI_STORE>), dim3((unsigned)grid), dim3(256), 0, s, a); break;
+        case WIDE_EPI_SIN: by_split(std::integral_constant<int, WIDE_EPI_SIN>{}); break;
+        case WIDE_EPI_SIN_L4: by_split(std::integral_constant<int, WIDE_EPI_SIN_L4>{}); break;
+        case WIDE_EPI_BWD: by_split(std::integral_constant<int, WIDE_EPI_BWD>{}); break;
+        case WIDE_EPI_STORE: by_split(std::integral_constant<int, WIDE_EPI_STORE>{}); break;
         default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
