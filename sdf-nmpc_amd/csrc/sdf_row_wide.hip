@@ -10,10 +10,11 @@
 // contiguous, so a GEMV gives each output row a group of 16 lanes (one DPP row): lane q loads the row's
 // float4 chunks q, q + 16, ... (each load instruction of a group contiguous), and a DPP group sum
 // reduces them; 32 rows per pass of the workgroup, eight passes x four chunks per lane unrolled so a
-// 256 x 256 layer's loads are all in flight at once (at one row a layer is a chain of L2 / MALL round trips,
-// as sdf_row.hip explains).  The backward pass uses the transposed copies the wide schedule keeps (B4, B3h, B3e, B2, B1e,
-// Bz), so it is the same GEMV.  Activations (sin(w0 .), ReLU, Softplus with threshold 20) and their
-// torch backward forms are wide_gemm_kernel's epilogues element for element.
+// 256 x 256 layer's loads are all in flight at once (at one row a layer is a chain of L2 / MALL round
+// trips, as sdf_row.hip explains).  The backward pass uses the transposed copies the wide schedule keeps
+// (B4, B3h, B3e, B2, B1e, Bz), so it is the same GEMV.  Each GEMV's epilogue runs on lanes 0..7 of every
+// group (its eight rows of the batch at once): the activation (sin(w0 .), ReLU, Softplus with threshold
+// 20) and its torch backward factor, wide_gemm_kernel's epilogues element for element.
 #include <hip/hip_runtime.h>
 
 #include <atomic>
