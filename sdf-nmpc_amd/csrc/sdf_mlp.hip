@@ -168,11 +168,18 @@ __device__ __forceinline__ void act_fwd(f32x16 (&acc)[RB][NCB], f32x16 (&d)[RB][
 #pragma unroll
         for (int c = 0; c < NCB; ++c)
 #pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                float s, co;
-                act_sincos(w0 * acc[rb][c][i], &s, &co);
-                d[rb][c][i] = co;
-                out[(rb * 32 + acc_row(i, h)) * stride + (cb0 + 4 * c) * 32 + col] = s;
+            for (int i = 0; i < 16; i += 2) {
+                float s0, c0, s1, c1;
+#ifdef SDF_CHEAP_SIN
+                act_sincos(w0 * acc[rb][c][i], &s0, &c0);
+                act_sincos(w0 * acc[rb][c][i + 1], &s1, &c1);
+#else
+                sdfn_sincosf2(w0 * acc[rb][c][i], w0 * acc[rb][c][i + 1], &s0, &c0, &s1, &c1);  // packed fp32 pipe
+#endif
+                d[rb][c][i] = c0;
+                d[rb][c][i + 1] = c1;
+                out[(rb * 32 + acc_row(i, h)) * stride + (cb0 + 4 * c) * 32 + col] = s0;
+                out[(rb * 32 + acc_row(i + 1, h)) * stride + (cb0 + 4 * c) * 32 + col] = s1;
             }
 }
 
@@ -186,8 +193,12 @@ __device__ __forceinline__ void act_bwd(const f32x16 (&acc)[RB][NCB], const f32x
 #pragma unroll
         for (int c = 0; c < NCB; ++c)
 #pragma unroll
-            for (int i = 0; i < 16; ++i)
-                out[(rb * 32 + acc_row(i, h)) * stride + (cb0 + 4 * c) * 32 + col] = (acc[rb][c][i] * d[rb][c][i]) * w0;
+            for (int i = 0; i < 16; i += 2) {  // two elements per packed multiply (the same products)
+                const sdfn_f2 a2 = {acc[rb][c][i], acc[rb][c][i + 1]}, d2 = {d[rb][c][i], d[rb][c][i + 1]};
+                const sdfn_f2 v = (a2 * d2) * w0;
+                out[(rb * 32 + acc_row(i, h)) * stride + (cb0 + 4 * c) * 32 + col] = v.x;
+                out[(rb * 32 + acc_row(i + 1, h)) * stride + (cb0 + 4 * c) * 32 + col] = v.y;
+            }
 }
 
 // ------------------------------------------------------------------------------------------------

@@ -48,3 +48,49 @@ SDFN_HD void sdfn_sincosf(float x, float* s_out, float* c_out) {
     *s_out = (qi & 2) ? -s1 : s1;
     *c_out = ((qi + 1) & 2) ? -c1 : c1;
 }
+
+#if defined(__HIPCC__)
+// Two arguments at once on the packed fp32 pipe (v_pk_fma_f32 / v_pk_mul_f32): the same operations as
+// sdfn_sincosf element by element (IEEE fma and products per element), so the same bits.
+typedef float sdfn_f2 __attribute__((ext_vector_type(2)));
+// the large-argument path out of line (it is never taken by a sane network; inlined at every pair it
+// doubled the epilogues' code)
+static __device__ __attribute__((noinline)) float4 sdfn_sincosf2_slow(float x0, float x1) {
+    float4 r;
+    sdfn_sincosf(x0, &r.x, &r.y);
+    sdfn_sincosf(x1, &r.z, &r.w);
+    return r;
+}
+__device__ __forceinline__ void sdfn_sincosf2(float x0, float x1, float* s0, float* c0, float* s1, float* c1) {
+#ifndef SDF_FAST_SIN_ONLY
+    if (!(fabsf(x0) < 131072.0f) || !(fabsf(x1) < 131072.0f)) {
+        const float4 r = sdfn_sincosf2_slow(x0, x1);
+        *s0 = r.x;
+        *c0 = r.y;
+        *s1 = r.z;
+        *c1 = r.w;
+        return;
+    }
+#endif
+    const sdfn_f2 x = {x0, x1};
+    const sdfn_f2 t = x * 0.636619772367581343f;
+    const sdfn_f2 q = {rintf(t.x), rintf(t.y)};
+    sdfn_f2 r = __builtin_elementwise_fma(q, (sdfn_f2)(-1.57079637050628662109375f), x);
+    r = __builtin_elementwise_fma(q, (sdfn_f2)(4.37113882867379289e-8f), r);
+    r = __builtin_elementwise_fma(q, (sdfn_f2)(1.71512451e-15f), r);
+    const sdfn_f2 r2 = r * r;
+    sdfn_f2 ps = __builtin_elementwise_fma(r2, (sdfn_f2)(-1.9515295891e-4f), (sdfn_f2)(8.3321608736e-3f));
+    ps = __builtin_elementwise_fma(r2, ps, (sdfn_f2)(-1.6666654611e-1f));
+    const sdfn_f2 sr = __builtin_elementwise_fma(r * r2, ps, r);
+    sdfn_f2 pc = __builtin_elementwise_fma(r2, (sdfn_f2)(2.443315711809948e-5f), (sdfn_f2)(-1.388731625493765e-3f));
+    pc = __builtin_elementwise_fma(r2, pc, (sdfn_f2)(4.166664568298827e-2f));
+    const sdfn_f2 cr = __builtin_elementwise_fma(r2 * r2, pc, __builtin_elementwise_fma(r2, (sdfn_f2)(-0.5f), (sdfn_f2)(1.0f)));
+    const int q0 = (int)q.x, q1 = (int)q.y;
+    const float sa = (q0 & 1) ? cr.x : sr.x, ca = (q0 & 1) ? sr.x : cr.x;
+    const float sb = (q1 & 1) ? cr.y : sr.y, cb = (q1 & 1) ? sr.y : cr.y;
+    *s0 = (q0 & 2) ? -sa : sa;
+    *c0 = ((q0 + 1) & 2) ? -ca : ca;
+    *s1 = (q1 & 2) ? -sb : sb;
+    *c1 = ((q1 + 1) & 2) ? -cb : cb;
+}
+#endif
